@@ -1,0 +1,189 @@
+#!/usr/bin/env python
+"""Benchmark: EE-GAN data-parallel G+D training step on MI355X.
+
+Metric (BASELINE.json): train images/sec at 256x256 CUB, full 3-stage G+D
+step (text encode x5 -> ATTR_Enhance -> G -> d_update x3 (hinge + class +
+MA gradient penalty, 2 Adam steps per D) -> g_update (3 D's + Inception-v3
+DAMSM words/sent losses, 1 Adam step)).  Workload C2: CUB GF=DF=32, batch 16
+per GPU, bf16 activations / fp32 master weights, synthetic data, random
+initialised weights (no datasets/checkpoints offline).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+Prints ONE JSON line on rank 0 (see the repo README / task contract), with a
+`roofline` object for the dominant kernel family (conv forward implicit GEMM,
+bf16 MFMA) measured with HIP events over the timed region, and a
+`cpu_baseline` object: the CPU oracle (oracle/, a PyTorch-CPU restatement of
+the reference step) timed on the host on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'ee-gan_amd'))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+CONFIGS = {
+    # name: (dataset, GF=DF, per-GPU batch, class_num (0 = no class head))
+    'C2': ('CUB-200', 32, 16, 200),
+    'C3': ('Oxford-102', 48, 32, 102),
+    'C4': ('MS-COCO', 64, 8, 0),
+    'C5': ('CUB-200', 32, 32, 200),
+}
+MFMA_PEAK_TFLOPS = 2500.0   # dense bf16 (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+
+def build(cfg_name, device):
+    import models
+    import DAMSM
+    from sync_batchnorm import DataParallelWithCallback
+    from eegan_hip.trainer import Trainer
+    _, W, B, ncls = CONFIGS[cfg_name]
+    torch.manual_seed(3407)
+    G = DataParallelWithCallback(models.Gen(W, 100).to(device))
+    A = DataParallelWithCallback(models.ATTR_Enhance().to(device))
+    disc_class = ncls > 0
+    Ds = [DataParallelWithCallback(models.Dis64(W).to(device)), DataParallelWithCallback(models.Dis128(W).to(device)),
+          DataParallelWithCallback(models.Dis256(W, disc_class, max(ncls, 1)).to(device))]
+    # zero-initialised gammas/heads of the reference would make most branches
+    # dead at step 0; use small non-zero values so every kernel does its work
+    with torch.no_grad():
+        for m in [G, A] + Ds:
+            for n, p in m.named_parameters():
+                if n.endswith('gamma'):
+                    p.fill_(0.5)
+                elif 'linear2' in n:
+                    p.normal_(0, 0.02)
+    enc_img = DAMSM.CNN_ENCODER(256).to(device).eval()
+    enc_txt = DAMSM.RNN_ENCODER(5450, nhidden=256).to(device).eval()
+    for p in enc_txt.parameters():
+        p.requires_grad = False
+    T = Trainer(G, A, Ds, enc_img, enc_txt, B, disc_class=disc_class, class_nums=max(ncls, 1), class_coe=10.0,
+                sim_coe=0.05, device=device)
+    return T, B, ncls
+
+
+def cpu_baseline(seconds_budget=20.0):
+    """Time the CPU oracle's full step (oracle.eegan_oracle.train_step incl.
+    the Inception-v3 encoder restatement) at B=4, W=32 (BASELINE.md CPU plan)."""
+    from oracle import eegan_oracle as O
+    from oracle.seeding import seeded_state, synthetic_batch, seeded_tensor
+    import models
+    import DAMSM
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    B, W, ncls = 4, 32, 200
+    spec = lambda m: [(k, tuple(v.shape)) for k, v in m.state_dict().items()]  # noqa: E731
+    sd_g = seeded_state(spec(models.Gen(W, 100)), 1)
+    sd_a = seeded_state(spec(models.ATTR_Enhance()), 2)
+    sd_ds = [seeded_state(spec(m), 3 + i) for i, m in enumerate([models.Dis64(W), models.Dis128(W),
+                                                                  models.Dis256(W, True, ncls)])]
+    sd_e = seeded_state(spec(DAMSM.CNN_ENCODER(256)), 9)
+    nets = O.OracleNets(sd_g, sd_a, sd_ds, W, W, True, ncls)
+    og, ods = O.make_adams(nets)
+    batch = synthetic_batch(B, seed=5, class_num=ncls)
+    emb = (seeded_tensor('w', (B, 256, 18)), seeded_tensor('s', (B, 256)), seeded_tensor('a', (B, 3, 256)),
+           seeded_tensor('u', (B, 256)))
+    enc = lambda x: O.cnn_encoder(sd_e, x)  # noqa: E731
+    O.train_step(nets, og, ods, batch, emb, enc)  # warm-up
+    times = []
+    t_end = time.time() + seconds_budget
+    while time.time() < t_end or len(times) < 2:
+        t0 = time.time()
+        O.train_step(nets, og, ods, batch, emb, enc)
+        times.append(time.time() - t0)
+        if len(times) >= 10:
+            break
+    times.sort()
+    med = times[len(times) // 2]
+    return {'value': B / med, 'unit': 'images/sec', 'cores': threads, 'kind': 'port',
+            'sample': 'oracle train_step (full 3-stage, W=32, B=4, Inception-v3 restatement), median of %d steps '
+                      'after 1 warm-up, %d threads' % (len(times), threads)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--config', default='C2', choices=sorted(CONFIGS))
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-seconds', type=float, default=20.0)
+    args = ap.parse_args()
+
+    from eegan_hip import dist as D
+    from eegan_hip import functional as Fn
+    from eegan_hip.synthetic import make_batch
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local_rank)
+    device = torch.device('cuda', local_rank)
+    rank, world = D.init_from_env()
+    T, B, ncls = build(args.config, device)
+    batch = make_batch(B, device, seed=3407 + rank, class_num=max(ncls, 1), with_class=True)
+
+    def step():
+        T.train_step(batch)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    Fn.TIMER = Fn.LaunchTimer()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    timer, Fn.TIMER = Fn.TIMER, None
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = t.item()
+    kern = timer.summary()
+    ms = dt / args.steps * 1e3
+    value = B * world * args.steps / dt
+    # dominant kernel family by time
+    dom = max(kern.items(), key=lambda kv: kv[1][3])
+    kind, (n, fl, nb, tsec) = dom
+    achieved = fl / tsec / 1e12
+    roof = {'kernel': kind, 'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': MFMA_PEAK_TFLOPS,
+            'unit': 'TFLOP/s', 'frac': round(achieved / MFMA_PEAK_TFLOPS, 4), 'traffic': None,
+            'launches_per_step': n // args.steps, 'avg_launch_us': round(tsec / n * 1e6, 2),
+            'algorithmic_hbm_GBs': round(nb / tsec / 1e9, 1),
+            'families': {k: {'ms_per_step': round(v[3] / args.steps * 1e3, 3),
+                             'TFLOPs': round(v[1] / max(v[3], 1e-12) / 1e12, 1)} for k, v in kern.items()}}
+    out = {'metric': 'train images/sec at 256x256 CUB, G+D step', 'value': round(value, 3), 'unit': 'images/sec',
+           'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
+           'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16',
+           'data': 'synthetic (U(-1,1) images, random captions/attributes/class ids), random-init weights',
+           'config': {'workload': '%s full 3-stage 64->128->256 G+D step, GF=DF=%d, batch %d/GPU%s' % (
+               CONFIGS[args.config][0], CONFIGS[args.config][1], B, ', class head %d' % ncls if ncls else ''),
+               'model': 'EE-GAN Gen+ATTR_Enhance+Dis64/128/256+DAMSM(Inception-v3, biLSTM)',
+               'global_batch': B * world, 'seq_len': 20, 'parallelism': 'dp%d' % world},
+           'roofline': roof}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out['cpu_baseline'] = cpu_baseline(args.cpu_seconds)
+        except Exception as e:  # baseline is reported, never fatal for the GPU measurement
+            out['cpu_baseline'] = {'error': repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,649 @@
+// Loss-side kernels: DAMSM words/sent losses (fused over all B^2 pairs),
+// cross-entropy over the similarity matrices, hinge/mean reductions of the
+// discriminator outputs, BCE-with-logits, the MA gradient penalty, class
+// one-hot labels and the ATTR_Enhance 4x4 self-attention core.
+//
+// replaces: miscc/DAMSM_losses.py:17-63 (cosine_similarity, func_attention),
+// 233-342 (sent_loss, words_loss); train.py:99-103 (prepare_class_labels),
+// 336-417 (d_loss / d_loss_class / MA_gradient_penalty tail / g_loss[_class]);
+// models.py:155-180 (ATTR_Enhance softmax(QK^T)/sqrt(d) V, attr_merge).
+#include "common.h"
+#include "../../include/eegan_hip.h"
+
+namespace {
+
+constexpr float GAMMA1 = 5.f, GAMMA2 = 5.f, GAMMA3 = 10.f;
+constexpr int NR = 289;   // 17 x 17 regions
+constexpr int ND = 256;   // embedding dim
+constexpr int TMAX = 20;  // max words per caption (cfg.TEXT.WORDS_NUM)
+
+// ----------------------------------------------------------- words loss --
+// One workgroup per (text i, image j) pair.  Regions are fp32 NHWC
+// [B][NR][ND]; words fp32 [B][ND][T] (the RNN_ENCODER layout), T <= 20
+// (cfg.TEXT.WORDS_NUM, miscc/config.py:66).
+struct WordsArgs {
+  const float* reg;     // [B][NR][ND]
+  const float* words;   // [B][ND][T]
+  const long* lens;     // [B]
+  int B, T;
+  float* sim;           // fwd: [B(img j)][B(txt i)] * gamma3 (unmasked)
+  const float* dsim;    // bwd: d loss / d sim  [j][i]
+  float* dreg;          // bwd: [B][NR][ND] (atomic accumulate)
+  float* dwords;        // bwd: [B][ND][T]  (atomic accumulate) or null
+  float* att;           // fwd: attention maps of the diagonal pairs [B][T][NR] or null
+};
+
+struct WordsSmem {
+  float q[ND][TMAX];
+  float a1[NR][TMAX];        // S -> softmax over words -> (bwd) dS
+  float a2[TMAX][NR + 3];    // softmax over regions
+  float da[TMAX][NR + 3];    // (bwd) dA2 -> dA1^T
+  float dc[ND][TMAX];        // (bwd) dC
+  float red[4][TMAX][3];
+  float cs[TMAX], nq[TMAX], nc[TMAX];
+};
+
+template <bool BWD>
+__global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  WordsSmem& sm = *reinterpret_cast<WordsSmem*>(smem_raw);
+  const int i = blockIdx.x, j = blockIdx.y;  // text i, image j
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int w = (int)a.lens[i];
+  const float* ctx = a.reg + (long)j * NR * ND;
+
+  // 1. words of caption i
+  for (int e = t; e < ND * TMAX; e += 256) {
+    const int d = e / TMAX, k = e % TMAX;
+    sm.q[d][k] = k < w ? a.words[((long)i * ND + d) * a.T + k] : 0.f;
+  }
+  __syncthreads();
+  // 2. S[r][k] = ctx_r . q_k ; softmax over words (DAMSM_losses.py:42-45)
+  for (int r = t; r < NR; r += 256) {
+    float s[TMAX];
+#pragma unroll
+    for (int k = 0; k < TMAX; ++k) s[k] = 0.f;
+    const float* row = ctx + (long)r * ND;
+    for (int d = 0; d < ND; d += 4) {
+      const float4 c4 = *reinterpret_cast<const float4*>(row + d);
+#pragma unroll
+      for (int k = 0; k < TMAX; ++k)
+        s[k] += c4.x * sm.q[d][k] + c4.y * sm.q[d + 1][k] + c4.z * sm.q[d + 2][k] + c4.w * sm.q[d + 3][k];
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < TMAX; ++k)
+      if (k < w) mx = fmaxf(mx, s[k]);
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < TMAX; ++k) {
+      s[k] = k < w ? __expf(s[k] - mx) : 0.f;
+      sum += s[k];
+    }
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int k = 0; k < TMAX; ++k) sm.a1[r][k] = s[k] * inv;
+  }
+  __syncthreads();
+  // 3. A2[k][:] = softmax_r(gamma1 * A1[:, k]) (DAMSM_losses.py:53-54); one wave per word
+  for (int k = wv; k < w; k += 4) {
+    float mx = -INFINITY;
+    for (int r = lane; r < NR; r += 64) mx = fmaxf(mx, GAMMA1 * sm.a1[r][k]);
+    mx = wave_max(mx);
+    float sum = 0.f;
+    for (int r = lane; r < NR; r += 64) {
+      const float e = __expf(GAMMA1 * sm.a1[r][k] - mx);
+      sm.a2[k][r] = e;
+      sum += e;
+    }
+    sum = wave_sum(sum);
+    const float inv = 1.f / sum;
+    for (int r = lane; r < NR; r += 64) sm.a2[k][r] *= inv;
+  }
+  for (int e = w * (NR + 3) + t; e < TMAX * (NR + 3); e += 256) (&sm.a2[0][0])[e] = 0.f;  // unused words
+  __syncthreads();
+  if (!BWD && a.att && i == j) {
+    for (int e = t; e < w * NR; e += 256) a.att[((long)i * a.T + e / NR) * NR + e % NR] = sm.a2[e / NR][e % NR];
+  }
+  // 4. C[d][k] = sum_r ctx[r][d] A2[k][r]  (thread = d)
+  const int d = t;
+  float c[TMAX];
+#pragma unroll
+  for (int k = 0; k < TMAX; ++k) c[k] = 0.f;
+  for (int r = 0; r < NR; ++r) {
+    const float v = ctx[(long)r * ND + d];
+#pragma unroll
+    for (int k = 0; k < TMAX; ++k) c[k] += v * sm.a2[k][r];
+  }
+  // 5. cosine per word (DAMSM_losses.py:17-23): block reductions over d
+#pragma unroll
+  for (int k = 0; k < TMAX; ++k) {
+    if (k < w) {
+      const float qv = sm.q[d][k];
+      const float u = wave_sum(qv * c[k]);
+      const float q2 = wave_sum(qv * qv);
+      const float c2 = wave_sum(c[k] * c[k]);
+      if (lane == 0) {
+        sm.red[wv][k][0] = u;
+        sm.red[wv][k][1] = q2;
+        sm.red[wv][k][2] = c2;
+      }
+    }
+  }
+  __syncthreads();
+  if (t < w) {
+    const int k = t;
+    const float u = sm.red[0][k][0] + sm.red[1][k][0] + sm.red[2][k][0] + sm.red[3][k][0];
+    const float q2 = sm.red[0][k][1] + sm.red[1][k][1] + sm.red[2][k][1] + sm.red[3][k][1];
+    const float c2 = sm.red[0][k][2] + sm.red[1][k][2] + sm.red[2][k][2] + sm.red[3][k][2];
+    sm.nq[k] = sqrtf(q2);
+    sm.nc[k] = sqrtf(c2);
+    sm.cs[k] = u / fmaxf(sm.nq[k] * sm.nc[k], 1e-8f);
+  }
+  __syncthreads();
+  // 6. row similarity = log sum_k exp(gamma2 cos_k)   (DAMSM_losses.py:315-317)
+  float se = 0.f;
+  for (int k = 0; k < w; ++k) se += __expf(GAMMA2 * sm.cs[k]);
+  if (!BWD) {
+    if (t == 0) a.sim[(long)j * a.B + i] = GAMMA3 * logf(se);
+    return;
+  }
+  // ================================ backward ================================
+  const float drow = GAMMA3 * a.dsim[(long)j * a.B + i];
+  float dqv[TMAX];
+#pragma unroll
+  for (int k = 0; k < TMAX; ++k) {
+    float dC = 0.f;
+    dqv[k] = 0.f;
+    if (k < w) {
+      const float cs = sm.cs[k], nq = sm.nq[k], nc = sm.nc[k];
+      const float dcos = drow * GAMMA2 * __expf(GAMMA2 * cs) / se;
+      const float den = nq * nc;
+      const float qv = sm.q[d][k];
+      if (den > 1e-8f) {
+        dC = dcos * (qv / den - cs * c[k] / (nc * nc));
+        dqv[k] = dcos * (c[k] / den - cs * qv / (nq * nq));
+      } else {
+        dC = dcos * qv / 1e-8f;
+        dqv[k] = dcos * c[k] / 1e-8f;
+      }
+    }
+    sm.dc[d][k] = dC;
+  }
+  __syncthreads();
+  // dA2[k][r] = sum_d ctx[r][d] dC[d][k]   (thread per region)
+  for (int r = t; r < NR; r += 256) {
+    float s[TMAX];
+#pragma unroll
+    for (int k = 0; k < TMAX; ++k) s[k] = 0.f;
+    const float* row = ctx + (long)r * ND;
+    for (int dd = 0; dd < ND; dd += 4) {
+      const float4 c4 = *reinterpret_cast<const float4*>(row + dd);
+#pragma unroll
+      for (int k = 0; k < TMAX; ++k)
+        s[k] += c4.x * sm.dc[dd][k] + c4.y * sm.dc[dd + 1][k] + c4.z * sm.dc[dd + 2][k] + c4.w * sm.dc[dd + 3][k];
+    }
+#pragma unroll
+    for (int k = 0; k < TMAX; ++k) sm.da[k][r] = s[k];
+  }
+  __syncthreads();
+  // softmax-over-regions backward: dZ = A2 (dA2 - <A2, dA2>); dA1[r][k] = gamma1 dZ[k][r]
+  for (int k = wv; k < w; k += 4) {
+    float s = 0.f;
+    for (int r = lane; r < NR; r += 64) s += sm.a2[k][r] * sm.da[k][r];
+    s = wave_sum(s);
+    for (int r = lane; r < NR; r += 64) sm.da[k][r] = GAMMA1 * sm.a2[k][r] * (sm.da[k][r] - s);
+  }
+  __syncthreads();
+  // softmax-over-words backward: dS[r][k] = A1 (dA1 - <A1, dA1>)  (thread per region)
+  for (int r = t; r < NR; r += 256) {
+    float s = 0.f;
+    for (int k = 0; k < w; ++k) s += sm.a1[r][k] * sm.da[k][r];
+    for (int k = 0; k < TMAX; ++k) sm.a1[r][k] = k < w ? sm.a1[r][k] * (sm.da[k][r] - s) : 0.f;
+  }
+  __syncthreads();
+  // dctx[r][d] = sum_k dC[d][k] A2[k][r] + q[d][k] dS[r][k] ;  dq[d][k] += sum_r ctx[r][d] dS[r][k]
+  float* dreg = a.dreg + (long)j * NR * ND;
+  for (int r = 0; r < NR; ++r) {
+    float g = 0.f;
+    const float v = ctx[(long)r * ND + d];
+#pragma unroll
+    for (int k = 0; k < TMAX; ++k) {
+      g += sm.dc[d][k] * sm.a2[k][r] + sm.q[d][k] * sm.a1[r][k];
+      dqv[k] += v * sm.a1[r][k];
+    }
+    atomicAdd(dreg + (long)r * ND + d, g);
+  }
+  if (a.dwords) {
+#pragma unroll
+    for (int k = 0; k < TMAX; ++k)
+      if (k < w) atomicAdd(a.dwords + ((long)i * ND + d) * a.T + k, dqv[k]);
+  }
+}
+
+// ------------------------------------------ masked bidirectional CE ------
+// sim[a][b] (rows a), mask[a][b] = cls[a]==cls[b] && a!=b  -> -inf.
+// loss0 = CE(sim, arange), loss1 = CE(sim^T, arange). One block.
+__global__ void sim_ce_kernel(const float* sim, int B, const long* cls, const long* lab, float* loss, const float* gl,
+                              float* dsim) {
+  extern __shared__ float sh[];
+  float* lse_r = sh;       // [B]
+  float* lse_c = sh + B;   // [B]
+  __shared__ float red[16];
+  auto masked = [&](int x, int y) { return cls && x != y && cls[x] == cls[y]; };
+  for (int x = threadIdx.x; x < 2 * B; x += blockDim.x) {
+    const bool row = x < B;
+    const int idx = row ? x : x - B;
+    float mx = -INFINITY;
+    for (int y = 0; y < B; ++y) {
+      const int a = row ? idx : y, b = row ? y : idx;
+      if (!masked(a, b)) mx = fmaxf(mx, sim[(long)a * B + b]);
+    }
+    float s = 0.f;
+    for (int y = 0; y < B; ++y) {
+      const int a = row ? idx : y, b = row ? y : idx;
+      if (!masked(a, b)) s += __expf(sim[(long)a * B + b] - mx);
+    }
+    (row ? lse_r : lse_c)[idx] = mx + logf(s);
+  }
+  __syncthreads();
+  if (!dsim) {
+    float l0 = 0.f, l1 = 0.f;
+    for (int x = threadIdx.x; x < B; x += blockDim.x) {
+      const long tx = lab ? lab[x] : x;
+      l0 += lse_r[x] - sim[(long)x * B + tx];
+      l1 += lse_c[x] - sim[tx * B + x];
+    }
+    l0 = block_sum(l0, red);
+    l1 = block_sum(l1, red);
+    if (threadIdx.x == 0) {
+      loss[0] = l0 / B;
+      loss[1] = l1 / B;
+    }
+  } else {
+    const float g0 = gl[0] / B, g1 = gl[1] / B;
+    for (int e = threadIdx.x; e < B * B; e += blockDim.x) {
+      const int a = e / B, b = e % B;
+      float g = 0.f;
+      if (!masked(a, b)) {
+        const float v = sim[e];
+        g = g0 * __expf(v - lse_r[a]) + g1 * __expf(v - lse_c[b]);
+      }
+      if (b == (lab ? lab[a] : a)) g -= g0;
+      if (a == (lab ? lab[b] : b)) g -= g1;
+      dsim[e] = g;
+    }
+  }
+}
+
+// ------------------------------------------------------------ sent loss --
+// cos[a][b] * gamma3 with norms clamped as in sent_loss (DAMSM_losses.py:253-258)
+__global__ void sent_sim_kernel(const float* cnn, const float* rnn, int B, int D, float* sim) {
+  const int a = blockIdx.x;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    float u = 0.f, n1 = 0.f, n2 = 0.f;
+    for (int k = 0; k < D; ++k) {
+      const float x = cnn[(long)a * D + k], y = rnn[(long)b * D + k];
+      u += x * y;
+      n1 += x * x;
+      n2 += y * y;
+    }
+    sim[(long)a * B + b] = u / fmaxf(sqrtf(n1) * sqrtf(n2), 1e-8f) * GAMMA3;
+  }
+}
+
+// norms of the rows of cnn (which 0) and rnn (which 1): nrm[which*B + b]
+__global__ void row_norm_kernel(const float* cnn, const float* rnn, int B, int D, float* nrm) {
+  const int b = blockIdx.x, which = blockIdx.y;
+  const float* X = which ? rnn : cnn;
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int k = threadIdx.x; k < D; k += blockDim.x) s += X[(long)b * D + k] * X[(long)b * D + k];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) nrm[which * B + b] = sqrtf(s);
+}
+
+// gradient of sim = gamma3 * cos wrt cnn (which=0, rows) or rnn (which=1, cols); thread per (row, k)
+__global__ void sent_sim_bwd_kernel(const float* cnn, const float* rnn, int B, int D, const float* sim,
+                                    const float* nrm, const float* dsim, int which, float* out) {
+  const long total = (long)B * D;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int x = e / D, k = e % D;
+    const float* X = which == 0 ? cnn : rnn;
+    const float* Y = which == 0 ? rnn : cnn;
+    const float nx = nrm[which * B + x];
+    const float xv = X[(long)x * D + k];
+    float g = 0.f;
+    for (int y = 0; y < B; ++y) {
+      const float ny = nrm[(1 - which) * B + y];
+      const long idx = which == 0 ? (long)x * B + y : (long)y * B + x;
+      const float ds = dsim[idx];
+      const float yv = Y[(long)y * D + k];
+      const float den = nx * ny;
+      if (den > 1e-8f) g += GAMMA3 * ds * (yv / den - (sim[idx] / GAMMA3) * xv / (nx * nx));
+      else g += GAMMA3 * ds * yv / 1e-8f;
+    }
+    out[e] = g;
+  }
+}
+
+// ------------------------------------------------- hinge / mean on D out --
+// mode 0: mean(relu(1 - x)); 1: mean(relu(1 + x)); 2: -mean(x); 3: mean(x)
+__global__ void dout_reduce_kernel(const float* x, int n, int mode, float* out, const float* gout, float* dx) {
+  __shared__ float red[16];
+  if (!dx) {
+    float s = 0.f;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+      const float v = x[k];
+      s += mode == 0 ? fmaxf(1.f - v, 0.f) : mode == 1 ? fmaxf(1.f + v, 0.f) : (mode == 2 ? -v : v);
+    }
+    s = block_sum(s, red);
+    if (threadIdx.x == 0) out[0] = s / n;
+  } else {
+    const float g = gout[0] / n;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+      const float v = x[k];
+      dx[k] = mode == 0 ? (1.f - v > 0.f ? -g : 0.f) : mode == 1 ? (1.f + v > 0.f ? g : 0.f) : (mode == 2 ? -g : g);
+    }
+  }
+}
+
+// mean BCE-with-logits (F.binary_cross_entropy_with_logits, numerically stable form)
+__global__ void bce_kernel(const float* x, const float* y, int n, float* out, const float* gout, float* dx) {
+  __shared__ float red[16];
+  if (!dx) {
+    float s = 0.f;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+      const float v = x[k], t = y[k];
+      s += fmaxf(v, 0.f) - v * t + log1pf(__expf(-fabsf(v)));
+    }
+    s = block_sum(s, red);
+    if (threadIdx.x == 0) out[0] = s / n;
+  } else {
+    const float g = gout[0] / n;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) dx[k] = g * (1.f / (1.f + __expf(-x[k])) - y[k]);
+  }
+}
+
+// ----------------------------------------------------- gradient penalty --
+// per-sample ||[g_img, g_sent]||^2 (g_img NHWC bf16 [B][HW][ld] with C channels)
+__global__ void gp_norm_kernel(const bf16_t* gx, int ld, int HW, int C, const float* gs, int E, float* nrm2) {
+  __shared__ float red[16];
+  const int b = blockIdx.x;
+  float s = 0.f;
+  for (long e = threadIdx.x; e < (long)HW * C; e += blockDim.x) {
+    const float v = bf2f(gx[((long)b * HW + e / C) * ld + e % C]);
+    s += v * v;
+  }
+  for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    const float v = gs[(long)b * E + e];
+    s += v * v;
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) nrm2[b] = s;
+}
+
+// loss = 2 * mean_b(||g_b||^6)
+__global__ void gp_loss_kernel(const float* nrm2, int B, float* out) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const float n = sqrtf(nrm2[b]);
+    const float n2 = n * n;
+    s += n2 * n2 * n2;
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) out[0] = 2.f * s / B;
+}
+
+// d/dg: 2/B * 6 ||g||^4 g * gout
+__global__ void gp_bwd_kernel(const bf16_t* gx, int ld, int HW, int C, const float* gs, int E, const float* nrm2,
+                              int B, const float* gout, bf16_t* dgx, int lddgx, float* dgs) {
+  const long nimg = (long)B * HW * C;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nimg + (long)B * E;
+       e += (long)gridDim.x * blockDim.x) {
+    if (e < nimg) {
+      const int c = e % C;
+      const long p = e / C;
+      const int b = p / HW;
+      const float n2 = nrm2[b];
+      const float coef = gout[0] * 12.f / B * n2 * n2;
+      dgx[p * lddgx + c] = f2bf(coef * bf2f(gx[p * ld + c]));
+    } else {
+      const long q = e - nimg;
+      const int b = q / E;
+      const float n2 = nrm2[b];
+      dgs[q] = gout[0] * 12.f / B * n2 * n2 * gs[q];
+    }
+  }
+}
+
+// --------------------------------------------------------- class labels --
+// labels[i][(idx - 1) mod ncls] = 1   (train.py:102: idx 0 wraps to the last column)
+__global__ void class_onehot_kernel(const long* ids, int B, int ncls, float* out, int* err) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < (long)B * ncls; e += (long)gridDim.x * blockDim.x) {
+    const int i = e / ncls, c = e % ncls;
+    long col = ids[i] - 1;
+    if (col < 0) col += ncls;
+    if (col < 0 || col >= ncls) {
+      if (err) *err = 1;
+      col = -1;
+    }
+    out[e] = (c == col) ? 1.f : 0.f;
+  }
+}
+
+// -------------------------------------------------- ATTR_Enhance core ----
+// per sample: P = softmax(q k^T) * scale (rows of 4), out = P v ; merged = sum_rows(out)
+__global__ void attr_attn_kernel(const float* q, const float* k, const float* v, int B, int L, int D, float scale,
+                                 float* probs, float* out, float* merged) {
+  const int b = blockIdx.x;
+  __shared__ float P[8][8];
+  __shared__ float red[16];
+  for (int x = 0; x < L; ++x)
+    for (int y = 0; y < L; ++y) {
+      float s = 0.f;
+      for (int d = threadIdx.x; d < D; d += blockDim.x)
+        s += q[((long)b * L + x) * D + d] * k[((long)b * L + y) * D + d];
+      s = block_sum(s, red);
+      if (threadIdx.x == 0) P[x][y] = s;
+    }
+  __syncthreads();
+  if (threadIdx.x < L) {
+    const int x = threadIdx.x;
+    float mx = -INFINITY;
+    for (int y = 0; y < L; ++y) mx = fmaxf(mx, P[x][y]);
+    float sm = 0.f;
+    for (int y = 0; y < L; ++y) sm += __expf(P[x][y] - mx);
+    for (int y = 0; y < L; ++y) {
+      const float pv = __expf(P[x][y] - mx) / sm * scale;
+      P[x][y] = pv;
+      probs[((long)b * L + x) * L + y] = pv;
+    }
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float m = 0.f;
+    for (int x = 0; x < L; ++x) {
+      float o = 0.f;
+      for (int y = 0; y < L; ++y) o += P[x][y] * v[((long)b * L + y) * D + d];
+      out[((long)b * L + x) * D + d] = o;
+      m += o;
+    }
+    if (merged) merged[(long)b * D + d] = m;
+  }
+}
+
+// backward given dout [B][L][D] (already including the merge broadcast):
+// dv = P^T dout ; dP = dout v^T ; dlogits = scale * sm*(dP' - sum sm dP') with P = scale*sm
+// dq = dlogits k ; dk = dlogits^T q
+__global__ void attr_attn_bwd_kernel(const float* q, const float* k, const float* v, const float* probs,
+                                     const float* dout, int B, int L, int D, float scale, float* dq, float* dk,
+                                     float* dv) {
+  const int b = blockIdx.x;
+  __shared__ float dP[8][8], G[8][8];
+  __shared__ float red[16];
+  for (int x = 0; x < L; ++x)
+    for (int y = 0; y < L; ++y) {
+      float s = 0.f;
+      for (int d = threadIdx.x; d < D; d += blockDim.x)
+        s += dout[((long)b * L + x) * D + d] * v[((long)b * L + y) * D + d];
+      s = block_sum(s, red);
+      if (threadIdx.x == 0) dP[x][y] = s;
+    }
+  __syncthreads();
+  if (threadIdx.x < L) {
+    const int x = threadIdx.x;
+    // P = scale * sm ; d sm = scale * dP ; dlogit = sm * (dsm - sum(sm * dsm))
+    float dot = 0.f;
+    for (int y = 0; y < L; ++y) dot += (probs[((long)b * L + x) * L + y] / scale) * scale * dP[x][y];
+    for (int y = 0; y < L; ++y) {
+      const float sm = probs[((long)b * L + x) * L + y] / scale;
+      G[x][y] = sm * (scale * dP[x][y] - dot);
+    }
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    for (int x = 0; x < L; ++x) {
+      float gq = 0.f, gk = 0.f, gv = 0.f;
+      for (int y = 0; y < L; ++y) {
+        gq += G[x][y] * k[((long)b * L + y) * D + d];
+        gk += G[y][x] * q[((long)b * L + y) * D + d];
+        gv += probs[((long)b * L + y) * L + x] * dout[((long)b * L + y) * D + d];
+      }
+      dq[((long)b * L + x) * D + d] = gq;
+      dk[((long)b * L + x) * D + d] = gk;
+      dv[((long)b * L + x) * D + d] = gv;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int eegan_words_sim(const float* regions, const float* words, const long* cap_lens, int B, int T, float* sim,
+                    float* att, hipStream_t s) {
+  if (T > TMAX) {
+    ee_set_error("words_sim: T=%d > %d", T, TMAX);
+    return -22;
+  }
+  WordsArgs a = {};
+  a.reg = regions;
+  a.words = words;
+  a.lens = cap_lens;
+  a.B = B;
+  a.T = T;
+  a.sim = sim;
+  a.att = att;
+  dim3 grid(B, B);
+  words_pair_kernel<false><<<grid, 256, sizeof(WordsSmem), s>>>(a);
+  return ee_check_launch("words_sim");
+}
+
+int eegan_words_sim_bwd(const float* regions, const float* words, const long* cap_lens, int B, int T,
+                        const float* dsim, float* dregions, float* dwords, hipStream_t s) {
+  if (T > TMAX) {
+    ee_set_error("words_sim_bwd: T=%d > %d", T, TMAX);
+    return -22;
+  }
+  (void)hipMemsetAsync(dregions, 0, (size_t)B * NR * ND * sizeof(float), s);
+  if (dwords) (void)hipMemsetAsync(dwords, 0, (size_t)B * ND * T * sizeof(float), s);
+  WordsArgs a = {};
+  a.reg = regions;
+  a.words = words;
+  a.lens = cap_lens;
+  a.B = B;
+  a.T = T;
+  a.dsim = dsim;
+  a.dreg = dregions;
+  a.dwords = dwords;
+  dim3 grid(B, B);
+  words_pair_kernel<true><<<grid, 256, sizeof(WordsSmem), s>>>(a);
+  return ee_check_launch("words_sim_bwd");
+}
+
+int eegan_sim_ce(const float* sim, int B, const long* class_ids, const long* labels, float* loss2, hipStream_t s) {
+  sim_ce_kernel<<<1, 256, 2 * B * sizeof(float), s>>>(sim, B, class_ids, labels, loss2, nullptr, nullptr);
+  return ee_check_launch("sim_ce");
+}
+
+int eegan_sim_ce_bwd(const float* sim, int B, const long* class_ids, const long* labels, const float* gloss2,
+                     float* dsim, hipStream_t s) {
+  sim_ce_kernel<<<1, 256, 2 * B * sizeof(float), s>>>(sim, B, class_ids, labels, nullptr, gloss2, dsim);
+  return ee_check_launch("sim_ce_bwd");
+}
+
+int eegan_sent_sim(const float* cnn, const float* rnn, int B, int D, float* sim, hipStream_t s) {
+  sent_sim_kernel<<<B, 64, 0, s>>>(cnn, rnn, B, D, sim);
+  return ee_check_launch("sent_sim");
+}
+
+int eegan_sent_sim_bwd(const float* cnn, const float* rnn, int B, int D, const float* sim, const float* dsim,
+                       float* nrm_ws, float* dcnn, float* drnn, hipStream_t s) {
+  row_norm_kernel<<<dim3(B, 2), 64, 0, s>>>(cnn, rnn, B, D, nrm_ws);
+  const int blocks = ee_cdiv((long)B * D, 256);
+  if (dcnn) sent_sim_bwd_kernel<<<blocks, 256, 0, s>>>(cnn, rnn, B, D, sim, nrm_ws, dsim, 0, dcnn);
+  if (drnn) sent_sim_bwd_kernel<<<blocks, 256, 0, s>>>(cnn, rnn, B, D, sim, nrm_ws, dsim, 1, drnn);
+  return ee_check_launch("sent_sim_bwd");
+}
+
+int eegan_dout_reduce(const float* x, int n, int mode, float* out, hipStream_t s) {
+  dout_reduce_kernel<<<1, 256, 0, s>>>(x, n, mode, out, nullptr, nullptr);
+  return ee_check_launch("dout_reduce");
+}
+
+int eegan_dout_reduce_bwd(const float* x, int n, int mode, const float* gout, float* dx, hipStream_t s) {
+  dout_reduce_kernel<<<1, 256, 0, s>>>(x, n, mode, nullptr, gout, dx);
+  return ee_check_launch("dout_reduce_bwd");
+}
+
+int eegan_bce_logits(const float* x, const float* target, int n, float* out, hipStream_t s) {
+  bce_kernel<<<1, 256, 0, s>>>(x, target, n, out, nullptr, nullptr);
+  return ee_check_launch("bce");
+}
+
+int eegan_bce_logits_bwd(const float* x, const float* target, int n, const float* gout, float* dx, hipStream_t s) {
+  bce_kernel<<<1, 256, 0, s>>>(x, target, n, nullptr, gout, dx);
+  return ee_check_launch("bce_bwd");
+}
+
+int eegan_gp_loss(const uint16_t* gx, int ld, int B, int HW, int C, const float* gs, int E, float* nrm2, float* out,
+                  hipStream_t s) {
+  gp_norm_kernel<<<B, 256, 0, s>>>(gx, ld, HW, C, gs, E, nrm2);
+  int rc = ee_check_launch("gp_norm");
+  if (rc) return rc;
+  gp_loss_kernel<<<1, 256, 0, s>>>(nrm2, B, out);
+  return ee_check_launch("gp_loss");
+}
+
+int eegan_gp_loss_bwd(const uint16_t* gx, int ld, int B, int HW, int C, const float* gs, int E, const float* nrm2,
+                      const float* gout, uint16_t* dgx, int lddgx, float* dgs, hipStream_t s) {
+  const long work = (long)B * HW * C + (long)B * E;
+  const int blocks = (int)std::min<long>(8192, (work + 255) / 256);
+  gp_bwd_kernel<<<blocks, 256, 0, s>>>(gx, ld, HW, C, gs, E, nrm2, B, gout, dgx, lddgx, dgs);
+  return ee_check_launch("gp_bwd");
+}
+
+int eegan_class_onehot(const long* ids, int B, int ncls, float* out, int* err, hipStream_t s) {
+  class_onehot_kernel<<<ee_cdiv((long)B * ncls, 256), 256, 0, s>>>(ids, B, ncls, out, err);
+  return ee_check_launch("class_onehot");
+}
+
+int eegan_attr_attn(const float* q, const float* k, const float* v, int B, int L, int D, float scale, float* probs,
+                    float* out, float* merged, hipStream_t s) {
+  if (L > 8) {
+    ee_set_error("attr_attn: L > 8");
+    return -22;
+  }
+  attr_attn_kernel<<<B, 256, 0, s>>>(q, k, v, B, L, D, scale, probs, out, merged);
+  return ee_check_launch("attr_attn");
+}
+
+int eegan_attr_attn_bwd(const float* q, const float* k, const float* v, const float* probs, const float* dout, int B,
+                        int L, int D, float scale, float* dq, float* dk, float* dv, hipStream_t s) {
+  attr_attn_bwd_kernel<<<B, 256, 0, s>>>(q, k, v, probs, dout, B, L, D, scale, dq, dk, dv);
+  return ee_check_launch("attr_attn_bwd");
+}
+
+}  // extern "C"

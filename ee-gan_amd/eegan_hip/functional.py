@@ -1,0 +1,1063 @@
+"""torch.autograd.Functions over libeegan_hip.so.
+
+Every Function launches HIP kernels through the C ABI on torch's current
+stream; torch provides memory (caching allocator), streams and the autograd
+tape.  The discriminator-side Functions (conv, activation, avg-pool,
+scale-add, cat-tile, cast) express their backward through other Functions,
+so they are differentiable to any order -- needed by the MA gradient penalty
+(train.py:378-402, autograd.grad(create_graph=True) through every D layer).
+Generator-side Functions (BN modulation, upsample-fused convs, linears,
+mask resize) are first-order, as the reference only differentiates G once.
+"""
+import math
+
+import torch
+
+from . import tensor as T
+from ._lib import ops, ConvDesc, BnModDesc, ACT_CODES
+from .tensor import BF16, F32, empty_nhwc, ld_of, ptr, stream, to_nhwc_bf16, workspace
+
+# In autograd.grad() mode the engine cannot report whether a leaf is needed;
+# parameters are then assumed NOT requested (the gradient penalty asks only
+# for input gradients: train.py:389-394).  Set False to always compute them.
+SKIP_PARAM_GRADS_IN_AUTOGRAD_GRAD = True
+
+# Process-group hook for SyncBN statistics (set by eegan_hip.dist)
+SYNC_BN_ALLREDUCE = None   # callable(tensor fp64) -> None (in-place sum over ranks)
+SYNC_BN_WORLD = 1
+
+
+def _needed(ctx, i):
+    if not ctx.needs_input_grad[i]:
+        return False
+    node = ctx.next_functions[i][0]
+    if node is None:
+        return False
+    try:
+        return bool(torch._C._will_engine_execute_node(node))
+    except RuntimeError:
+        var = getattr(node, 'variable', None)
+        if SKIP_PARAM_GRADS_IN_AUTOGRAD_GRAD and isinstance(var, torch.nn.Parameter):
+            return False
+        return True
+
+
+# ============================================================== weights ===
+class PackCache:
+    """bf16 packed images of one conv weight (forward and bwd-data layouts),
+    rebuilt whenever the fp32 parameter changes (torch in-place version or
+    the flat-Adam generation counter)."""
+
+    def __init__(self, scale=None):
+        self.fwd_key = self.bwd_key = None
+        self.fwd = self.bwd = None
+        self.scale = scale  # optional per-output-channel fp32 scale folded into the packs
+
+    @staticmethod
+    def _key(W, Cg):
+        gen = getattr(W, '_eegan_gen', None)
+        return (W.data_ptr(), W._version, gen[0] if gen is not None else 0, Cg)
+
+    def get(self, W, Cg, transposed):
+        key = self._key(W, Cg)
+        if transposed:
+            if self.bwd_key != key:
+                self.bwd = pack_weight(W, Cg, True, self.scale)
+                self.bwd_key = key
+            return self.bwd
+        if self.fwd_key != key:
+            self.fwd = pack_weight(W, Cg, False, self.scale)
+            self.fwd_key = key
+        return self.fwd
+
+
+def pack_weight(W, Cg, transposed, scale=None):
+    Cout, Cin, R, S = W.shape
+    n = ops.conv_packed_elems(Cout, Cin, R, S, int(transposed), Cg)
+    out = torch.empty(n, dtype=BF16, device=W.device)
+    Wc = W.detach()
+    if not Wc.is_contiguous() or Wc.dtype != F32:
+        Wc = Wc.float().contiguous()
+    ops.conv_pack_weights(Wc.data_ptr(), ptr(scale), Cout, Cin, R, S, int(transposed), Cg, out.data_ptr(), stream())
+    return out
+
+
+def _pack(W, cache, Cg, transposed):
+    if cache is not None:
+        return cache.get(W, Cg, transposed)
+    return pack_weight(W, Cg, transposed)
+
+
+class Geom:
+    """Static conv geometry (per module); the batch/grid sizes come from x."""
+    __slots__ = ('K', 'R', 'S', 'stride', 'ph', 'pw', 'up2')
+
+    def __init__(self, K, R, S, stride, ph, pw, up2=0):
+        self.K, self.R, self.S, self.stride, self.ph, self.pw, self.up2 = K, R, S, stride, ph, pw, up2
+
+    def out_hw(self, H, W):
+        Hl, Wl = (H * 2, W * 2) if self.up2 else (H, W)
+        return ((Hl + 2 * self.ph - self.R) // self.stride + 1, (Wl + 2 * self.pw - self.S) // self.stride + 1)
+
+    def desc(self, x, ldy):
+        N, C, H, W = x.shape
+        Ho, Wo = self.out_hw(H, W)
+        Hl, Wl = (H * 2, W * 2) if self.up2 else (H, W)
+        return ConvDesc(N, Hl, Wl, C, ld_of(x), self.K, self.R, self.S, self.stride, self.ph, self.pw, self.up2,
+                        Ho, Wo, ldy)
+
+
+def _desc_io(g, x_shape, ldx, ldy):
+    N, C, H, W = x_shape
+    Hl, Wl = (H * 2, W * 2) if g.up2 else (H, W)
+    Ho = (Hl + 2 * g.ph - g.R) // g.stride + 1
+    Wo = (Wl + 2 * g.pw - g.S) // g.stride + 1
+    return ConvDesc(N, Hl, Wl, C, ldx, g.K, g.R, g.S, g.stride, g.ph, g.pw, g.up2, Ho, Wo, ldy)
+
+
+# ====================================================== launch timing ====
+class LaunchTimer(object):
+    """Brackets every launch of the conv kernels with HIP events on the stream
+    they run on (bench.py's roofline): records (kind, algorithmic flops,
+    algorithmic bytes, start, end)."""
+
+    def __init__(self):
+        self.rec = []
+
+    def __call__(self, kind, flops, nbytes, fn):
+        s = torch.cuda.current_stream()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        fn()
+        e1.record(s)
+        self.rec.append((kind, flops, nbytes, e0, e1))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for kind, fl, nb, e0, e1 in self.rec:
+            t = e0.elapsed_time(e1) * 1e-3
+            o = out.setdefault(kind, [0, 0.0, 0.0, 0.0])
+            o[0] += 1
+            o[1] += fl
+            o[2] += nb
+            o[3] += t
+        return out
+
+
+TIMER = None
+
+
+def _launch(kind, flops, nbytes, fn):
+    if TIMER is None:
+        fn()
+    else:
+        TIMER(kind, flops, nbytes, fn)
+
+
+# ============================================================ conv core ===
+def conv_fwd_raw(x, W, b, g, act=0, slope=0.2, out_f32=False, cache=None, res=None, gamma=None):
+    x = to_nhwc_bf16(x)
+    N, C, H, Wd = x.shape
+    Ho, Wo = g.out_hw(H, Wd)
+    y = empty_nhwc(N, g.K, Ho, Wo, x.device, dtype=F32 if out_f32 else BF16)
+    d = _desc_io(g, x.shape, ld_of(x), ld_of(y))
+    Cg = ops.conv_gather_channels(C, ld_of(x))
+    wp = _pack(W, cache, Cg, False)
+    flops = 2.0 * N * Ho * Wo * g.K * C * g.R * g.S
+    nbytes = 2.0 * (N * H * Wd * C + N * Ho * Wo * g.K * (2 if out_f32 else 1) + g.K * C * g.R * g.S)
+    _launch('conv_fwd', flops, nbytes, lambda: ops.conv_fwd(
+        d, x.data_ptr(), wp.data_ptr(), ptr(b), act, slope, ptr(res), ld_of(res) if res is not None else 0,
+        ptr(gamma), y.data_ptr(), int(out_f32), stream()))
+    return y
+
+
+def conv_bwd_data_raw(dz, W, g, x_shape, cache=None):
+    """dx for the LOGICAL input grid (hi-res when g.up2), NHWC bf16."""
+    N, C, H, Wd = x_shape
+    Hl, Wl = (H * 2, Wd * 2) if g.up2 else (H, Wd)
+    dx = empty_nhwc(N, C, Hl, Wl, dz.device)
+    d = _desc_io(g, x_shape, T.ld_for(C), ld_of(dz))
+    if g.up2:
+        d.H, d.W, d.up2 = Hl, Wl, 0
+    Cg = ops.conv_gather_channels(g.K, ld_of(dz))
+    wp = _pack(W, cache, Cg, True)
+    Ho, Wo = d.Ho, d.Wo
+    flops = 2.0 * N * Ho * Wo * g.K * C * g.R * g.S
+    nbytes = 2.0 * (N * Hl * Wl * C + N * Ho * Wo * g.K + g.K * C * g.R * g.S)
+    _launch('conv_bwd_data', flops, nbytes, lambda: ops.conv_bwd_data(
+        d, dz.data_ptr(), wp.data_ptr(), dx.data_ptr(), ld_of(dx), 0, stream()))
+    if g.up2:
+        lo = empty_nhwc(N, C, H, Wd, dz.device)
+        ops.sumpool2(dx.data_ptr(), N, Hl, Wl, C, ld_of(dx), lo.data_ptr(), ld_of(lo), stream())
+        return lo
+    return dx
+
+
+def conv_bwd_weight_raw(x, dz, g, W_shape):
+    x = to_nhwc_bf16(x)
+    d = _desc_io(g, x.shape, ld_of(x), ld_of(dz))
+    ws = workspace(ops.conv_wgrad_workspace(d), x.device)
+    dW = torch.empty(W_shape, dtype=F32, device=x.device)
+    N, C, H, Wd = x.shape
+    flops = 2.0 * N * d.Ho * d.Wo * g.K * C * g.R * g.S
+    nbytes = 2.0 * (N * H * Wd * C + N * d.Ho * d.Wo * g.K) + 4.0 * g.K * C * g.R * g.S
+    _launch('conv_bwd_weight', flops, nbytes, lambda: ops.conv_bwd_weight(
+        d, x.data_ptr(), dz.data_ptr(), ws.data_ptr(), dW.data_ptr(), 0, stream()))
+    return dW
+
+
+def chansum_raw(dz):
+    N, C, H, W = dz.shape
+    P = N * H * W
+    ws = workspace(ops.chansum_workspace(P, C), dz.device)
+    out = torch.empty(C, dtype=F32, device=dz.device)
+    ops.chansum(dz.data_ptr(), ld_of(dz), P, C, ws.data_ptr(), out.data_ptr(), 0, stream())
+    return out
+
+
+def act_bwd_raw(gy, y, act, slope):
+    N, C, H, W = y.shape
+    dx = empty_nhwc(N, C, H, W, y.device)
+    ops.act_bwd(gy.data_ptr(), ld_of(gy), y.data_ptr(), ld_of(y), N * H * W, C, act, slope, dx.data_ptr(), ld_of(dx),
+                stream())
+    return dx
+
+
+def _as_bf16_grad(g):
+    if g.dtype == F32:
+        return CastF32Bf16Fn.apply(g)
+    return to_nhwc_bf16(g)
+
+
+class Conv2dFn(torch.autograd.Function):
+    """y = act(conv(x, W) + b); NHWC bf16 in, bf16 (or fp32) out."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, g, act, slope, out_f32, cache):
+        x = to_nhwc_bf16(x)
+        y = conv_fwd_raw(x, W, b, g, act, slope, out_f32, cache)
+        ctx.g, ctx.act, ctx.slope, ctx.cache = g, act, slope, cache
+        ctx.x_shape = tuple(x.shape)
+        ctx.save_for_backward(x, W, y if act else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, W, y = ctx.saved_tensors
+        g = ctx.g
+        gy = _as_bf16_grad(gy)
+        dz = ActBwdFn.apply(gy, y, ctx.act, ctx.slope) if ctx.act else gy
+        dx = dW = db = None
+        if _needed(ctx, 0):
+            if g.up2:
+                dx = conv_bwd_data_raw(dz, W, g, ctx.x_shape, ctx.cache)
+            else:
+                dx = ConvBwdDataFn.apply(dz, W, g, ctx.x_shape, ctx.cache)
+        if _needed(ctx, 1):
+            dW = ConvBwdWeightFn.apply(x, dz, g) if not g.up2 else conv_bwd_weight_raw(x, dz, g, W.shape)
+        if ctx.needs_input_grad[2] and _needed(ctx, 2):
+            db = ChanSumFn.apply(dz)
+        return dx, dW, db, None, None, None, None, None
+
+
+class ConvBwdDataFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, dz, W, g, x_shape, cache):
+        ctx.g, ctx.cache, ctx.x_shape = g, cache, x_shape
+        ctx.save_for_backward(dz, W)
+        return conv_bwd_data_raw(dz, W, g, x_shape, cache)
+
+    @staticmethod
+    def backward(ctx, gdx):
+        dz, W = ctx.saved_tensors
+        gdx = _as_bf16_grad(gdx)
+        g_dz = g_W = None
+        if ctx.needs_input_grad[0]:
+            g_dz = Conv2dFn.apply(gdx, W, None, ctx.g, 0, 0.0, False, ctx.cache)
+        if ctx.needs_input_grad[1]:
+            g_W = ConvBwdWeightFn.apply(gdx, dz, ctx.g)
+        return g_dz, g_W, None, None, None
+
+
+class ConvBwdWeightFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dz, g):
+        ctx.g = g
+        ctx.x_shape = tuple(x.shape)
+        ctx.save_for_backward(x, dz)
+        K = g.K
+        return conv_bwd_weight_raw(x, dz, g, (K, x.shape[1], g.R, g.S))
+
+    @staticmethod
+    def backward(ctx, gW):
+        x, dz = ctx.saved_tensors
+        gx = gdz = None
+        if ctx.needs_input_grad[0]:
+            gx = ConvBwdDataFn.apply(dz, gW, ctx.g, ctx.x_shape, None)
+        if ctx.needs_input_grad[1]:
+            gdz = Conv2dFn.apply(x, gW, None, ctx.g, 0, 0.0, False, None)
+        return gx, gdz, None
+
+
+class ActBwdFn(torch.autograd.Function):
+    """dz = g * act'(y); linear in g (relu/lrelu derivative is piecewise constant)."""
+
+    @staticmethod
+    def forward(ctx, g, y, act, slope):
+        ctx.act, ctx.slope = act, slope
+        ctx.save_for_backward(y)
+        return act_bwd_raw(g, y, act, slope)
+
+    @staticmethod
+    def backward(ctx, gg):
+        (y,) = ctx.saved_tensors
+        if ctx.act not in (ACT_CODES['relu'], ACT_CODES['lrelu'], 0) and ctx.needs_input_grad[1]:
+            raise NotImplementedError('second derivative through tanh/sigmoid is not used by the step')
+        return ActBwdFn.apply(_as_bf16_grad(gg), y, ctx.act, ctx.slope), None, None, None
+
+
+class ChanSumFn(torch.autograd.Function):
+    """bias gradient: per-channel sum over pixels (fp32 [C])."""
+
+    @staticmethod
+    def forward(ctx, dz):
+        ctx.shape = tuple(dz.shape)
+        return chansum_raw(dz)
+
+    @staticmethod
+    def backward(ctx, gb):
+        N, C, H, W = ctx.shape
+        out = empty_nhwc(N, C, H, W, gb.device)
+        out.copy_(gb.view(1, C, 1, 1).expand(N, C, H, W))  # broadcast (never on the step's hot path)
+        return out
+
+
+class CastF32Bf16Fn(torch.autograd.Function):
+    """fp32 (N,C,H,W) NHWC-dense -> bf16 NHWC (used on grads of fp32-output convs)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N, C, H, W = x.shape
+        xc = x if (T.is_nhwc(x) and ld_of(x) == C) else x.contiguous(memory_format=torch.channels_last)
+        out = empty_nhwc(N, C, H, W, x.device)
+        ops.convert(xc.data_ptr(), N * H * W, C, out.data_ptr(), 0, ld_of(out), stream())
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return CastBf16F32Fn.apply(_as_bf16_grad(g))
+
+
+class CastBf16F32Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        N, C, H, W = x.shape
+        out = torch.empty((N, H, W, C), dtype=F32, device=x.device)
+        ops.nhwc_to_nchw(x.data_ptr(), ld_of(x), N * H * W, C, 1, out.data_ptr(), stream())
+        return out.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, g):
+        return CastF32Bf16Fn.apply(g)
+
+
+class ImageToNhwcFn(torch.autograd.Function):
+    """fp32 NCHW image (reference data layout) -> bf16 NHWC; grads return fp32 NCHW."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return to_nhwc_bf16(x.contiguous())
+
+    @staticmethod
+    def backward(ctx, g):
+        return ImageToNchwFn.apply(_as_bf16_grad(g))
+
+
+class ImageToNchwFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        N, C, H, W = x.shape
+        out = torch.empty((N, C, H, W), dtype=F32, device=x.device)
+        ops.nhwc_to_nchw(x.data_ptr(), ld_of(x), N, C, H * W, out.data_ptr(), stream())
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return ImageToNhwcFn.apply(g)
+
+
+# ===================================================== pool / combine =====
+class AvgPool2Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = to_nhwc_bf16(x)
+        N, C, H, W = x.shape
+        y = empty_nhwc(N, C, H // 2, W // 2, x.device)
+        ops.avgpool2(x.data_ptr(), N, H, W, C, ld_of(x), y.data_ptr(), ld_of(y), stream())
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        return AvgPool2AdjFn.apply(_as_bf16_grad(g))
+
+
+class AvgPool2AdjFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, g):
+        N, C, H, W = g.shape
+        dx = empty_nhwc(N, C, H * 2, W * 2, g.device)
+        ops.upsample2(g.data_ptr(), N, H, W, C, ld_of(g), 0.25, dx.data_ptr(), ld_of(dx), stream())
+        return dx
+
+    @staticmethod
+    def backward(ctx, gg):
+        return AvgPool2Fn.apply(_as_bf16_grad(gg))
+
+
+class Upsample2Fn(torch.autograd.Function):
+    """F.interpolate(x, scale_factor=2) (nearest); adjoint = 2x2 sum-pool."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = to_nhwc_bf16(x)
+        N, C, H, W = x.shape
+        y = empty_nhwc(N, C, H * 2, W * 2, x.device)
+        ops.upsample2(x.data_ptr(), N, H, W, C, ld_of(x), 1.0, y.data_ptr(), ld_of(y), stream())
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _as_bf16_grad(g)
+        N, C, H, W = g.shape
+        dx = empty_nhwc(N, C, H // 2, W // 2, g.device)
+        ops.sumpool2(g.data_ptr(), N, H, W, C, ld_of(g), dx.data_ptr(), ld_of(dx), stream())
+        return dx
+
+
+def _scale_raw(x, gamma, alpha=1.0):
+    N, C, H, W = x.shape
+    out = empty_nhwc(N, C, H, W, x.device)
+    ops.scale_add(0, 0, x.data_ptr(), ld_of(x), ptr(gamma), alpha, N * H * W, C, out.data_ptr(), ld_of(out), stream())
+    return out
+
+
+def _dot_raw(x, y):
+    N, C, H, W = x.shape
+    out = torch.empty(1, dtype=F32, device=x.device)
+    ws = workspace(ops.dot_workspace(), x.device)
+    ops.dot(x.data_ptr(), ld_of(x), ptr(y), ld_of(y) if y is not None else 0, N * H * W, C, 1.0, ws.data_ptr(),
+            out.data_ptr(), 0, stream())
+    return out
+
+
+class ScaleAddFn(torch.autograd.Function):
+    """out = res + gamma * h   (gamma: fp32 (1,) parameter; models.py:122,142,278)."""
+
+    @staticmethod
+    def forward(ctx, res, h, gamma):
+        res = to_nhwc_bf16(res)
+        h = to_nhwc_bf16(h)
+        N, C, H, W = h.shape
+        out = empty_nhwc(N, C, H, W, h.device)
+        ops.scale_add(res.data_ptr(), ld_of(res), h.data_ptr(), ld_of(h), gamma.data_ptr(), 1.0, N * H * W, C,
+                      out.data_ptr(), ld_of(out), stream())
+        ctx.save_for_backward(h, gamma)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        h, gamma = ctx.saved_tensors
+        g = _as_bf16_grad(g)
+        d_res = g if ctx.needs_input_grad[0] else None
+        d_h = ScaleFn.apply(g, gamma) if ctx.needs_input_grad[1] else None
+        d_g = DotFn.apply(g, h) if ctx.needs_input_grad[2] else None
+        return d_res, d_h, d_g
+
+
+class ScaleFn(torch.autograd.Function):
+    """gamma * x with gamma a device scalar."""
+
+    @staticmethod
+    def forward(ctx, x, gamma):
+        ctx.save_for_backward(x, gamma)
+        return _scale_raw(x, gamma)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, gamma = ctx.saved_tensors
+        g = _as_bf16_grad(g)
+        gx = ScaleFn.apply(g, gamma) if ctx.needs_input_grad[0] else None
+        gg = DotFn.apply(g, x) if ctx.needs_input_grad[1] else None
+        return gx, gg
+
+
+class DotFn(torch.autograd.Function):
+    """<x, y> summed over all elements -> fp32 (1,)."""
+
+    @staticmethod
+    def forward(ctx, x, y):
+        ctx.save_for_backward(x, y)
+        return _dot_raw(x, y)
+
+    @staticmethod
+    def backward(ctx, gs):
+        x, y = ctx.saved_tensors
+        gs = gs.reshape(1).contiguous()
+        gx = ScaleFn.apply(y, gs) if ctx.needs_input_grad[0] else None
+        gy = ScaleFn.apply(x, gs) if ctx.needs_input_grad[1] else None
+        return gx, gy
+
+
+class CatTileFn(torch.autograd.Function):
+    """torch.cat((feat, cond.view(-1,E,1,1).repeat(1,1,H,W)), 1) (models.py:302-304, 327-331)."""
+
+    @staticmethod
+    def forward(ctx, feat, cond):
+        feat = to_nhwc_bf16(feat)
+        cond = cond.reshape(cond.shape[0], -1).float().contiguous()
+        N, C, H, W = feat.shape
+        E = cond.shape[1]
+        out = empty_nhwc(N, C + E, H, W, feat.device)
+        ops.cat_tile(feat.data_ptr(), ld_of(feat), cond.data_ptr(), N, H * W, C, E, out.data_ptr(), ld_of(out),
+                     stream())
+        ctx.dims = (N, C, H, W, E)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return CatTileBwdFn.apply(_as_bf16_grad(g), ctx.dims)
+
+
+class CatTileBwdFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, g, dims):
+        N, C, H, W, E = dims
+        ctx.dims = dims
+        df = empty_nhwc(N, C, H, W, g.device)
+        dc = torch.empty((N, E), dtype=F32, device=g.device)
+        ops.cat_tile_bwd(g.data_ptr(), ld_of(g), N, H * W, C, E, df.data_ptr(), ld_of(df), dc.data_ptr(), stream())
+        return df, dc
+
+    @staticmethod
+    def backward(ctx, gf, gc):
+        N, C, H, W, E = ctx.dims
+        if gf is None:
+            gf = torch.zeros_like(empty_nhwc(N, C, H, W, gc.device))
+        if gc is None:
+            gc = torch.zeros((N, E), dtype=F32, device=gf.device)
+        return CatTileFn.apply(_as_bf16_grad(gf), gc), None
+
+
+class CatChannelsFn(torch.autograd.Function):
+    """torch.cat(parts, 1) for NHWC activations (Inception branch concat).  The
+    backward hands each branch a strided view of the incoming gradient (no copy)."""
+
+    @staticmethod
+    def forward(ctx, *parts):
+        parts = [to_nhwc_bf16(p) for p in parts]
+        N, _, H, W = parts[0].shape
+        Cs = [p.shape[1] for p in parts]
+        out = empty_nhwc(N, sum(Cs), H, W, parts[0].device)
+        ldo = ld_of(out)
+        off = 0
+        for p, c in zip(parts, Cs):
+            ops.scale_add(0, 0, p.data_ptr(), ld_of(p), 0, 1.0, N * H * W, c, out[:, off:off + c].data_ptr(), ldo,
+                          stream())
+            off += c
+        ctx.Cs = Cs
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _as_bf16_grad(g)
+        outs, off = [], 0
+        for c in ctx.Cs:
+            outs.append(g[:, off:off + c])
+            off += c
+        return tuple(outs)
+
+
+# ================================================================ linear ===
+class LinearFn(torch.autograd.Function):
+    """y = act(x W^T + b), fp32 (first order)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, act):
+        x2 = x.reshape(-1, x.shape[-1]).float().contiguous()
+        M, K = x2.shape
+        N = W.shape[0]
+        y = torch.empty((M, N), dtype=F32, device=x.device)
+        ops.gemm_f32(x2.data_ptr(), K, 1, W.data_ptr(), 1, K, y.data_ptr(), N, M, N, K, ptr(b), act, 1.0, 0.0,
+                     stream())
+        ctx.act = act
+        ctx.in_shape = tuple(x.shape)
+        ctx.save_for_backward(x2, W, y if act else None)
+        return y.reshape(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, W, y = ctx.saved_tensors
+        M, K = x2.shape
+        N = W.shape[0]
+        g = gy.reshape(M, N).float().contiguous()
+        if ctx.act:
+            dz = torch.empty_like(g)
+            ops.act_bwd_f32(g.data_ptr(), y.data_ptr(), M * N, ctx.act, 0.2, dz.data_ptr(), stream())
+            g = dz
+        dx = dW = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((M, K), dtype=F32, device=g.device)
+            ops.gemm_f32(g.data_ptr(), N, 1, W.data_ptr(), K, 1, dx.data_ptr(), K, M, K, N, 0, 0, 1.0, 0.0, stream())
+            dx = dx.reshape(ctx.in_shape)
+        if _needed(ctx, 1):
+            dW = torch.empty((N, K), dtype=F32, device=g.device)
+            ops.gemm_f32(g.data_ptr(), 1, N, x2.data_ptr(), K, 1, dW.data_ptr(), K, N, K, M, 0, 0, 1.0, 0.0, stream())
+        if ctx.needs_input_grad[2] and _needed(ctx, 2):
+            db = torch.empty(N, dtype=F32, device=g.device)
+            ops.colsum_f32(g.data_ptr(), N, M, N, db.data_ptr(), 0, stream())
+        return dx, dW, db, None
+
+
+# =========================================================== SyncBN path ===
+def _allreduce_f64(t):
+    if SYNC_BN_ALLREDUCE is not None and SYNC_BN_WORLD > 1:
+        SYNC_BN_ALLREDUCE(t)
+
+
+class BnModFn(torch.autograd.Function):
+    """SyncBN (training statistics) + affine / affine_ssa modulation + act,
+    optionally reading x through a nearest-2x upsample.  mode 0: affine BN
+    (w, b may be None); mode 1: (gam*m+1)*xhat + bet*m with gam/bet [N][C]
+    and m [N,1,Ho,Wo] fp32."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, gam, bet, mask, bn, mode, act, slope, up2):
+        x = to_nhwc_bf16(x)
+        N, C, H, W = x.shape
+        P = N * H * W
+        dev = x.device
+        s = stream()
+        count = float(P * (4 if up2 else 1))
+        # statistics (+ cross-rank all-reduce of (sum, sumsq))
+        ws = workspace(ops.bn_stats_workspace(P, C), dev)
+        sums = torch.empty(2 * C, dtype=torch.float64, device=dev)
+        ops.bn_stats(x.data_ptr(), P, C, ld_of(x), ws.data_ptr(), sums.data_ptr(), s)
+        world = SYNC_BN_WORLD
+        if world > 1:
+            _allreduce_f64(sums)
+            count *= world
+        stats = torch.empty(3 * C, dtype=F32, device=dev)
+        clamp_mode = 1 if world > 1 else 0
+        rm = bn.running_mean if (bn is not None and bn.track_running_stats) else None
+        rv = bn.running_var if rm is not None else None
+        ops.bn_finalize(sums.data_ptr(), C, count, bn.eps if bn is not None else 1e-5,
+                        bn.momentum if bn is not None else 0.1, clamp_mode, ptr(rm), ptr(rv), stats.data_ptr(), s)
+        # (the reference calls F.batch_norm directly, so num_batches_tracked never moves)
+        Ho, Wo = (H * 2, W * 2) if up2 else (H, W)
+        gam_c = gam.float().contiguous() if gam is not None else None
+        bet_c = bet.float().contiguous() if bet is not None else None
+        mask_c = mask.float().contiguous() if mask is not None else None
+        d = BnModDesc(x.data_ptr(), N, H, W, C, ld_of(x), int(up2), stats.data_ptr(), mode, ptr(w), ptr(b),
+                      ptr(gam_c), ptr(bet_c), ptr(mask_c), act, slope)
+        y = empty_nhwc(N, C, Ho, Wo, dev)
+        ops.bnmod_fwd(d, y.data_ptr(), ld_of(y), s)
+        ctx.meta = (mode, act, slope, up2, count)
+        ctx.save_for_backward(x, w, b, gam_c, bet_c, mask_c, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, b, gam, bet, mask, stats = ctx.saved_tensors
+        mode, act, slope, up2, count = ctx.meta
+        g = to_nhwc_bf16(g)
+        N, C, H, W = x.shape
+        dev = x.device
+        s = stream()
+        d = BnModDesc(x.data_ptr(), N, H, W, C, ld_of(x), int(up2), stats.data_ptr(), mode, ptr(w), ptr(b),
+                      ptr(gam), ptr(bet), ptr(mask), act, slope)
+        ws = workspace(ops.bnmod_bwd_workspace(d), dev)
+        if mode == 0:
+            d0 = torch.empty(C, dtype=F32, device=dev)
+            d1 = torch.empty(C, dtype=F32, device=dev)
+        else:
+            d0 = torch.empty((N, C), dtype=F32, device=dev)
+            d1 = torch.empty((N, C), dtype=F32, device=dev)
+        Ho, Wo = (H * 2, W * 2) if up2 else (H, W)
+        dmask = torch.empty((N, 1, Ho, Wo), dtype=F32, device=dev) if (mode == 1 and ctx.needs_input_grad[5]) else None
+        chan = torch.empty(2 * C, dtype=torch.float64, device=dev)
+        ops.bnmod_bwd(d, g.data_ptr(), ld_of(g), ws.data_ptr(), d0.data_ptr(), d1.data_ptr(), ptr(dmask),
+                      chan.data_ptr(), s)
+        _allreduce_f64(chan)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = empty_nhwc(N, C, H, W, dev)
+            ops.bnmod_bwd_dx(d, g.data_ptr(), ld_of(g), chan.data_ptr(), count, dx.data_ptr(), ld_of(dx), s)
+        if mode == 0:
+            dw = d0 if (w is not None and ctx.needs_input_grad[1]) else None
+            db = d1 if (b is not None and ctx.needs_input_grad[2]) else None
+            return dx, dw, db, None, None, None, None, None, None, None, None
+        dg = d0 if ctx.needs_input_grad[3] else None
+        dbt = d1 if ctx.needs_input_grad[4] else None
+        return dx, None, None, dg, dbt, dmask, None, None, None, None, None
+
+
+class BnEvalFn(torch.autograd.Function):
+    """eval-mode BN (running statistics) = per-channel affine + act (sampling only)."""
+
+    @staticmethod
+    def forward(ctx, x, scale, shift, act, slope, up2):
+        x = to_nhwc_bf16(x)
+        N, C, H, W = x.shape
+        C_ = scale.numel()
+        stats = torch.cat([torch.zeros(C_, device=x.device), torch.ones(C_, device=x.device),
+                           torch.ones(C_, device=x.device)]).float()
+        d = BnModDesc(x.data_ptr(), N, H, W, C, ld_of(x), int(up2), stats.data_ptr(), 0, scale.data_ptr(),
+                      shift.data_ptr(), 0, 0, 0, act, slope)
+        Ho, Wo = (H * 2, W * 2) if up2 else (H, W)
+        y = empty_nhwc(N, C, Ho, Wo, x.device)
+        ops.bnmod_fwd(d, y.data_ptr(), ld_of(y), stream())
+        ctx.save_for_backward(y, scale)
+        ctx.act, ctx.slope, ctx.up2 = act, slope, up2
+        return y
+
+    @staticmethod
+    def backward(ctx, g):  # not on the training path (G runs in train mode there)
+        y, scale = ctx.saved_tensors
+        g = to_nhwc_bf16(g)
+        dz = act_bwd_raw(g, y, ctx.act, ctx.slope) if ctx.act else g
+        dx = dz.float() * scale.view(1, -1, 1, 1)
+        if ctx.up2:
+            N, C, H, W = dx.shape
+            dx = dx.reshape(N, C, H // 2, 2, W // 2, 2).sum((3, 5))
+        return to_nhwc_bf16(dx.contiguous()), None, None, None, None, None
+
+
+# ================================================================= masks ===
+class MaskResizeSigmoidFn(torch.autograd.Function):
+    """sigmoid(F.interpolate(m, size, mode='bilinear', align_corners=True)) on
+    fp32 [N,1,h,w] masks (models.py:220-221, 231-232)."""
+
+    @staticmethod
+    def forward(ctx, m, size):
+        m = m.float().contiguous()
+        N, Cm, h, w = m.shape
+        out = torch.empty((N, Cm, size, size), dtype=F32, device=m.device)
+        ops.bilinear(m.data_ptr(), 1, N, h, w, Cm, Cm, size, size, 1, 1, out.data_ptr(), 1, Cm, stream())
+        ctx.dims = (N, Cm, h, w, size)
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (out,) = ctx.saved_tensors
+        N, Cm, h, w, size = ctx.dims
+        g = g.float().contiguous()
+        dm = torch.empty((N, Cm, h, w), dtype=F32, device=g.device)
+        ops.bilinear_bwd(g.data_ptr(), 1, out.data_ptr(), 1, Cm, N, h, w, Cm, size, size, 1, 1, dm.data_ptr(),
+                         stream())
+        return dm, None
+
+
+class BilinearFn(torch.autograd.Function):
+    """F.interpolate(x, size, mode='bilinear', align_corners=False) on bf16 NHWC
+    (CNN_ENCODER input resize, DAMSM.py:173)."""
+
+    @staticmethod
+    def forward(ctx, x, Ho, Wo):
+        x = to_nhwc_bf16(x)
+        N, C, H, W = x.shape
+        y = empty_nhwc(N, C, Ho, Wo, x.device)
+        ops.bilinear(x.data_ptr(), 0, N, H, W, C, ld_of(x), Ho, Wo, 0, 0, y.data_ptr(), 0, ld_of(y), stream())
+        ctx.dims = (N, C, H, W, Ho, Wo)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        N, C, H, W, Ho, Wo = ctx.dims
+        g = to_nhwc_bf16(g)
+        d32 = torch.empty((N, H, W, C), dtype=F32, device=g.device)
+        ops.bilinear_bwd(g.data_ptr(), 0, 0, 0, ld_of(g), N, H, W, C, Ho, Wo, 0, 0, d32.data_ptr(), stream())
+        dx = empty_nhwc(N, C, H, W, g.device)
+        ops.convert(d32.data_ptr(), N * H * W, C, dx.data_ptr(), 0, ld_of(dx), stream())
+        return dx, None, None
+
+
+class FcToNhwcFn(torch.autograd.Function):
+    """Gen.fc output (N, C*16) fp32 -> view(N, C, 4, 4) as NHWC bf16 (models.py:228-230)."""
+
+    @staticmethod
+    def forward(ctx, x, C):
+        x = x.float().contiguous()
+        N = x.shape[0]
+        y = empty_nhwc(N, C, 4, 4, x.device)
+        ops.fc_to_nhwc(x.data_ptr(), 1, N, C, 16, y.data_ptr(), ld_of(y), stream())
+        ctx.C = C
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        g = to_nhwc_bf16(g)
+        N = g.shape[0]
+        dx = torch.empty((N, ctx.C * 16), dtype=F32, device=g.device)
+        ops.nhwc_to_fc(g.data_ptr(), ld_of(g), N, ctx.C, 16, dx.data_ptr(), 1, stream())
+        return dx, None
+
+
+# ============================================================ Inception ====
+class MaxPool3s2Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = to_nhwc_bf16(x)
+        N, C, H, W = x.shape
+        Ho, Wo = (H - 3) // 2 + 1, (W - 3) // 2 + 1
+        y = empty_nhwc(N, C, Ho, Wo, x.device)
+        arg = torch.empty(N * Ho * Wo * C, dtype=torch.uint8, device=x.device)
+        ops.maxpool3s2(x.data_ptr(), N, H, W, C, ld_of(x), y.data_ptr(), ld_of(y), arg.data_ptr(), stream())
+        ctx.dims = (N, C, H, W)
+        ctx.save_for_backward(arg)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (arg,) = ctx.saved_tensors
+        N, C, H, W = ctx.dims
+        g = to_nhwc_bf16(g)
+        dx = empty_nhwc(N, C, H, W, g.device)
+        ops.maxpool3s2_bwd(g.data_ptr(), ld_of(g), arg.data_ptr(), N, H, W, C, dx.data_ptr(), ld_of(dx), stream())
+        return dx
+
+
+class AvgPool3s1Fn(torch.autograd.Function):
+    """avg_pool2d(3, 1, 1, count_include_pad=True): self-adjoint."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = to_nhwc_bf16(x)
+        N, C, H, W = x.shape
+        y = empty_nhwc(N, C, H, W, x.device)
+        ops.avgpool3s1(x.data_ptr(), N, H, W, C, ld_of(x), y.data_ptr(), ld_of(y), stream())
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        g = to_nhwc_bf16(g)
+        N, C, H, W = g.shape
+        dx = empty_nhwc(N, C, H, W, g.device)
+        ops.avgpool3s1(g.data_ptr(), N, H, W, C, ld_of(g), dx.data_ptr(), ld_of(dx), stream())
+        return dx
+
+
+class GlobalAvgPoolFn(torch.autograd.Function):
+    """mean over H*W -> fp32 (N, C)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = to_nhwc_bf16(x)
+        N, C, H, W = x.shape
+        y = torch.empty((N, C), dtype=F32, device=x.device)
+        ops.global_avgpool(x.data_ptr(), ld_of(x), N, H * W, C, y.data_ptr(), 1, stream())
+        ctx.dims = (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        N, C, H, W = ctx.dims
+        g = g.float().contiguous()
+        dx = empty_nhwc(N, C, H, W, g.device)
+        ops.global_avgpool_bwd(g.data_ptr(), 1, N, H * W, C, dx.data_ptr(), ld_of(dx), stream())
+        return dx
+
+
+# ================================================================ losses ===
+class DoutReduceFn(torch.autograd.Function):
+    """mode 0 mean(relu(1-x)), 1 mean(relu(1+x)), 2 -mean(x), 3 mean(x) (train.py:342-417)."""
+
+    @staticmethod
+    def forward(ctx, x, mode):
+        xc = x.float().contiguous()
+        out = torch.empty((), dtype=F32, device=x.device)
+        ops.dout_reduce(xc.data_ptr(), xc.numel(), mode, out.data_ptr(), stream())
+        ctx.mode = mode
+        ctx.shape = x.shape
+        ctx.save_for_backward(xc)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (xc,) = ctx.saved_tensors
+        g = g.float().reshape(1).contiguous()
+        dx = torch.empty_like(xc)
+        ops.dout_reduce_bwd(xc.data_ptr(), xc.numel(), ctx.mode, g.data_ptr(), dx.data_ptr(), stream())
+        return dx.reshape(ctx.shape), None
+
+
+class BceLogitsFn(torch.autograd.Function):
+    """F.binary_cross_entropy_with_logits(x, target) (mean)."""
+
+    @staticmethod
+    def forward(ctx, x, target):
+        xc = x.float().contiguous()
+        tc = target.float().contiguous()
+        out = torch.empty((), dtype=F32, device=x.device)
+        ops.bce_logits(xc.data_ptr(), tc.data_ptr(), xc.numel(), out.data_ptr(), stream())
+        ctx.save_for_backward(xc, tc)
+        ctx.shape = x.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        xc, tc = ctx.saved_tensors
+        g = g.float().reshape(1).contiguous()
+        dx = torch.empty_like(xc)
+        ops.bce_logits_bwd(xc.data_ptr(), tc.data_ptr(), xc.numel(), g.data_ptr(), dx.data_ptr(), stream())
+        return dx.reshape(ctx.shape), None
+
+
+class GradPenaltyFn(torch.autograd.Function):
+    """2 * mean_b ||[g_img_b, g_sent_b]||_2^6  (train.py:396-402)."""
+
+    @staticmethod
+    def forward(ctx, gx, gs):
+        gx = to_nhwc_bf16(gx)
+        gs = gs.float().reshape(gs.shape[0], -1).contiguous()
+        N, C, H, W = gx.shape
+        nrm2 = torch.empty(N, dtype=F32, device=gx.device)
+        out = torch.empty((), dtype=F32, device=gx.device)
+        ops.gp_loss(gx.data_ptr(), ld_of(gx), N, H * W, C, gs.data_ptr(), gs.shape[1], nrm2.data_ptr(),
+                    out.data_ptr(), stream())
+        ctx.save_for_backward(gx, gs, nrm2)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        gx, gs, nrm2 = ctx.saved_tensors
+        N, C, H, W = gx.shape
+        g = g.float().reshape(1).contiguous()
+        dgx = empty_nhwc(N, C, H, W, gx.device)
+        dgs = torch.empty_like(gs)
+        ops.gp_loss_bwd(gx.data_ptr(), ld_of(gx), N, H * W, C, gs.data_ptr(), gs.shape[1], nrm2.data_ptr(),
+                        g.data_ptr(), dgx.data_ptr(), ld_of(dgx), dgs.data_ptr(), stream())
+        return dgx, dgs
+
+
+def _class_ids_dev(class_ids, device):
+    if class_ids is None:
+        return None
+    t = torch.as_tensor(class_ids)
+    return t.to(device=device, dtype=torch.long).contiguous()
+
+
+class SimCEFn(torch.autograd.Function):
+    """(CE(sim, labels), CE(sim^T, labels)) with same-class off-diagonal -inf masking
+    (DAMSM_losses.py:238-245, 262-267, 326-338)."""
+
+    @staticmethod
+    def forward(ctx, sim, cls, labels=None):
+        simc = sim.float().contiguous()
+        B = simc.shape[0]
+        out = torch.empty(2, dtype=F32, device=sim.device)
+        ops.sim_ce(simc.data_ptr(), B, ptr(cls), ptr(labels), out.data_ptr(), stream())
+        ctx.save_for_backward(simc, cls, labels)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        simc, cls, labels = ctx.saved_tensors
+        g = g.float().contiguous()
+        d = torch.empty_like(simc)
+        ops.sim_ce_bwd(simc.data_ptr(), simc.shape[0], ptr(cls), ptr(labels), g.data_ptr(), d.data_ptr(), stream())
+        return d, None, None
+
+
+class WordsSimFn(torch.autograd.Function):
+    """similarity matrix of words_loss (DAMSM_losses.py:281-331) before masking."""
+
+    @staticmethod
+    def forward(ctx, regions, words, cap_lens, want_att):
+        # regions: (B, 256, 17, 17) fp32 NHWC-dense or NCHW
+        B = regions.shape[0]
+        if regions.dtype == F32 and T.is_nhwc(regions) and ld_of(regions) == regions.shape[1]:
+            reg = regions
+        else:
+            reg = regions.float().permute(0, 2, 3, 1).contiguous().permute(0, 3, 1, 2)
+        wd = words.float().contiguous()
+        lens = cap_lens.to(device=regions.device, dtype=torch.long).contiguous()
+        Tn = wd.shape[2]
+        sim = torch.empty((B, B), dtype=F32, device=regions.device)
+        att = torch.zeros((B, Tn, 289) if want_att else (0,), dtype=F32, device=regions.device)
+        ops.words_sim(reg.data_ptr(), wd.data_ptr(), lens.data_ptr(), B, Tn, sim.data_ptr(),
+                      att.data_ptr() if want_att else 0, stream())
+        ctx.save_for_backward(reg, wd, lens)
+        ctx.mark_non_differentiable(att)
+        return sim, att
+
+    @staticmethod
+    def backward(ctx, dsim, _datt):
+        reg, wd, lens = ctx.saved_tensors
+        B, Tn = wd.shape[0], wd.shape[2]
+        dsim = dsim.float().contiguous()
+        dreg = torch.empty((B, 17, 17, 256), dtype=F32, device=dsim.device)
+        dw = torch.empty_like(wd) if ctx.needs_input_grad[1] else None
+        ops.words_sim_bwd(reg.data_ptr(), wd.data_ptr(), lens.data_ptr(), B, Tn, dsim.data_ptr(), dreg.data_ptr(),
+                          ptr(dw), stream())
+        return dreg.permute(0, 3, 1, 2), dw, None, None
+
+
+class SentSimFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cnn, rnn):
+        c = cnn.float().contiguous()
+        r = rnn.float().contiguous()
+        B, Dm = c.shape
+        sim = torch.empty((B, B), dtype=F32, device=c.device)
+        ops.sent_sim(c.data_ptr(), r.data_ptr(), B, Dm, sim.data_ptr(), stream())
+        ctx.save_for_backward(c, r, sim)
+        return sim
+
+    @staticmethod
+    def backward(ctx, dsim):
+        c, r, sim = ctx.saved_tensors
+        B, Dm = c.shape
+        dsim = dsim.float().contiguous()
+        nrm = torch.empty(2 * B, dtype=F32, device=c.device)
+        dc = torch.empty_like(c) if ctx.needs_input_grad[0] else None
+        dr = torch.empty_like(r) if ctx.needs_input_grad[1] else None
+        ops.sent_sim_bwd(c.data_ptr(), r.data_ptr(), B, Dm, sim.data_ptr(), dsim.data_ptr(), nrm.data_ptr(), ptr(dc),
+                         ptr(dr), stream())
+        return dc, dr
+
+
+class AttrAttnFn(torch.autograd.Function):
+    """softmax(q k^T) / sqrt(d) v over the 4 rows [sent; attrs] (models.py:161-169)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, scale):
+        q, k, v = q.float().contiguous(), k.float().contiguous(), v.float().contiguous()
+        B, L, Dm = q.shape
+        probs = torch.empty((B, L, L), dtype=F32, device=q.device)
+        out = torch.empty_like(q)
+        ops.attr_attn(q.data_ptr(), k.data_ptr(), v.data_ptr(), B, L, Dm, scale, probs.data_ptr(), out.data_ptr(), 0,
+                      stream())
+        ctx.scale = scale
+        ctx.save_for_backward(q, k, v, probs)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        q, k, v, probs = ctx.saved_tensors
+        B, L, Dm = q.shape
+        g = g.float().contiguous()
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        ops.attr_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), probs.data_ptr(), g.data_ptr(), B, L, Dm,
+                          ctx.scale, dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), stream())
+        return dq, dk, dv, None
+
+
+def class_onehot(class_ids, B, ncls, device):
+    ids = _class_ids_dev(class_ids, device)
+    out = torch.empty((B, ncls), dtype=F32, device=device)
+    err = torch.zeros(1, dtype=torch.int32, device=device)
+    ops.class_onehot(ids.data_ptr(), B, ncls, out.data_ptr(), err.data_ptr(), stream())
+    return out, err

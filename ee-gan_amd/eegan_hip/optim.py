@@ -1,0 +1,96 @@
+"""Flat-buffer Adam on libeegan_hip.so (replaces torch.optim.Adam of
+train.py:252-263).
+
+All parameters of one optimizer are re-homed into ONE contiguous fp32
+buffer (parameters become views), their gradients into another, so
+zero_grad is one fill and step is one fused kernel launch.  With a process
+group, step() first averages the flat gradient buffer across ranks with
+bucketed RCCL all-reduces (data parallelism; train.py's DataParallel
+gradient reduction).  After each step a generation counter shared by the
+parameters is bumped so cached bf16 weight packs are rebuilt.
+"""
+import torch
+
+from ._lib import ops
+from .tensor import stream
+
+
+def _align(n, a=4):
+    return (n + a - 1) // a * a
+
+
+class FlatAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, process_group=None,
+                 bucket_bytes=64 << 20):
+        params = [p for p in params]
+        seen, uniq = set(), []
+        for p in params:
+            if id(p) not in seen:
+                seen.add(id(p))
+                uniq.append(p)
+        super().__init__(uniq, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self.process_group = process_group
+        self.bucket_elems = max(1, bucket_bytes // 4)
+        dev = uniq[0].device
+        offs, n = [], 0
+        for p in uniq:
+            offs.append(n)
+            n += _align(p.numel())
+        self.numel = n
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.gflat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.m = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(n, dtype=torch.float32, device=dev)
+        self._gen = [0]
+        self._views = []
+        with torch.no_grad():
+            for p, o in zip(uniq, offs):
+                k = p.numel()
+                self.flat[o:o + k].copy_(p.detach().reshape(-1).float())
+                p.data = self.flat[o:o + k].view_as(p)
+                g = self.gflat[o:o + k].view_as(p)
+                p.grad = g
+                p._eegan_gen = self._gen
+                self._views.append((p, o, k, g))
+        self.step_count = 0
+
+    def zero_grad(self, set_to_none=False):
+        ops.fill_f32(self.gflat.data_ptr(), self.numel, 0.0, stream())
+        for p, o, k, g in self._views:
+            if p.grad is None or p.grad.data_ptr() != g.data_ptr():
+                p.grad = g
+
+    def _sync_grads(self):
+        # gradients that autograd produced out of place (or dropped) are folded back in
+        for p, o, k, g in self._views:
+            if p.grad is None:
+                p.grad = g
+                g.zero_()
+            elif p.grad.data_ptr() != g.data_ptr():
+                g.copy_(p.grad)
+                p.grad = g
+
+    def _allreduce(self):
+        import torch.distributed as dist
+        if self.process_group is None or not dist.is_initialized() or dist.get_world_size(self.process_group) == 1:
+            return
+        world = dist.get_world_size(self.process_group)
+        for s in range(0, self.numel, self.bucket_elems):
+            dist.all_reduce(self.gflat[s:s + self.bucket_elems], group=self.process_group)
+        self.gflat.mul_(1.0 / world)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        self._sync_grads()
+        self._allreduce()
+        g = self.param_groups[0]
+        b1, b2 = g['betas']
+        self.step_count += 1
+        t = self.step_count
+        bc1 = 1 - b1 ** t
+        bc2 = 1 - b2 ** t
+        ops.adam(self.flat.data_ptr(), self.gflat.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.numel, b1, b2,
+                 g['lr'] / bc1, bc2 ** 0.5, g['eps'], g['weight_decay'], stream())
+        self._gen[0] += 1
+        return loss

@@ -1,0 +1,226 @@
+"""The EE-GAN inner G/D training step on MI355X (mirror of train.py:90-103,
+148-206, 252-263, 336-502).
+
+Method names, arguments and the order of operations follow the reference
+Trainer so the step reads like train.py; the arithmetic of every loss runs in
+HIP kernels (hinge means, BCE-with-logits, the MA gradient penalty, masked
+bidirectional CE of the DAMSM losses), the optimizers are flat fused Adams,
+and nothing in the step reads device memory on the host (no .item(), no
+cap_lens.tolist()).  Scalar loss combinations stay torch expressions on
+0-d tensors.
+"""
+import torch
+
+from . import functional as Fn
+from . import dist as D
+from .optim import FlatAdam
+
+
+def prepare_labels(batch_size, device):
+    """train.py:90-97."""
+    real = torch.ones(batch_size, device=device)
+    fake = torch.zeros(batch_size, device=device)
+    match = torch.arange(batch_size, device=device)
+    return real, fake, match
+
+
+def prepare_class_labels(batch_size, class_num, class_ids, device):
+    """train.py:99-103 on the device: labels[i][(id_i - 1) mod class_num] = 1 (bit-exact)."""
+    lab, _ = Fn.class_onehot(class_ids, batch_size, class_num, device)
+    return lab
+
+
+class Trainer(object):
+    def __init__(self, netG, attr_enhance, netsD, image_encoder, text_encoder, batch_size, disc_class=True,
+                 class_nums=200, class_coe=10.0, sim_coe=0.05, device='cuda', max_attr_nums=3, damsm_global=True):
+        self.netG, self.attr_enhance, self.netsD = netG, attr_enhance, netsD
+        self.image_encoder, self.text_encoder = image_encoder, text_encoder
+        self.batch_size = batch_size
+        self.disc_class, self.class_nums = disc_class, class_nums
+        self.d_class_coe = self.g_class_coe = class_coe
+        self.DAMSM_coe = sim_coe
+        self.device = device
+        self.max_attr_nums = max_attr_nums
+        self.damsm_global = damsm_global
+        self.optimizerG, self.optimizerDs = self.load_optimizers(netG, netsD, attr_enhance)
+        self.records = {}
+
+    @staticmethod
+    def load_optimizers(netG, netDs, attr_enhance):
+        """train.py:252-263: Adam(betas=(0, 0.9)), G+ATTR lr 1e-4, each D lr 4e-4."""
+        pg = torch.distributed.group.WORLD if D.is_on() else None
+        EG = [p for p in list(netG.parameters()) + list(attr_enhance.parameters()) if p.requires_grad]
+        optG = FlatAdam(EG, lr=0.0001, betas=(0.0, 0.9), process_group=pg)
+        optDs = [FlatAdam([p for p in d.parameters() if p.requires_grad], lr=0.0004, betas=(0.0, 0.9),
+                          process_group=pg) for d in netDs]
+        return optG, optDs
+
+    # ------------------------------------------------------------ losses --
+    @staticmethod
+    def d_loss(imgs, fake_imgs, sent_emb, wrong_sent_emb, netD):
+        """train.py:336-353."""
+        real_features = netD(imgs)
+        real_out = netD.module.COND_DNET(real_features, sent_emb)
+        errD_real = Fn.DoutReduceFn.apply(real_out, 0)
+        unpair_out = netD.module.COND_DNET(real_features, wrong_sent_emb)
+        errD_mismatch = Fn.DoutReduceFn.apply(unpair_out, 1)
+        fake_features = netD(fake_imgs.detach())
+        fake_out = netD.module.COND_DNET(fake_features, sent_emb)
+        errD_fake = Fn.DoutReduceFn.apply(fake_out, 1)
+        return errD_real, errD_fake, errD_mismatch
+
+    @staticmethod
+    def d_loss_class(imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, netD):
+        """train.py:355-376."""
+        real_feature = netD(imgs)
+        real_sent_out, real_class_out = netD.module.COND_DNET(real_feature, sent_emb)
+        errD_real = Fn.DoutReduceFn.apply(real_sent_out, 0)
+        errD_real_class = Fn.BceLogitsFn.apply(real_class_out, class_labels)
+        unpair_sent_out, unpair_class_out = netD.module.COND_DNET(real_feature, unpair_sent_emb)
+        errD_mismatch = Fn.DoutReduceFn.apply(unpair_sent_out, 1)
+        errD_mismatch_class = Fn.BceLogitsFn.apply(unpair_class_out, class_labels)
+        fake_features = netD(fake_imgs.detach())
+        fake_sent_out, fake_class_out = netD.module.COND_DNET(fake_features, sent_emb)
+        errD_fake = Fn.DoutReduceFn.apply(fake_sent_out, 1)
+        errD_fake_class = Fn.BceLogitsFn.apply(fake_class_out, class_labels)
+        return errD_real, errD_fake, errD_mismatch, errD_real_class, errD_fake_class, errD_mismatch_class
+
+    @staticmethod
+    def MA_gradient_penalty(imgs, sent_emb, netD, disc_class):
+        """train.py:378-402: 2 * mean(||d D(x,s) / d(x,s)||^6), double backward."""
+        interpolated = imgs.detach().requires_grad_()
+        sent_inter = sent_emb.detach().requires_grad_()
+        features = netD(interpolated)
+        if disc_class:
+            out, _ = netD.module.COND_DNET(features, sent_inter)
+        else:
+            out = netD.module.COND_DNET(features, sent_inter)
+        grads = torch.autograd.grad(outputs=out, inputs=(interpolated, sent_inter), grad_outputs=torch.ones_like(out),
+                                    retain_graph=True, create_graph=True, only_inputs=True)
+        return Fn.GradPenaltyFn.apply(grads[0], grads[1])
+
+    @staticmethod
+    def g_loss_class(fake_imgs, sent_emb, class_labels, netD):
+        features = netD(fake_imgs)
+        fake_sent, fake_class = netD.module.COND_DNET(features, sent_emb)
+        return Fn.DoutReduceFn.apply(fake_sent, 2), Fn.BceLogitsFn.apply(fake_class, class_labels)
+
+    @staticmethod
+    def g_loss(fake_imgs, sent_emb, netD):
+        features = netD(fake_imgs)
+        return Fn.DoutReduceFn.apply(netD.module.COND_DNET(features, sent_emb), 2)
+
+    def DAMSM_loss(self, fake_imgs, sent_emb, words_embs, attrs_emb, class_ids, batch_size, match_labels, cap_lens,
+                   image_encoder):
+        """train.py:419-435 over the GLOBAL batch when data-parallel."""
+        region_features, cnn_code = image_encoder(fake_imgs)
+        if self.damsm_global and D.world_size() > 1:
+            region_features = D.all_gather(region_features)
+            cnn_code = D.all_gather(cnn_code)
+            sent_emb = D.all_gather(sent_emb, differentiable=False)
+            attrs_emb = D.all_gather(attrs_emb)
+            words_embs = D.all_gather(words_embs, differentiable=False)
+            cap_lens = D.all_gather(torch.as_tensor(cap_lens, device=sent_emb.device), differentiable=False)
+            class_ids = D.all_gather(class_ids, differentiable=False) if class_ids is not None else None
+            batch_size = batch_size * D.world_size()
+            match_labels = torch.arange(batch_size, device=sent_emb.device)
+        s = Fn.SimCEFn.apply(Fn.SentSimFn.apply(cnn_code, sent_emb), class_ids, match_labels)
+        wsim, _ = Fn.WordsSimFn.apply(region_features, words_embs, cap_lens, False)
+        w = Fn.SimCEFn.apply(wsim, class_ids, match_labels)
+        a = Fn.SimCEFn.apply(Fn.SentSimFn.apply(cnn_code, attrs_emb), class_ids, match_labels)
+        lam = 1.0
+        return (w[0] + w[1]) * lam, (s[0] + s[1]) * lam, (a[0] + a[1]) * lam
+
+    # ----------------------------------------------------------- updates --
+    def d_update(self, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec=False):
+        """train.py:437-469: per D a hinge(+class) step, then a GP step."""
+        for i in range(len(self.netsD)):
+            real_img, fake_img, netD, optD = imgs[i], fake_imgs[i], self.netsD[i], self.optimizerDs[i]
+            disc_class = self.disc_class and i == 2
+            if disc_class:
+                e_real, e_fake, e_unpair, c_real, c_fake, c_unpair = self.d_loss_class(
+                    real_img, fake_img, sent_emb, unpair_sent_emb, class_labels, netD)
+                d_loss = e_real + (e_fake + e_unpair) / 2.0 + (c_real + c_fake + c_unpair) / 3.0 * self.d_class_coe
+            else:
+                e_real, e_fake, e_unpair = self.d_loss(real_img, fake_img, sent_emb, unpair_sent_emb, netD)
+                d_loss = e_real + (e_fake + e_unpair) / 2.0
+            optD.zero_grad()
+            d_loss.backward()
+            optD.step()
+            d_loss_gp = self.MA_gradient_penalty(real_img, sent_emb, netD, disc_class)
+            optD.zero_grad()
+            d_loss_gp.backward()
+            optD.step()
+            if iter_rec:
+                self.records['errD_%d/real_sent' % i] = e_real.detach()
+                self.records['errD_%d/fake_sent' % i] = e_fake.detach()
+                self.records['errD_%d/unpair_sent' % i] = e_unpair.detach()
+                self.records['errD_%d/d_loss_gp' % i] = d_loss_gp.detach()
+                if disc_class:
+                    self.records['errD_%d/real_class' % i] = c_real.detach()
+                    self.records['errD_%d/fake_class' % i] = c_fake.detach()
+                    self.records['errD_%d/mismatch_class' % i] = c_unpair.detach()
+
+    def g_update(self, fake_imgs, sent_emb, words_emb, attr_emb, class_ids, batch_size, match_labels, cap_lens,
+                 class_labels, iter_rec=False):
+        """train.py:471-502."""
+        g_loss = None
+        for i in range(len(self.netsD)):
+            fake_img, netD = fake_imgs[i], self.netsD[i]
+            if self.disc_class and i == 2:
+                errG, errG_class = self.g_loss_class(fake_img, sent_emb, class_labels, netD)
+                term = errG + errG_class * self.g_class_coe
+            else:
+                errG = self.g_loss(fake_img, sent_emb, netD)
+                term = errG
+            g_loss = term if g_loss is None else g_loss + term
+            if iter_rec:
+                self.records['errG/G_%d_fake_sent' % i] = errG.detach()
+                if self.disc_class and i == 2:
+                    self.records['errG/G_%d_fake_class' % i] = errG_class.detach()
+        w_loss, s_loss, a_loss = self.DAMSM_loss(fake_imgs[-1], sent_emb, words_emb, attr_emb, class_ids, batch_size,
+                                                 match_labels, cap_lens, self.image_encoder)
+        g_loss = g_loss + self.DAMSM_coe * (s_loss + w_loss + a_loss)
+        if iter_rec:
+            self.records['errG/s_loss'] = s_loss.detach()
+            self.records['errG/w_loss'] = w_loss.detach()
+            self.records['errG/a_loss'] = a_loss.detach()
+        self.optimizerG.zero_grad()
+        g_loss.backward()
+        self.optimizerG.step()
+        return g_loss.detach()
+
+    # -------------------------------------------------------- inner step --
+    def encode_text(self, batch):
+        """train.py:169-184: 5 frozen text-encoder calls (captions, 3 attributes, unpaired)."""
+        enc = self.text_encoder
+        with torch.no_grad():
+            words, sent = enc(batch['caps'], batch['cap_lens'], None, max_len=batch.get('max_len'))
+            attrs = []
+            for i in range(self.max_attr_nums):
+                _, a = enc(batch['attrs'][:, i, :], batch['attrs_len'][:, i], None, max_len=batch['attrs'].shape[2])
+                attrs.append(a)
+            attrs = torch.stack(attrs, dim=1)
+            _, unpair = enc(batch['unpair_caps'], batch['unpair_cap_lens'], None,
+                            max_len=batch['unpair_caps'].shape[1])
+        return words, sent, attrs, unpair
+
+    def train_step(self, batch, noise=None, emb=None, iter_rec=False):
+        """One iteration of train.py:163-206 on a device-resident batch."""
+        B = self.batch_size
+        dev = self.device
+        words, sent, attrs, unpair = emb if emb is not None else self.encode_text(batch)
+        class_labels = None
+        if self.disc_class:
+            class_labels = prepare_class_labels(B, self.class_nums, batch['cls_ids'], dev)
+        if noise is None:
+            noise = torch.randn(B, 100, device=dev)
+        _, attn_attr_emb = self.attr_enhance(sent, attrs)
+        attn_attr_emb = self.attr_enhance.module.attr_merge(attn_attr_emb)
+        fake_imgs = self.netG(noise, sent, attn_attr_emb)
+        self.d_update(batch['imgs'], fake_imgs, sent, unpair, class_labels, iter_rec)
+        _, _, match_labels = prepare_labels(B, dev)
+        cls_ids = batch.get('cls_ids')  # train.py:490 passes class ids to DAMSM_loss even without USE_CLASS
+        g = self.g_update(fake_imgs, sent, words, attn_attr_emb, cls_ids, B, match_labels, batch['cap_lens'],
+                          class_labels, iter_rec)
+        return fake_imgs, g

@@ -1,0 +1,125 @@
+"""DAMSM text-image matching losses (API of miscc/DAMSM_losses.py).
+
+Hot path: ``words_loss`` (DAMSM_losses.py:272-342) and ``sent_loss``
+(233-270) run as fused HIP kernels: ONE launch computes func_attention
+(25-63), the word-level cosine similarity (17-23) and the log-sum-exp row
+similarity for all B^2 (image, text) pairs, one launch applies the
+same-class -inf mask and the bidirectional cross-entropy, and the backward
+recomputes the attention in-kernel (no per-sample Python loop, no
+``cap_lens.tolist()`` host sync).
+
+``cosine_similarity``, ``func_attention``, ``GlobalAttentionGeneral``,
+``sent_similarity`` and ``words_similarity`` are kept for API completeness
+(the reference never calls them on the training path) and are thin tensor
+expressions.
+"""
+import torch
+import torch.nn as nn
+
+from miscc.config import cfg
+from eegan_hip import functional as Fn
+
+
+def cosine_similarity(x1, x2, dim=1, eps=1e-8):
+    w12 = torch.sum(x1 * x2, dim)
+    return (w12 / (torch.norm(x1, 2, dim) * torch.norm(x2, 2, dim)).clamp(min=eps)).squeeze()
+
+
+def func_attention(query, context, gamma1):
+    B, L = query.size(0), query.size(2)
+    ih, iw = context.size(2), context.size(3)
+    ctx = context.reshape(B, -1, ih * iw)
+    a = torch.softmax(torch.bmm(ctx.transpose(1, 2), query).reshape(B * ih * iw, L), dim=1)
+    a = a.reshape(B, ih * iw, L).transpose(1, 2).reshape(B * L, ih * iw)
+    a = torch.softmax(a * gamma1, dim=1).reshape(B, L, ih * iw)
+    return torch.bmm(ctx, a.transpose(1, 2)), a.reshape(B, -1, ih, iw)
+
+
+class GlobalAttentionGeneral(nn.Module):
+    """word <-> feature-map attention (DAMSM_losses.py:65-132; unused by the reference step)."""
+
+    def __init__(self, idf, cdf):
+        super().__init__()
+        self.sm = nn.Softmax(dim=1)
+        self.mask = None
+
+    def applyMask(self, mask):
+        self.mask = mask
+
+    def forward(self, input, context_key, content_value):
+        B, _, ih, iw = input.shape
+        Lq = ih * iw
+        S = context_key.size(2)
+        attn = torch.bmm(input.reshape(B, -1, Lq).transpose(1, 2), context_key).reshape(B * Lq, S)
+        if self.mask is not None:
+            attn = attn.masked_fill(self.mask.repeat(Lq, 1), -float('inf'))
+        attn = self.sm(attn).reshape(B, Lq, S).transpose(1, 2)
+        wc = torch.bmm(content_value, attn)
+        return wc.reshape(B, -1, ih, iw), attn.reshape(B, -1, ih, iw)
+
+
+def _cls_dev(class_ids, device):
+    if class_ids is None:
+        return None
+    return torch.as_tensor(class_ids).to(device=device, dtype=torch.long, non_blocking=True).contiguous()
+
+
+def _labels_dev(labels, device):
+    if labels is None:
+        return None
+    return torch.as_tensor(labels).to(device=device, dtype=torch.long, non_blocking=True).contiguous()
+
+
+def sent_similarity(cnn_code, rnn_code, class_ids, batch_size, eps=1e-8):
+    sim = Fn.SentSimFn.apply(cnn_code, rnn_code)
+    cls = _cls_dev(class_ids, sim.device)
+    if cls is not None:
+        m = (cls[None, :] == cls[:batch_size, None]) & ~torch.eye(batch_size, dtype=torch.bool, device=sim.device)
+        sim = sim.masked_fill(m, -float('inf'))
+    return sim
+
+
+def sent_loss(cnn_code, rnn_code, labels, class_ids, batch_size, eps=1e-8):
+    """(CE(scores, labels), CE(scores^T, labels)); scores = gamma3 * cos, same-class masked."""
+    if labels is None:
+        return None, None
+    sim = Fn.SentSimFn.apply(cnn_code, rnn_code)
+    losses = Fn.SimCEFn.apply(sim, _cls_dev(class_ids, sim.device), _labels_dev(labels, sim.device))
+    return losses[0], losses[1]
+
+
+class _AttMaps(object):
+    """Lazy ``att_maps`` list of words_loss: element i is attn of (text i, image i),
+    shape (1, w_i, 17, 17).  Materialised (with a host read of cap_lens) only on access."""
+
+    def __init__(self, att, cap_lens):
+        self._att, self._lens = att, cap_lens
+
+    def __len__(self):
+        return self._att.shape[0]
+
+    def __getitem__(self, i):
+        w = int(self._lens[i])
+        return self._att[i, :w].reshape(1, w, 17, 17)
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+
+def words_similarity(img_features, words_emb, cap_lens, class_ids, batch_size):
+    sim, att = Fn.WordsSimFn.apply(img_features, words_emb, torch.as_tensor(cap_lens), True)
+    cls = _cls_dev(class_ids, sim.device)
+    if cls is not None:
+        m = (cls[None, :] == cls[:batch_size, None]) & ~torch.eye(batch_size, dtype=torch.bool, device=sim.device)
+        sim = sim.masked_fill(m, -float('inf'))
+    return sim, _AttMaps(att, cap_lens)
+
+
+def words_loss(img_features, words_emb, labels, cap_lens, class_ids, batch_size):
+    """Returns (loss0, loss1, att_maps) like DAMSM_losses.py:272-342."""
+    sim, att = Fn.WordsSimFn.apply(img_features, words_emb, torch.as_tensor(cap_lens), True)
+    maps = _AttMaps(att, cap_lens)
+    if labels is None:
+        return None, None, maps
+    losses = Fn.SimCEFn.apply(sim, _cls_dev(class_ids, sim.device), _labels_dev(labels, sim.device))
+    return losses[0], losses[1], maps

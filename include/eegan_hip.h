@@ -1,0 +1,204 @@
+/*
+ * eegan_hip.h -- C ABI of libeegan_hip.so, the MI355X (gfx950) kernel library
+ * behind EE-GAN's data-parallel G+D training step.
+ *
+ * Conventions
+ *  - Activations: NHWC, bf16 stored as uint16_t, channel stride `ld`
+ *    (ld == C for C < 8, else ld % 8 == 0 and ld >= round_up(C, 8)).
+ *  - Parameters / statistics / losses: fp32.
+ *  - Every entry point is asynchronous on the `hipStream_t` it is given,
+ *    never allocates or frees (the caller owns all memory, including
+ *    workspaces sized by the *_workspace queries), keeps no global mutable
+ *    state (safe to call concurrently from several threads/devices) and
+ *    returns 0 or a negative error code; eegan_last_error() then returns a
+ *    thread-local description.
+ *  - "replaces" names the reference (qikizh/EE-GAN) code each entry point
+ *    stands in for (file:line under the reference root).
+ */
+#ifndef EEGAN_HIP_H
+#define EEGAN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EEGAN_ABI_VERSION 1
+
+const char* eegan_last_error(void);
+int eegan_abi_version(void);
+
+/* ------------------------------------------------------------------ conv --
+ * replaces: every nn.Conv2d / nn.Linear forward+backward of models.py:14-403
+ * (conv1x1/conv3x3/conv4x4 helpers 14-23, SAGB c1/c2/c_sc 97-103, Cum_Block
+ * 132-137, get_image/get_mask 25-41, resD 267-274, DiscSent/DiscCond 296-321,
+ * Dis* conv_img 343/361/381) and DAMSM.py CNN_ENCODER's Inception convs.
+ * A Linear(in, out) is the 1x1 conv over an (N,1,1,in) tensor. */
+typedef struct eegan_conv_desc {
+  int N, H, W, C, ldx;  /* input; (H, W) is the LOGICAL grid (physical H/2 x W/2 when up2) */
+  int K, R, S;          /* output channels, kernel height/width */
+  int stride, pad_h, pad_w;
+  int up2;              /* 1: input is nearest-2x upsampled on the fly (F.interpolate(x, 2)) */
+  int Ho, Wo, ldy;      /* output grid and channel stride */
+} eegan_conv_desc;
+
+/* elements of the packed bf16 weight image; Cg = eegan_conv_gather_channels(C_gathered, ld) */
+long eegan_conv_packed_elems(int Cout, int Cin, int R, int S, int transposed, int Cg);
+int eegan_conv_gather_channels(int C, int ld);
+/* torch layout W[Cout][Cin][R][S] fp32 (x optional per-Cout scale) -> packed bf16.
+ * transposed=0: forward image [Cout][R][S][Cg(Cin)]; 1: bwd-data image [Cin][R][S][Cg(Cout)] */
+int eegan_conv_pack_weights(const float* w, const float* scale, int Cout, int Cin, int R, int S,
+                            int transposed, int Cg, uint16_t* out, hipStream_t stream);
+/* y = res + gamma * act(conv(x, W) + bias)   (res/gamma optional; act: 0 none,1 relu,2 lrelu,3 tanh,4 sigmoid) */
+int eegan_conv_fwd(const eegan_conv_desc* d, const uint16_t* x, const uint16_t* wpack, const float* bias,
+                   int act, float slope, const uint16_t* res, int ldres, const float* gamma, void* y,
+                   int y_f32, hipStream_t stream);
+/* dx (logical input grid, channel stride lddx) = conv_transpose(dy, W) */
+int eegan_conv_bwd_data(const eegan_conv_desc* d, const uint16_t* dy, const uint16_t* wpackT, void* dx,
+                        int lddx, int dx_f32, hipStream_t stream);
+/* dW[Cout][Cin][R][S] (fp32, torch layout) = sum_pixels dy x im2col(x); split-K slabs in ws */
+long eegan_conv_wgrad_workspace(const eegan_conv_desc* d);
+int eegan_conv_bwd_weight(const eegan_conv_desc* d, const uint16_t* x, const uint16_t* dy, float* ws, float* dw,
+                          int accumulate, hipStream_t stream);
+
+/* ----------------------------------------------------- SyncBN / modulation --
+ * replaces: sync_batchnorm/batchnorm.py:48-125 (statistics, running buffers,
+ * clamp(var,eps) multi-replica formula), models.py:69-86 (affine_ssa) and the
+ * ReLU/LeakyReLU after every BN (models.py:28,38,115,118); the nearest-2x
+ * upsample of models.py:219 is folded in via up2. */
+long eegan_bn_stats_workspace(long P, int C);
+/* sums[0..C) = sum x, sums[C..2C) = sum x^2 (fp64) over P pixels */
+int eegan_bn_stats(const uint16_t* x, long P, int C, int ld, float* ws, double* sums, hipStream_t stream);
+/* stats[3C] = (mean, inv_std, var-grad flag); updates running buffers (nullable) */
+int eegan_bn_finalize(const double* sums, int C, double count, float eps, float momentum, int clamp_mode,
+                      float* running_mean, float* running_var, float* stats, hipStream_t stream);
+
+typedef struct eegan_bnmod_desc {
+  const uint16_t* x;  /* input (physical grid N x H x W, channel stride ldx) */
+  int N, H, W, C, ldx;
+  int up2;            /* output grid is (2H, 2W) */
+  const float* stats; /* from eegan_bn_finalize */
+  int mode;           /* 0: affine BN  t = act(xhat*w + b)   1: affine_ssa t = act((gam*m+1)*xhat + bet*m) */
+  const float* w;     /* [C] (mode 0, nullable) */
+  const float* b;     /* [C] (mode 0, nullable) */
+  const float* gam;   /* [N][C] (mode 1) */
+  const float* bet;   /* [N][C] (mode 1) */
+  const float* mask;  /* [N][Ho*Wo] fp32 (mode 1) */
+  int act;            /* 0 none, 1 relu, 2 lrelu */
+  float slope;
+} eegan_bnmod_desc;
+
+int eegan_bnmod_fwd(const eegan_bnmod_desc* d, uint16_t* y, int ldy, hipStream_t stream);
+long eegan_bnmod_bwd_workspace(const eegan_bnmod_desc* d);
+/* pass 1: dparam0/1 = (dw, db) [C] (mode 0) or (dgam, dbet) [N][C] (mode 1); dmask [N][Ho*Wo];
+ * chan[2C] (fp64) = (sum dxhat, sum dxhat*xhat) -- all-reduce these across ranks for SyncBN */
+int eegan_bnmod_bwd(const eegan_bnmod_desc* d, const uint16_t* dt, int lddt, float* ws, float* dparam0,
+                    float* dparam1, float* dmask, double* chan, hipStream_t stream);
+/* pass 2: dx on the physical input grid (2x2 children summed when up2) */
+int eegan_bnmod_bwd_dx(const eegan_bnmod_desc* d, const uint16_t* dt, int lddt, const double* chan, double count,
+                       uint16_t* dx, int lddx, hipStream_t stream);
+
+/* ------------------------------------------------------------ elementwise --
+ * replaces: activation backward (models.py:28-30,38,115-118,269-271),
+ * F.avg_pool2d(x,2) (models.py:284), nearest upsample (models.py:134,219),
+ * shortcut + gamma*residual (models.py:122,142,278), cond.repeat+cat
+ * (models.py:302-304,327-331), F.interpolate bilinear (models.py:220,
+ * DAMSM.py:173), sigmoid (models.py:221,232), Inception pools (DAMSM.py:181-218),
+ * Gen.fc view (models.py:228-230). */
+int eegan_act_bwd(const uint16_t* dy, int lddy, const uint16_t* y, int ldy, long P, int C, int act, float slope,
+                  uint16_t* dx, int lddx, hipStream_t s);
+int eegan_scale_add(const uint16_t* x, int ldx, const uint16_t* y, int ldy, const float* gamma, float alpha, long P,
+                    int C, uint16_t* out, int ldo, hipStream_t s);
+long eegan_dot_workspace(void);
+int eegan_dot(const uint16_t* x, int ldx, const uint16_t* y, int ldy, long P, int C, float scale, float* ws,
+              float* out, int accumulate, hipStream_t s);
+long eegan_chansum_workspace(long P, int C);
+int eegan_chansum(const uint16_t* x, int ld, long P, int C, float* ws, float* out, int accumulate, hipStream_t s);
+int eegan_avgpool2(const uint16_t* x, int N, int H, int W, int C, int ld, uint16_t* y, int ldy, hipStream_t s);
+int eegan_upsample2(const uint16_t* x, int N, int H, int W, int C, int ld, float scale, uint16_t* y, int ldy,
+                    hipStream_t s);
+int eegan_sumpool2(const uint16_t* x, int N, int H, int W, int C, int ld, uint16_t* y, int ldy, hipStream_t s);
+int eegan_cat_tile(const uint16_t* feat, int ldf, const float* cond, int N, int HW, int C, int E, uint16_t* out,
+                   int ldo, hipStream_t s);
+int eegan_cat_tile_bwd(const uint16_t* dout, int ldo, int N, int HW, int C, int E, uint16_t* dfeat, int ldf,
+                       float* dcond, hipStream_t s);
+int eegan_bilinear(const void* x, int x_f32, int N, int H, int W, int C, int ld, int Ho, int Wo, int align_corners,
+                   int post, void* y, int y_f32, int ldy, hipStream_t s);
+int eegan_bilinear_bwd(const void* dy, int dy_f32, const void* y, int y_f32, int lddy, int N, int H, int W, int C,
+                       int Ho, int Wo, int align_corners, int post, float* dx32, hipStream_t s);
+int eegan_convert(const float* x, long P, int C, void* y, int y_f32, int ldy, hipStream_t s);
+int eegan_nchw_to_nhwc(const float* x, int N, int C, int HW, uint16_t* y, int ldy, hipStream_t s);
+int eegan_nhwc_to_nchw(const uint16_t* x, int ldx, int N, int C, int HW, float* y, hipStream_t s);
+int eegan_fc_to_nhwc(const void* x, int x_f32, int N, int C, int HW, uint16_t* y, int ldy, hipStream_t s);
+int eegan_nhwc_to_fc(const uint16_t* y, int ldy, int N, int C, int HW, void* x, int x_f32, hipStream_t s);
+int eegan_maxpool3s2(const uint16_t* x, int N, int H, int W, int C, int ld, uint16_t* y, int ldy, uint8_t* arg,
+                     hipStream_t s);
+int eegan_maxpool3s2_bwd(const uint16_t* dy, int lddy, const uint8_t* arg, int N, int H, int W, int C, uint16_t* dx,
+                         int lddx, hipStream_t s);
+int eegan_avgpool3s1(const uint16_t* x, int N, int H, int W, int C, int ld, uint16_t* y, int ldy, hipStream_t s);
+int eegan_global_avgpool(const uint16_t* x, int ld, int N, int HW, int C, void* y, int y_f32, hipStream_t s);
+int eegan_global_avgpool_bwd(const void* dy, int dy_f32, int N, int HW, int C, uint16_t* dx, int lddx, hipStream_t s);
+int eegan_fill_f32(float* x, long n, float v, hipStream_t s);
+
+/* ------------------------------------------------------------------ linear --
+ * replaces: nn.Linear of models.py:51-60,150-152,188,321 and DAMSM.py:163 (fp32) */
+int eegan_gemm_f32(const float* A, long sai, long sak, const float* B, long sbk, long sbj, float* C, long ldc, int M,
+                   int N, int K, const float* bias, int act, float alpha, float beta, hipStream_t s);
+int eegan_colsum_f32(const float* X, long ld, int M, int N, float* out, int accumulate, hipStream_t s);
+int eegan_act_bwd_f32(const float* dy, const float* y, long n, int act, float slope, float* dx, hipStream_t s);
+
+/* ------------------------------------------------------------------ losses --
+ * replaces: miscc/DAMSM_losses.py:17-63 (cosine_similarity, func_attention),
+ * 233-342 (sent_loss, words_loss); train.py:99-103, 336-417; models.py:155-180 */
+/* sim[j][i] = gamma3 * log sum_k exp(gamma2 cos(word_ik, attn-context_jk)) for every (image j, text i) */
+int eegan_words_sim(const float* regions, const float* words, const long* cap_lens, int B, int T, float* sim,
+                    float* att, hipStream_t s);
+int eegan_words_sim_bwd(const float* regions, const float* words, const long* cap_lens, int B, int T,
+                        const float* dsim, float* dregions, float* dwords, hipStream_t s);
+/* loss2 = (CE(sim, labels), CE(sim^T, labels)) with same-class off-diagonal entries masked to -inf
+ * (labels == NULL means arange(B), the reference's match_labels) */
+int eegan_sim_ce(const float* sim, int B, const long* class_ids, const long* labels, float* loss2, hipStream_t s);
+int eegan_sim_ce_bwd(const float* sim, int B, const long* class_ids, const long* labels, const float* gloss2,
+                     float* dsim, hipStream_t s);
+int eegan_sent_sim(const float* cnn, const float* rnn, int B, int D, float* sim, hipStream_t s);
+int eegan_sent_sim_bwd(const float* cnn, const float* rnn, int B, int D, const float* sim, const float* dsim,
+                       float* nrm_ws, float* dcnn, float* drnn, hipStream_t s);
+/* mode 0 mean(relu(1-x)), 1 mean(relu(1+x)), 2 -mean(x), 3 mean(x) */
+int eegan_dout_reduce(const float* x, int n, int mode, float* out, hipStream_t s);
+int eegan_dout_reduce_bwd(const float* x, int n, int mode, const float* gout, float* dx, hipStream_t s);
+int eegan_bce_logits(const float* x, const float* target, int n, float* out, hipStream_t s);
+int eegan_bce_logits_bwd(const float* x, const float* target, int n, const float* gout, float* dx, hipStream_t s);
+/* MA gradient penalty: out = 2 * mean_b ||[g_img_b, g_sent_b]||^6 */
+int eegan_gp_loss(const uint16_t* gx, int ld, int B, int HW, int C, const float* gs, int E, float* nrm2, float* out,
+                  hipStream_t s);
+int eegan_gp_loss_bwd(const uint16_t* gx, int ld, int B, int HW, int C, const float* gs, int E, const float* nrm2,
+                      const float* gout, uint16_t* dgx, int lddgx, float* dgs, hipStream_t s);
+/* labels[i][(id_i - 1) mod ncls] = 1 (bit-exact with train.py:99-103; *err set if an id is out of range) */
+int eegan_class_onehot(const long* ids, int B, int ncls, float* out, int* err, hipStream_t s);
+int eegan_attr_attn(const float* q, const float* k, const float* v, int B, int L, int D, float scale, float* probs,
+                    float* out, float* merged, hipStream_t s);
+int eegan_attr_attn_bwd(const float* q, const float* k, const float* v, const float* probs, const float* dout, int B,
+                        int L, int D, float scale, float* dq, float* dk, float* dv, hipStream_t s);
+
+/* ------------------------------------------------------------ text encoder --
+ * replaces: RNN_ENCODER.forward (DAMSM.py:88-115) in eval mode: nn.Embedding,
+ * pack_padded_sequence/nn.LSTM(bidirectional)/pad_packed_sequence, with the
+ * caption lengths read on the device (no cap_lens.tolist() host sync). */
+int eegan_embedding(const long* ids, long n, const float* table, int E, float* out, hipStream_t s);
+/* xproj [2][B][T][4H] = x W_ih^T + b_ih + b_hh per direction; whhT [2][H][4H];
+ * words [B][2H][Tout] (zero padded past each length), sent [B][2H] = [h_fwd(last), h_bwd(first)] */
+int eegan_lstm_bidir(const float* xproj, const float* whhT, const long* lens, int B, int T, int H, int Tout,
+                     float* words, float* sent, hipStream_t s);
+
+/* -------------------------------------------------------------------- adam --
+ * replaces: torch.optim.Adam(betas=(0.0, 0.9)) of train.py:252-263 on one flat buffer */
+int eegan_adam(float* p, const float* g, float* m, float* v, long n, float beta1, float beta2, float step_size,
+               float bc2_sqrt, float eps, float weight_decay, hipStream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EEGAN_HIP_H */

@@ -1,0 +1,99 @@
+"""CPU tests: the C-ABI library loads and exports every symbol include/eegan_hip.h
+declares; the drop-in modules expose the reference's state_dict keys and
+shapes (so reference checkpoints load); config parsing; host logic."""
+import os
+import re
+
+import pytest
+import torch
+
+from _util import REPO, spec
+
+
+def test_library_exports_header_symbols():
+    import eegan_hip
+    from eegan_hip import _lib
+    hdr = open(os.path.join(REPO, 'include', 'eegan_hip.h')).read()
+    declared = sorted(set(re.findall(r'\b(eegan_[a-z0-9_]+)\s*\(', hdr)))
+    assert len(declared) >= 60
+    for name in declared:
+        assert hasattr(_lib.LIB, name), name          # exported by libeegan_hip.so
+        assert name in _lib._SIGS, name               # bound with a ctypes signature
+    assert set(_lib._SIGS) == set(declared)
+    assert eegan_hip.ABI_VERSION == 1
+    assert _lib.ops.conv_gather_channels(100, 104) == 104
+    assert _lib.ops.conv_gather_channels(3, 3) == 3
+
+
+def _keys(mod):
+    return [(k, tuple(v.shape)) for k, v in mod.state_dict().items()]
+
+
+def test_state_dict_parity_with_reference():
+    import models
+    import DAMSM
+    from sync_batchnorm import SynchronizedBatchNorm2d
+    cases = [
+        ('gen', models.Gen(8, 100)),
+        ('sagb_sc', models.SAGB_Block(16, 8, pred_mask=True)),
+        ('sagb_id', models.SAGB_Block(16, 16, pred_mask=True)),
+        ('sagb_nomask', models.SAGB_Block(8, 8, pred_mask=False)),
+        ('cum', models.Cum_Block(16, 8)),
+        ('resd_sc', models.resD(8, 16)),
+        ('resd_id', models.resD(16, 16)),
+        ('discsent', models.DiscSent(32, 256)),
+        ('disccond', models.DiscCond(32, 256, class_nums=10)),
+        ('attr', models.ATTR_Enhance()),
+        ('syncbn', SynchronizedBatchNorm2d(8)),
+        ('dis64', models.Dis64(8)),
+        ('dis128', models.Dis128(8)),
+        ('dis256', models.Dis256(8, True, 10)),
+        ('rnn', DAMSM.RNN_ENCODER(50, nhidden=256)),
+    ]
+    for name, mod in cases:
+        assert _keys(mod) == spec(name), name
+
+
+def test_dataparallel_prefix_and_module():
+    import models
+    from sync_batchnorm import DataParallelWithCallback
+    g = DataParallelWithCallback(models.Gen(8, 100))
+    keys = list(g.state_dict().keys())
+    assert len(keys) == 262 and all(k.startswith('module.') for k in keys)
+    assert 'module.blocks.0.affine1.norm2d.running_mean' in keys
+    assert isinstance(g.module, models.Gen)
+
+
+def test_cnn_encoder_keys_torchvision_names():
+    import DAMSM
+    enc = DAMSM.CNN_ENCODER(256)
+    sd = enc.state_dict()
+    for k in ['Conv2d_1a_3x3.conv.weight', 'Conv2d_1a_3x3.bn.running_var', 'Mixed_5b.branch_pool.conv.weight',
+              'Mixed_6e.branch7x7dbl_5.conv.weight', 'Mixed_7c.branch3x3dbl_3b.bn.bias', 'emb_features.weight',
+              'emb_cnn_code.bias']:
+        assert k in sd, k
+    assert tuple(sd['Mixed_6b.branch7x7_2.conv.weight'].shape) == (128, 128, 1, 7)
+    assert tuple(sd['emb_cnn_code.weight'].shape) == (256, 2048)
+    assert not any(p.requires_grad for p in enc.parameters())
+
+
+def test_config_merge(tmp_path):
+    from miscc.config import cfg, cfg_from_file
+    y = tmp_path / 'bird.yml'
+    y.write_text('CONFIG_NAME: x\nDATASET_NAME: bird\nGPU_ID: 0\nTRAIN:\n  BATCH_SIZE: 16\n  CLASS_NUM: 200\n'
+                 'GAN:\n  GF_DIM: 32\n  DF_DIM: 32\n')
+    old = (cfg.TRAIN.BATCH_SIZE, cfg.GAN.GF_DIM, cfg.GAN.DF_DIM)
+    cfg_from_file(str(y))
+    assert cfg.TRAIN.BATCH_SIZE == 16 and cfg.GAN.GF_DIM == 32 and cfg.TRAIN.SMOOTH.GAMMA1 == 5.0
+    bad = tmp_path / 'bad.yml'
+    bad.write_text('NOT_A_KEY: 1\n')
+    with pytest.raises(KeyError):
+        cfg_from_file(str(bad))
+    cfg.TRAIN.BATCH_SIZE, cfg.GAN.GF_DIM, cfg.GAN.DF_DIM = old
+
+
+def test_att_maps_lazy_list():
+    from miscc.DAMSM_losses import _AttMaps
+    att = torch.arange(2 * 3 * 289, dtype=torch.float32).reshape(2, 3, 289)
+    m = _AttMaps(att, torch.tensor([3, 1]))
+    assert len(m) == 2 and m[1].shape == (1, 1, 17, 17) and m[0].shape == (1, 3, 17, 17)

@@ -1,0 +1,341 @@
+"""Kernel-level parity: every HIP op (through the C ABI) against a plain
+PyTorch fp32 CPU reference of the same op on the same bf16-rounded inputs.
+
+Tolerances: bf16 storage of activations/gradients with fp32 accumulation ->
+relative L2 error <= 1e-2 (outputs rounded once to bf16: ~2e-3 expected);
+integer / label work bit-exact."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from _util import rel_l2  # noqa: E402
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _mods():
+    from eegan_hip import functional as Fn
+    from eegan_hip import tensor as T
+    from eegan_hip.nn import Conv2d
+    return Fn, T, Conv2d
+
+
+def _nhwc(x, dev):
+    """fp32 NCHW CPU -> bf16 NHWC device activation (padded ld for C >= 8)."""
+    Fn, T, _ = _mods()
+    N, C, H, W = x.shape
+    t = T.empty_nhwc(N, C, H, W, dev)
+    t.copy_(x.to(dev).to(torch.bfloat16))
+    return t
+
+
+CONV_CASES = [
+    # N, Cin, H, W, Cout, k, stride, pad, bias, act, up2
+    (2, 32, 16, 16, 64, 3, 1, 1, False, None, False),
+    (2, 64, 16, 16, 32, 4, 2, 1, False, 'lrelu', False),
+    (2, 3, 32, 32, 16, 3, 1, 1, True, None, False),
+    (2, 16, 8, 8, 3, 3, 1, 1, False, 'tanh', False),
+    (2, 100, 8, 8, 1, 1, 1, 0, False, None, False),
+    (2, 24, 8, 8, 100, 3, 1, 1, False, 'relu', False),
+    (2, 64, 8, 8, 64, 4, 4, 0, True, None, False),
+    (3, 32, 4, 4, 1, 4, 1, 0, False, None, False),
+    (2, 32, 8, 8, 16, (1, 7), 1, (0, 3), False, 'relu', False),
+    (2, 32, 17, 17, 48, 3, 2, 0, False, None, False),
+    (2, 32, 8, 8, 32, 3, 1, 1, False, None, True),
+    (2, 16, 8, 8, 24, 1, 1, 0, True, None, True),
+    (4, 128, 32, 32, 256, 3, 1, 1, False, 'lrelu', False),
+    (2, 48, 9, 9, 40, 3, 1, 1, False, None, False),
+]
+
+
+@pytest.mark.parametrize('case', CONV_CASES, ids=[str(i) for i in range(len(CONV_CASES))])
+def test_conv_fwd_bwd(gpu, case):
+    Fn, T, Conv2d = _mods()
+    N, Cin, H, W, Cout, k, st, pad, bias, act, up2 = case
+    torch.manual_seed(hash(str(case)) & 0xffff)
+    m = Conv2d(Cin, Cout, k, st, pad, bias=bias)
+    x = _bf(torch.randn(N, Cin, H, W))
+    Wt = _bf(m.weight.detach())
+    m.weight.data.copy_(Wt)
+    m = m.to(gpu)
+    xd = _nhwc(x, gpu).requires_grad_()
+    y = m(xd, act=act, up2=up2)
+    # reference
+    xr = x.clone().requires_grad_()
+    wr = Wt.clone().requires_grad_()
+    br = m.bias.detach().cpu().clone().requires_grad_() if bias else None
+    xin = F.interpolate(xr, scale_factor=2) if up2 else xr
+    yr = F.conv2d(xin, wr, br, st, pad)
+    if act == 'lrelu':
+        yr = F.leaky_relu(yr, 0.2)
+    elif act == 'relu':
+        yr = F.relu(yr)
+    elif act == 'tanh':
+        yr = torch.tanh(yr)
+    assert y.shape == yr.shape
+    assert rel_l2(y.float().cpu(), yr) < 1e-2
+    gy = _bf(torch.randn(yr.shape))
+    yr.backward(gy)
+    y.backward(_nhwc(gy, gpu))
+    assert rel_l2(xd.grad.float().cpu(), xr.grad) < 2e-2
+    assert rel_l2(m.weight.grad.cpu(), wr.grad) < 2e-2
+    if bias:
+        assert rel_l2(m.bias.grad.cpu(), br.grad) < 2e-2
+
+
+def test_conv_double_backward(gpu):
+    """d/dW of ||d<y,r>/dx||^2 -- the gradient-penalty pattern (train.py:389-402)."""
+    Fn, T, Conv2d = _mods()
+    torch.manual_seed(3)
+    for (Cin, Cout, k, st, pad) in [(8, 16, 4, 2, 1), (16, 16, 3, 1, 1), (3, 8, 3, 1, 1)]:
+        m = Conv2d(Cin, Cout, k, st, pad, bias=False)
+        Wt = _bf(m.weight.detach())
+        m.weight.data.copy_(Wt)
+        m = m.to(gpu)
+        x = _bf(torch.randn(2, Cin, 8, 8))
+        r = _bf(torch.randn(2, Cout, (8 + 2 * pad - k) // st + 1, (8 + 2 * pad - k) // st + 1))
+        xd = _nhwc(x, gpu).requires_grad_()
+        y = m(xd, act='lrelu')
+        (gx,) = torch.autograd.grad(y, xd, _nhwc(r, gpu), create_graph=True)
+        loss = Fn.DotFn.apply(gx, gx)
+        loss.backward()
+        xr = x.clone().requires_grad_()
+        wr = Wt.clone().requires_grad_()
+        yr = F.leaky_relu(F.conv2d(xr, wr, None, st, pad), 0.2)
+        (gxr,) = torch.autograd.grad(yr, xr, r, create_graph=True)
+        (gxr * gxr).sum().backward()
+        assert rel_l2(loss.detach().cpu(), (gxr * gxr).sum().detach()) < 2e-2
+        assert rel_l2(m.weight.grad.cpu(), wr.grad) < 3e-2
+
+
+@pytest.mark.parametrize('mode,up2,act', [(0, False, 'relu'), (0, False, 'lrelu'), (1, True, 'relu'),
+                                          (1, False, None), (0, True, None)])
+def test_bn_modulation(gpu, mode, up2, act):
+    """SyncBN (batch stats) + affine / affine_ssa modulation + act (+ fused nearest-up)."""
+    Fn, T, _ = _mods()
+    from eegan_hip.nn import SyncBatchNorm2d
+    torch.manual_seed(5)
+    N, C, H, W = 3, 24, 6, 6
+    bn = SyncBatchNorm2d(C, affine=(mode == 0))
+    if mode == 0:
+        bn.weight.data.normal_(1, 0.2)
+        bn.bias.data.normal_(0, 0.2)
+    bn = bn.to(gpu)
+    x = _bf(torch.randn(N, C, H, W) * 2 + 0.5)
+    Ho, Wo = (2 * H, 2 * W) if up2 else (H, W)
+    gam = torch.randn(N, C) * 0.5
+    bet = torch.randn(N, C) * 0.5
+    msk = torch.rand(N, 1, Ho, Wo)
+    xd = _nhwc(x, gpu).requires_grad_()
+    gd, bd, md = gam.to(gpu).requires_grad_(), bet.to(gpu).requires_grad_(), msk.to(gpu).requires_grad_()
+    if mode == 0:
+        y = bn(xd, act=act, up2=up2)
+    else:
+        y = bn.modulate(xd, gd, bd, md, act=act, up2=up2)
+    xr = x.clone().requires_grad_()
+    gr, br_, mr = gam.clone().requires_grad_(), bet.clone().requires_grad_(), msk.clone().requires_grad_()
+    wr = bn.weight.detach().cpu().clone().requires_grad_() if mode == 0 else None
+    bb = bn.bias.detach().cpu().clone().requires_grad_() if mode == 0 else None
+    rm, rv = torch.zeros(C), torch.ones(C)
+    xin = F.interpolate(xr, scale_factor=2) if up2 else xr
+    n = F.batch_norm(xin, rm, rv, wr, bb, True, 0.1, 1e-5)
+    if mode == 1:
+        n = (gr[:, :, None, None] * mr + 1) * n + br_[:, :, None, None] * mr
+    if act == 'relu':
+        n = F.relu(n)
+    elif act == 'lrelu':
+        n = F.leaky_relu(n, 0.2)
+    assert rel_l2(y.float().cpu(), n) < 1e-2
+    assert rel_l2(bn.running_mean.cpu(), rm) < 1e-4
+    assert rel_l2(bn.running_var.cpu(), rv) < 1e-4
+    g = _bf(torch.randn(n.shape))
+    n.backward(g)
+    y.backward(_nhwc(g, gpu))
+    assert rel_l2(xd.grad.float().cpu(), xr.grad) < 2e-2
+    if mode == 0:
+        assert rel_l2(bn.weight.grad.cpu(), wr.grad) < 1e-2
+        assert rel_l2(bn.bias.grad.cpu(), bb.grad) < 1e-2
+    else:
+        assert rel_l2(gd.grad.cpu(), gr.grad) < 1e-2
+        assert rel_l2(bd.grad.cpu(), br_.grad) < 1e-2
+        assert rel_l2(md.grad.cpu(), mr.grad) < 1e-2
+
+
+def test_elementwise_ops(gpu):
+    Fn, T, _ = _mods()
+    torch.manual_seed(7)
+    x = _bf(torch.randn(2, 24, 8, 8))
+    # avg pool 2 + adjoint + double adjoint
+    xd = _nhwc(x, gpu).requires_grad_()
+    y = Fn.AvgPool2Fn.apply(xd)
+    assert rel_l2(y.float().cpu(), F.avg_pool2d(x, 2)) < 1e-2
+    # upsample
+    u = Fn.Upsample2Fn.apply(_nhwc(x, gpu))
+    assert rel_l2(u.float().cpu(), F.interpolate(x, scale_factor=2)) < 1e-6
+    # scale-add with device gamma
+    h = _bf(torch.randn(2, 24, 8, 8))
+    gm = torch.tensor([0.7], device=gpu)
+    o = Fn.ScaleAddFn.apply(_nhwc(x, gpu), _nhwc(h, gpu), gm)
+    assert rel_l2(o.float().cpu(), x + 0.7 * h) < 1e-2
+    # cat + tile cond, and its adjoint
+    f = _nhwc(x[:, :, :4, :4].contiguous(), gpu).requires_grad_()
+    c = torch.randn(2, 256, device=gpu, requires_grad=True)
+    ct = Fn.CatTileFn.apply(f, c)
+    ref = torch.cat([x[:, :, :4, :4], c.detach().cpu().view(2, 256, 1, 1).repeat(1, 1, 4, 4)], 1)
+    assert rel_l2(ct.float().cpu(), ref) < 1e-2
+    gct = _bf(torch.randn(ref.shape))
+    ct.backward(_nhwc(gct, gpu))
+    assert rel_l2(c.grad.cpu(), gct[:, 24:].sum((2, 3))) < 1e-2
+    assert rel_l2(f.grad.float().cpu(), gct[:, :24]) < 1e-6
+    # mask bilinear (align_corners=True) + sigmoid and its backward
+    m = torch.randn(2, 1, 8, 8)
+    md = m.to(gpu).requires_grad_()
+    s = Fn.MaskResizeSigmoidFn.apply(md, 16)
+    mr = m.clone().requires_grad_()
+    sr = torch.sigmoid(F.interpolate(mr, size=16, mode='bilinear', align_corners=True))
+    assert rel_l2(s.cpu(), sr) < 1e-5
+    gs = torch.randn(sr.shape)
+    sr.backward(gs)
+    s.backward(gs.to(gpu))
+    assert rel_l2(md.grad.cpu(), mr.grad) < 1e-5
+    # image bilinear 256 -> 299 (align_corners=False)
+    im = _bf(torch.rand(2, 3, 32, 32) * 2 - 1)
+    imd = _nhwc(im, gpu).requires_grad_()
+    r = Fn.BilinearFn.apply(imd, 37, 37)
+    imr = im.clone().requires_grad_()
+    rr = F.interpolate(imr, size=(37, 37), mode='bilinear', align_corners=False)
+    assert rel_l2(r.float().cpu(), rr) < 1e-2
+    g2 = _bf(torch.randn(rr.shape))
+    rr.backward(g2)
+    r.backward(_nhwc(g2, gpu))
+    assert rel_l2(imd.grad.float().cpu(), imr.grad) < 1e-2
+    # max pool 3x3 s2 / avg pool 3x3 s1 p1 / global average pool
+    z = _bf(torch.randn(2, 16, 11, 11))
+    zd = _nhwc(z, gpu).requires_grad_()
+    mp = Fn.MaxPool3s2Fn.apply(zd)
+    zr = z.clone().requires_grad_()
+    mpr = F.max_pool2d(zr, 3, 2)
+    assert rel_l2(mp.float().cpu(), mpr) < 1e-6
+    gm2 = _bf(torch.randn(mpr.shape))
+    mpr.backward(gm2)
+    mp.backward(_nhwc(gm2, gpu))
+    assert rel_l2(zd.grad.float().cpu(), zr.grad) < 1e-2
+    ap = Fn.AvgPool3s1Fn.apply(_nhwc(z, gpu))
+    assert rel_l2(ap.float().cpu(), F.avg_pool2d(z, 3, 1, 1)) < 1e-2
+    ga = Fn.GlobalAvgPoolFn.apply(_nhwc(z, gpu))
+    assert rel_l2(ga.cpu(), z.mean((2, 3))) < 1e-3
+    # fc -> NHWC view and back
+    fc = torch.randn(3, 32 * 16)
+    fcd = fc.to(gpu).requires_grad_()
+    v = Fn.FcToNhwcFn.apply(fcd, 32)
+    assert rel_l2(v.float().cpu(), fc.view(3, 32, 4, 4)) < 1e-2
+    gv = _bf(torch.randn(3, 32, 4, 4))
+    v.backward(_nhwc(gv, gpu))
+    assert rel_l2(fcd.grad.cpu(), gv.reshape(3, -1)) < 1e-6
+
+
+def test_linear_and_attr(gpu):
+    Fn, T, _ = _mods()
+    from eegan_hip.nn import Linear
+    torch.manual_seed(9)
+    lin = Linear(100, 70).to(gpu)
+    x = torch.randn(5, 100)
+    xd = x.to(gpu).requires_grad_()
+    y = lin(xd, act='relu')
+    wr = lin.weight.detach().cpu().clone().requires_grad_()
+    br = lin.bias.detach().cpu().clone().requires_grad_()
+    xr = x.clone().requires_grad_()
+    yr = F.relu(F.linear(xr, wr, br))
+    assert rel_l2(y.cpu(), yr) < 1e-5
+    g = torch.randn(yr.shape)
+    yr.backward(g)
+    y.backward(g.to(gpu))
+    assert rel_l2(xd.grad.cpu(), xr.grad) < 1e-5
+    assert rel_l2(lin.weight.grad.cpu(), wr.grad) < 1e-5
+    assert rel_l2(lin.bias.grad.cpu(), br.grad) < 1e-5
+    q, k, v = [torch.randn(3, 4, 256) for _ in range(3)]
+    qd, kd, vd = [t.to(gpu).requires_grad_() for t in (q, k, v)]
+    o = Fn.AttrAttnFn.apply(qd, kd, vd, 1 / 16)
+    qr, kr, vr = [t.clone().requires_grad_() for t in (q, k, v)]
+    orf = torch.bmm(torch.softmax(torch.bmm(qr, kr.transpose(1, 2)), -1) / 16, vr)
+    assert rel_l2(o.cpu(), orf) < 1e-5
+    go = torch.randn(orf.shape)
+    orf.backward(go)
+    o.backward(go.to(gpu))
+    for a, b in [(qd, qr), (kd, kr), (vd, vr)]:
+        assert rel_l2(a.grad.cpu(), b.grad) < 1e-4
+
+
+def test_losses_small(gpu):
+    Fn, T, _ = _mods()
+    torch.manual_seed(11)
+    x = torch.randn(7)
+    for mode, fn in [(0, lambda t: F.relu(1 - t).mean()), (1, lambda t: F.relu(1 + t).mean()),
+                     (2, lambda t: -t.mean()), (3, lambda t: t.mean())]:
+        xd = x.to(gpu).requires_grad_()
+        o = Fn.DoutReduceFn.apply(xd, mode)
+        xr = x.clone().requires_grad_()
+        orf = fn(xr)
+        assert abs(o.item() - orf.item()) < 1e-5
+        o.backward()
+        orf.backward()
+        assert rel_l2(xd.grad.cpu(), xr.grad) < 1e-5
+    lg = torch.randn(4, 10)
+    tg = torch.zeros(4, 10)
+    tg[torch.arange(4), torch.tensor([1, 5, 9, 0])] = 1
+    ld = lg.to(gpu).requires_grad_()
+    o = Fn.BceLogitsFn.apply(ld, tg.to(gpu))
+    lr = lg.clone().requires_grad_()
+    orf = F.binary_cross_entropy_with_logits(lr, tg)
+    assert abs(o.item() - orf.item()) < 1e-5
+    o.backward()
+    orf.backward()
+    assert rel_l2(ld.grad.cpu(), lr.grad) < 1e-5
+    # gradient penalty
+    gx = _bf(torch.randn(3, 3, 8, 8) * 0.1)
+    gs = torch.randn(3, 256) * 0.05
+    gxd, gsd = _nhwc(gx, gpu).requires_grad_(), gs.to(gpu).requires_grad_()
+    o = Fn.GradPenaltyFn.apply(gxd, gsd)
+    gxr, gsr = gx.clone().requires_grad_(), gs.clone().requires_grad_()
+    g = torch.cat([gxr.reshape(3, -1), gsr], 1)
+    orf = 2.0 * torch.mean(torch.sqrt((g ** 2).sum(1)) ** 6)
+    assert abs(o.item() - orf.item()) / orf.item() < 1e-4
+    o.backward()
+    orf.backward()
+    assert rel_l2(gxd.grad.float().cpu(), gxr.grad) < 1e-2
+    assert rel_l2(gsd.grad.cpu(), gsr.grad) < 1e-4
+
+
+def test_class_onehot_bit_exact(gpu):
+    Fn, T, _ = _mods()
+    from oracle import eegan_oracle as O
+    ids = torch.tensor([1, 200, 0, 57, 57, 3])
+    got, err = Fn.class_onehot(ids, 6, 200, gpu)
+    assert torch.equal(got.cpu(), O.prepare_class_labels(6, 200, ids.tolist()))
+    assert err.item() == 0
+
+
+def test_adam_matches_torch(gpu):
+    from eegan_hip.optim import FlatAdam
+    torch.manual_seed(13)
+    ps = [torch.nn.Parameter(torch.randn(s, device=gpu)) for s in [(7, 3), (5,), (1,), (33, 2, 3)]]
+    qs = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    opt = FlatAdam(ps, lr=4e-4, betas=(0.0, 0.9))
+    ref = torch.optim.Adam(qs, lr=4e-4, betas=(0.0, 0.9))
+    for it in range(3):
+        gs = [torch.randn(p.shape, device=gpu) for p in ps]
+        opt.zero_grad()
+        ref.zero_grad()
+        for p, q, g in zip(ps, qs, gs):
+            p.grad.add_(g)
+            q.grad = g.clone()
+        opt.step()
+        ref.step()
+    for p, q in zip(ps, qs):
+        assert torch.allclose(p.detach(), q.detach(), rtol=1e-5, atol=1e-7)
