@@ -87,13 +87,16 @@ __global__ void bn_reduce_kernel(const float* __restrict__ ws, int nblk, int C, 
 }
 
 // stats[0..C) mean, [C..2C) inv_std, [2C..3C) 1 if d(inv_std)/d(var) != 0
-__global__ void bn_finalize_kernel(const double* __restrict__ sums, int C, double count, float eps, float mom,
-                                   int clamp_mode, float* __restrict__ rmean, float* __restrict__ rvar,
+__global__ void bn_finalize_kernel(const double* __restrict__ sums, int C, double count, double sum_scale, float eps,
+                                   float mom, int clamp_mode, float* __restrict__ rmean, float* __restrict__ rvar,
                                    float* __restrict__ stats) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  const double mean = sums[c] / count;
-  double sumvar = sums[C + c] - sums[c] * mean;
+  // sum_scale: replication factor of the statistics tensor (4 when x is read
+  // through the nearest-2x upsample: every low-res element appears 4 times)
+  const double s1 = sums[c] * sum_scale, s2 = sums[C + c] * sum_scale;
+  const double mean = s1 / count;
+  double sumvar = s2 - s1 * mean;
   if (sumvar < 0) sumvar = 0;
   const double var_b = sumvar / count;
   float istd, vg = 1.f;
@@ -431,10 +434,10 @@ int eegan_bn_stats(const uint16_t* x, long P, int C, int ld, float* ws, double* 
   return ee_check_launch("bn_reduce");
 }
 
-int eegan_bn_finalize(const double* sums, int C, double count, float eps, float momentum, int clamp_mode,
-                      float* running_mean, float* running_var, float* stats, hipStream_t stream) {
-  bn_finalize_kernel<<<ee_cdiv(C, 256), 256, 0, stream>>>(sums, C, count, eps, momentum, clamp_mode, running_mean,
-                                                           running_var, stats);
+int eegan_bn_finalize(const double* sums, int C, double count, double sum_scale, float eps, float momentum,
+                      int clamp_mode, float* running_mean, float* running_var, float* stats, hipStream_t stream) {
+  bn_finalize_kernel<<<ee_cdiv(C, 256), 256, 0, stream>>>(sums, C, count, sum_scale, eps, momentum, clamp_mode,
+                                                           running_mean, running_var, stats);
   return ee_check_launch("bn_finalize");
 }
 

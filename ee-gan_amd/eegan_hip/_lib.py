@@ -42,7 +42,7 @@ _SIGS = {
     'eegan_conv_bwd_weight': ([CD, P, P, P, P, I, P], I),
     'eegan_bn_stats_workspace': ([L, I], L),
     'eegan_bn_stats': ([P, L, I, I, P, P, P], I),
-    'eegan_bn_finalize': ([P, I, D, F, F, I, P, P, P, P], I),
+    'eegan_bn_finalize': ([P, I, D, D, F, F, I, P, P, P, P], I),
     'eegan_bnmod_fwd': ([BD, P, I, P], I),
     'eegan_bnmod_bwd_workspace': ([BD], L),
     'eegan_bnmod_bwd': ([BD, P, I, P, P, P, P, P, P], I),

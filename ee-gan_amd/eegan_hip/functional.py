@@ -121,17 +121,18 @@ class LaunchTimer(object):
     they run on (bench.py's roofline): records (kind, algorithmic flops,
     algorithmic bytes, start, end)."""
 
-    def __init__(self):
+    def __init__(self, detail=False):
         self.rec = []
+        self.detail = detail
 
-    def __call__(self, kind, flops, nbytes, fn):
+    def __call__(self, kind, flops, nbytes, fn, key=None):
         s = torch.cuda.current_stream()
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(s)
         fn()
         e1.record(s)
-        self.rec.append((kind, flops, nbytes, e0, e1))
+        self.rec.append((kind if not self.detail else (kind, key), flops, nbytes, e0, e1))
 
     def summary(self):
         torch.cuda.synchronize()
@@ -149,11 +150,16 @@ class LaunchTimer(object):
 TIMER = None
 
 
-def _launch(kind, flops, nbytes, fn):
+def _launch(kind, flops, nbytes, fn, key=None):
     if TIMER is None:
         fn()
     else:
-        TIMER(kind, flops, nbytes, fn)
+        TIMER(kind, flops, nbytes, fn, key)
+
+
+def _shape_key(d):
+    return 'N%d %dx%d C%d->K%d %dx%d s%d p%d,%d%s -> %dx%d' % (d.N, d.H, d.W, d.C, d.K, d.R, d.S, d.stride, d.pad_h,
+                                                             d.pad_w, ' up2' if d.up2 else '', d.Ho, d.Wo)
 
 
 # ============================================================ conv core ===
@@ -169,7 +175,7 @@ def conv_fwd_raw(x, W, b, g, act=0, slope=0.2, out_f32=False, cache=None, res=No
     nbytes = 2.0 * (N * H * Wd * C + N * Ho * Wo * g.K * (2 if out_f32 else 1) + g.K * C * g.R * g.S)
     _launch('conv_fwd', flops, nbytes, lambda: ops.conv_fwd(
         d, x.data_ptr(), wp.data_ptr(), ptr(b), act, slope, ptr(res), ld_of(res) if res is not None else 0,
-        ptr(gamma), y.data_ptr(), int(out_f32), stream()))
+        ptr(gamma), y.data_ptr(), int(out_f32), stream()), key=_shape_key(d) if TIMER is not None else None)
     return y
 
 
@@ -187,7 +193,8 @@ def conv_bwd_data_raw(dz, W, g, x_shape, cache=None):
     flops = 2.0 * N * Ho * Wo * g.K * C * g.R * g.S
     nbytes = 2.0 * (N * Hl * Wl * C + N * Ho * Wo * g.K + g.K * C * g.R * g.S)
     _launch('conv_bwd_data', flops, nbytes, lambda: ops.conv_bwd_data(
-        d, dz.data_ptr(), wp.data_ptr(), dx.data_ptr(), ld_of(dx), 0, stream()))
+        d, dz.data_ptr(), wp.data_ptr(), dx.data_ptr(), ld_of(dx), 0, stream()),
+        key=_shape_key(d) if TIMER is not None else None)
     if g.up2:
         lo = empty_nhwc(N, C, H, Wd, dz.device)
         ops.sumpool2(dx.data_ptr(), N, Hl, Wl, C, ld_of(dx), lo.data_ptr(), ld_of(lo), stream())
@@ -204,7 +211,8 @@ def conv_bwd_weight_raw(x, dz, g, W_shape):
     flops = 2.0 * N * d.Ho * d.Wo * g.K * C * g.R * g.S
     nbytes = 2.0 * (N * H * Wd * C + N * d.Ho * d.Wo * g.K) + 4.0 * g.K * C * g.R * g.S
     _launch('conv_bwd_weight', flops, nbytes, lambda: ops.conv_bwd_weight(
-        d, x.data_ptr(), dz.data_ptr(), ws.data_ptr(), dW.data_ptr(), 0, stream()))
+        d, x.data_ptr(), dz.data_ptr(), ws.data_ptr(), dW.data_ptr(), 0, stream()),
+        key=_shape_key(d) if TIMER is not None else None)
     return dW
 
 
@@ -652,7 +660,7 @@ class BnModFn(torch.autograd.Function):
         clamp_mode = 1 if world > 1 else 0
         rm = bn.running_mean if (bn is not None and bn.track_running_stats) else None
         rv = bn.running_var if rm is not None else None
-        ops.bn_finalize(sums.data_ptr(), C, count, bn.eps if bn is not None else 1e-5,
+        ops.bn_finalize(sums.data_ptr(), C, count, 4.0 if up2 else 1.0, bn.eps if bn is not None else 1e-5,
                         bn.momentum if bn is not None else 0.1, clamp_mode, ptr(rm), ptr(rv), stats.data_ptr(), s)
         # (the reference calls F.batch_norm directly, so num_batches_tracked never moves)
         Ho, Wo = (H * 2, W * 2) if up2 else (H, W)

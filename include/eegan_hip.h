@@ -72,9 +72,11 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const uint16_t* x, const uin
 long eegan_bn_stats_workspace(long P, int C);
 /* sums[0..C) = sum x, sums[C..2C) = sum x^2 (fp64) over P pixels */
 int eegan_bn_stats(const uint16_t* x, long P, int C, int ld, float* ws, double* sums, hipStream_t stream);
-/* stats[3C] = (mean, inv_std, var-grad flag); updates running buffers (nullable) */
-int eegan_bn_finalize(const double* sums, int C, double count, float eps, float momentum, int clamp_mode,
-                      float* running_mean, float* running_var, float* stats, hipStream_t stream);
+/* stats[3C] = (mean, inv_std, var-grad flag) of sums*sum_scale over `count` elements
+ * (sum_scale = 4 when the normalised tensor is the nearest-2x upsample of x);
+ * updates running buffers (nullable) */
+int eegan_bn_finalize(const double* sums, int C, double count, double sum_scale, float eps, float momentum,
+                      int clamp_mode, float* running_mean, float* running_var, float* stats, hipStream_t stream);
 
 typedef struct eegan_bnmod_desc {
   const uint16_t* x;  /* input (physical grid N x H x W, channel stride ldx) */
