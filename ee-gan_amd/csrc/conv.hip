@@ -1,16 +1,23 @@
 // Implicit-GEMM direct convolutions for gfx950 (bf16 MFMA 16x16x32, fp32 acc).
 //
-// Activations are NHWC bf16 with a channel stride `ld` (== C, or C rounded up
-// to 8 for C >= 8).  No im2col is materialised: every B-operand tile is
-// gathered straight from the activation tensor into LDS.
+// Activations are NHWC bf16 with a channel stride `ld` (a multiple of 8:
+// 3-channel images are stored with ld = 8).  No im2col is materialised:
+// every B-operand tile is gathered straight from the activation tensor into LDS.
 //
 //   FWD  : y[p, co]  = sum_{r,s,c} x[gather_fwd(p,r,s), c] * W[co,r,s,c]
 //   BWDD : dx[p, ci] = sum_{r,s,co} dy[gather_bwd(p,r,s), co] * W[co,ci,r,s]
 //   WGRAD: dW[co, (r,s,c)] = sum_p dy[p, co] * x[gather_fwd(p,r,s), c]
 //
-// GEMM orientation: MFMA rows = output channels (A operand = packed weights),
-// MFMA cols = pixels (B operand = gathered activations), so every lane of the
-// accumulator owns 4 consecutive channels of one pixel -> 8-byte NHWC stores.
+// FWD/BWDD: MFMA rows = output channels (A = packed weights), MFMA columns =
+// pixels (B = gathered activations), so each accumulator lane owns 4
+// consecutive channels of one pixel -> 8-byte NHWC stores.  The K axis is
+// (tap, channel) with every tap's channel run padded to a multiple of 32, so
+// the tap and channel offset of each 32-deep K step are block-uniform: the
+// gather does no per-element index arithmetic.  A stride-s backward-data
+// pass is split into s^2 parity classes of input pixels; each class only
+// visits the kernel taps that reach it (a 4x4/s2 bwd-data does 1/4 of the
+// naive MFMA work).  Small grids are split along K (fp32 partial slab +
+// a reduce kernel that applies the epilogue).
 // Replaces every nn.Conv2d of models.py:14-403 and DAMSM.py.
 #include "common.h"
 #include "../../include/eegan_hip.h"
@@ -23,142 +30,148 @@ constexpr int KROW = BK + LDS_PAD;
 
 enum { MODE_FWD = 0, MODE_BWDD = 1 };
 
-struct ConvArgs {
-  const bf16_t* src;   // FWD: x ; BWDD: dy
-  const bf16_t* wp;    // packed weights [rows_pad][Kpad]
-  const float* bias;   // per output channel (FWD) or null
-  const bf16_t* res;   // residual (FWD): out = res + gamma * act(acc + bias)
-  const float* gamma;  // device scalar
-  void* out;
-  int ldres, ldo, out_f32, act;
-  float slope;
-  // source tensor (x for FWD, dy for BWDD)
-  int N, IH, IW, lds_src;  // logical grid of the source (FWD up2: physical IH/2 x IW/2)
-  int up2;
-  // pixel grid of the GEMM columns
-  int OH, OW;
-  int R, S, st, ph, pw;
-  int Cg, Cvalid;  // gathered channels (padded to 8 when vectorised) / valid channels
-  int Mrows;       // valid output channels
-  int P;           // N*OH*OW
-  int K, Kpad;     // R*S*Cg, round_up(K, BK)
-};
-
-// ---------------------------------------------------------------- gathers --
-template <int MODE>
-EE_DEV bool gather_addr(const ConvArgs& a, int n, int oy, int ox, int r, int s, long& off) {
-  if (MODE == MODE_FWD) {
-    const int iy = oy * a.st - a.ph + r, ix = ox * a.st - a.pw + s;
-    if ((unsigned)iy >= (unsigned)a.IH || (unsigned)ix >= (unsigned)a.IW) return false;
-    const int PH = a.IH >> a.up2, PW = a.IW >> a.up2;
-    off = ((long)(n * PH + (iy >> a.up2)) * PW + (ix >> a.up2)) * a.lds_src;
-    return true;
-  } else {
-    const int ty = oy + a.ph - r, tx = ox + a.pw - s;
-    if (ty < 0 || tx < 0) return false;
-    const int qy = ty / a.st, qx = tx / a.st;
-    if (qy * a.st != ty || qx * a.st != tx) return false;
-    if (qy >= a.IH || qx >= a.IW) return false;
-    off = ((long)(n * a.IH + qy) * a.IW + qx) * a.lds_src;
-    return true;
-  }
-}
-
-// load an 8-element k-chunk of the gathered operand for one pixel
-template <int MODE, bool VEC>
-EE_DEV uint4 gather_chunk(const ConvArgs& a, bool pvalid, int n, int oy, int ox, int k) {
-  uint4 v = make_uint4(0, 0, 0, 0);
-  if (!pvalid) return v;
-  if (VEC) {
-    if (k >= a.K) return v;
-    const int rs = k / a.Cg, c = k - rs * a.Cg;
-    const int r = rs / a.S, s = rs - r * a.S;
-    long off;
-    if (!gather_addr<MODE>(a, n, oy, ox, r, s, off)) return v;
-    v = *reinterpret_cast<const uint4*>(a.src + off + c);
-    if (c + 8 > a.Cvalid) {  // zero the padded channels (their storage is undefined)
-      uint32_t* w = reinterpret_cast<uint32_t*>(&v);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c0 = c + 2 * j;
-        if (c0 >= a.Cvalid) w[j] = 0;
-        else if (c0 + 1 >= a.Cvalid) w[j] &= 0xffffu;
-      }
-    }
-    return v;
-  } else {
-    uint16_t e[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      e[j] = 0;
-      const int kk = k + j;
-      if (kk < a.K) {
-        const int rs = kk / a.Cg, c = kk - rs * a.Cg;
-        const int r = rs / a.S, s = rs - r * a.S;
-        long off;
-        if (gather_addr<MODE>(a, n, oy, ox, r, s, off)) e[j] = a.src[off + c];
-      }
-    }
-    v.x = e[0] | ((uint32_t)e[1] << 16);
-    v.y = e[2] | ((uint32_t)e[3] << 16);
-    v.z = e[4] | ((uint32_t)e[5] << 16);
-    v.w = e[6] | ((uint32_t)e[7] << 16);
-    return v;
-  }
-}
-
 EE_DEV bf16x8_t as_frag(uint4 v) { return __builtin_bit_cast(bf16x8_t, v); }
 
+// zero the channels >= cvalid of an 8-channel chunk starting at channel c
+EE_DEV uint4 mask_chunk(uint4 v, int c, int cvalid) {
+  if (c + 8 > cvalid) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c0 = c + 2 * j;
+      if (c0 >= cvalid) w[j] = 0;
+      else if (c0 + 1 >= cvalid) w[j] &= 0xffffu;
+    }
+  }
+  return v;
+}
+
+struct ConvArgs {
+  const bf16_t* src;   // FWD: x ; BWDD: dy
+  const bf16_t* wp;    // packed weights [rows_pad][Kw], K = (tap, channel padded to Cgp)
+  const float* bias;   // per output channel or null
+  const bf16_t* res;   // residual: out = res + gamma * act(acc + bias)
+  const float* gamma;  // device scalar
+  void* out;
+  float* part;         // split-K partial slab [nsplit][P][Mrows] or null
+  int ldres, ldo, out_f32, act;
+  float slope;
+  int N, IH, IW, lds_src, up2;  // source grid (LOGICAL; FWD up2: physical IH/2 x IW/2)
+  int OH, OW;                   // full pixel grid of the GEMM columns
+  int R, S, st, ph, pw;
+  int Cgp, Cvalid;              // per-tap K run (multiple of 32) / valid gathered channels
+  int Mrows, Kw;                // output channels / packed-weight row stride
+  int P;                        // N*OH*OW
+  int ncls, nsplit;             // parity classes (BWDD stride>1), K splits
+};
+
 // ------------------------------------------------------- FWD / BWDD kernel --
-template <int MODE, bool VEC, int TCO, int TPIX, int WCO>
+template <int MODE, int TCO, int TPIX, int WCO>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   constexpr int WPIX = 4 / WCO;
   constexpr int WT_CO = TCO / WCO, WT_PIX = TPIX / WPIX;
   constexpr int FI = WT_CO / 16, FJ = WT_PIX / 16;
-  constexpr int A_CHUNKS = TCO * (BK / 8);     // 16-B chunks per A stage
+  constexpr int A_CHUNKS = TCO * (BK / 8);
   constexpr int B_CHUNKS = TPIX * (BK / 8);
   constexpr int A_PER = (A_CHUNKS + 255) / 256;
   constexpr int B_PER = B_CHUNKS / 256;
   static_assert(B_CHUNKS % 256 == 0, "pixel tile");
+  static_assert(FI >= 1 && FJ >= 1, "wave tile");
 
   __shared__ __attribute__((aligned(16))) bf16_t lds_a[2][TCO * KROW];
   __shared__ __attribute__((aligned(16))) bf16_t lds_b[2][TPIX * KROW];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wi = wave / WPIX, wj = wave % WPIX;
-  const int pix0 = blockIdx.x * TPIX, co0 = blockIdx.y * TCO;
+  const int cls = blockIdx.z % a.ncls, split = blockIdx.z / a.ncls;
+  const int co0 = blockIdx.y * TCO;
 
-  // per-thread fixed B rows (pixels) and k-chunk
+  // ---- parity class (BWDD with stride > 1): input pixels (qy + st*i, qx + st*j)
+  int qy = 0, qx = 0, CH = a.OH, CW = a.OW, stc = 1;
+  int r0 = 0, s0 = 0, TR = a.R, TS = a.S, dqy = 0, dqx = 0;
+  if (MODE == MODE_BWDD) {
+    if (a.ncls > 1) {
+      qy = cls / a.st;
+      qx = cls - qy * a.st;
+      CH = (a.OH - qy + a.st - 1) / a.st;
+      CW = (a.OW - qx + a.st - 1) / a.st;
+      stc = a.st;
+    }
+    r0 = (qy + a.ph) % a.st;
+    s0 = (qx + a.pw) % a.st;
+    TR = r0 < a.R ? (a.R - r0 + a.st - 1) / a.st : 0;
+    TS = s0 < a.S ? (a.S - s0 + a.st - 1) / a.st : 0;
+    dqy = (qy + a.ph - r0) / a.st;
+    dqx = (qx + a.pw - s0) / a.st;
+  }
+  const int Pc = a.N * CH * CW;
+  const int pix0 = blockIdx.x * TPIX;
+  if (pix0 >= Pc) return;  // block-uniform
+  const int nc = a.Cgp / BK;
+  const int nk_all = TR * TS * nc;
+  const int kchunk = (nk_all + a.nsplit - 1) / a.nsplit;
+  const int kt0 = min(nk_all, split * kchunk), kt1 = min(nk_all, kt0 + kchunk);
+
+  // ---- per-thread B rows (pixels) and k-chunk
   const int b_kc = tid & 3;
   int b_n[B_PER], b_y[B_PER], b_x[B_PER];
   bool b_ok[B_PER];
 #pragma unroll
   for (int i = 0; i < B_PER; ++i) {
-    const int row = (tid >> 2) + i * 64;
-    const int p = pix0 + row;
-    b_ok[i] = p < a.P;
+    const int p = pix0 + (tid >> 2) + i * 64;
+    b_ok[i] = p < Pc;
     const int pp = b_ok[i] ? p : 0;
-    const int hw = a.OH * a.OW;
-    b_n[i] = pp / hw;
-    const int rem = pp - b_n[i] * hw;
-    b_y[i] = rem / a.OW;
-    b_x[i] = rem - b_y[i] * a.OW;
+    const int hw = CH * CW;
+    const int n = pp / hw;
+    const int rem = pp - n * hw;
+    const int yy = rem / CW;
+    const int xx = rem - yy * CW;
+    b_n[i] = n;
+    if (MODE == MODE_FWD) {
+      b_y[i] = yy * a.st - a.ph;
+      b_x[i] = xx * a.st - a.pw;
+    } else {
+      b_y[i] = yy + dqy;  // oh = yy + dqy - tap_a
+      b_x[i] = xx + dqx;
+    }
   }
+  const int PH = a.IH >> a.up2, PW = a.IW >> a.up2;
 
   uint4 ra[A_PER], rb[B_PER];
   auto load_stage = [&](int kt) {
-    const int k0 = kt * BK;
+    const int tap = kt / nc;
+    const int cc = kt - tap * nc;
+    const int ta = tap / TS, tb = tap - ta * TS;
+    const int r = (MODE == MODE_FWD) ? ta : r0 + a.st * ta;
+    const int s = (MODE == MODE_FWD) ? tb : s0 + a.st * tb;
+    const int kbase = (r * a.S + s) * a.Cgp + cc * BK;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int ch = tid + i * 256;
       if (ch < A_CHUNKS) {
         const int row = ch >> 2, kc = ch & 3;
-        ra[i] = *reinterpret_cast<const uint4*>(a.wp + (long)(co0 + row) * a.Kpad + k0 + kc * 8);
+        ra[i] = *reinterpret_cast<const uint4*>(a.wp + (long)(co0 + row) * a.Kw + kbase + kc * 8);
       }
     }
+    const int c = cc * BK + b_kc * 8;
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i)
-      rb[i] = gather_chunk<MODE, VEC>(a, b_ok[i], b_n[i], b_y[i], b_x[i], k0 + b_kc * 8);
+    for (int i = 0; i < B_PER; ++i) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (b_ok[i] && c < a.Cvalid) {
+        long off = -1;
+        if (MODE == MODE_FWD) {
+          const int iy = b_y[i] + r, ix = b_x[i] + s;
+          if ((unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW)
+            off = ((long)(b_n[i] * PH + (iy >> a.up2)) * PW + (ix >> a.up2)) * a.lds_src;
+        } else {
+          const int oy = b_y[i] - ta, ox = b_x[i] - tb;
+          if ((unsigned)oy < (unsigned)a.IH && (unsigned)ox < (unsigned)a.IW)
+            off = ((long)(b_n[i] * a.IH + oy) * a.IW + ox) * a.lds_src;
+        }
+        if (off >= 0) v = mask_chunk(*reinterpret_cast<const uint4*>(a.src + off + c), c, a.Cvalid);
+      }
+      rb[i] = v;
+    }
   };
   auto store_stage = [&](int buf) {
 #pragma unroll
@@ -182,60 +195,77 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = a.Kpad / BK;
-  load_stage(0);
-  store_stage(0);
-  __syncthreads();
   const int fr = lane & 15, fk = (lane >> 4) * 8;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) load_stage(kt + 1);
-    bf16x8_t fa[FI], fb[FJ];
+  if (kt0 < kt1) {
+    load_stage(kt0);
+    store_stage(0);
+    __syncthreads();
+    int buf = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = kt + 1 < kt1;
+      if (more) load_stage(kt + 1);
+      bf16x8_t fa[FI], fb[FJ];
 #pragma unroll
-    for (int i = 0; i < FI; ++i)
-      fa[i] = as_frag(*reinterpret_cast<const uint4*>(&lds_a[buf][(wi * WT_CO + i * 16 + fr) * KROW + fk]));
-#pragma unroll
-    for (int j = 0; j < FJ; ++j)
-      fb[j] = as_frag(*reinterpret_cast<const uint4*>(&lds_b[buf][(wj * WT_PIX + j * 16 + fr) * KROW + fk]));
-#pragma unroll
-    for (int i = 0; i < FI; ++i)
+      for (int i = 0; i < FI; ++i)
+        fa[i] = as_frag(*reinterpret_cast<const uint4*>(&lds_a[buf][(wi * WT_CO + i * 16 + fr) * KROW + fk]));
 #pragma unroll
       for (int j = 0; j < FJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    if (kt + 1 < nk) store_stage(buf ^ 1);
-    __syncthreads();
+        fb[j] = as_frag(*reinterpret_cast<const uint4*>(&lds_b[buf][(wj * WT_PIX + j * 16 + fr) * KROW + fk]));
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      if (more) store_stage(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
   }
 
   // ------------------------------------------------------------ epilogue --
   const float gam = a.res ? *a.gamma : 1.f;
 #pragma unroll
-  for (int i = 0; i < FI; ++i) {
-    const int co = co0 + wi * WT_CO + i * 16 + (lane >> 4) * 4;
-    if (co >= a.Mrows) continue;
-    float bv[4];
+  for (int j = 0; j < FJ; ++j) {
+    const int pc = pix0 + wj * WT_PIX + j * 16 + fr;
+    if (pc >= Pc) continue;
+    long p = pc;
+    if (MODE == MODE_BWDD && a.ncls > 1) {
+      const int hw = CH * CW;
+      const int n = pc / hw, rem = pc - n * hw;
+      const int yy = rem / CW, xx = rem - yy * CW;
+      p = ((long)n * a.OH + qy + stc * yy) * a.OW + qx + stc * xx;
+    }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bv[r] = (a.bias && co + r < a.Mrows) ? a.bias[co + r] : 0.f;
+    for (int i = 0; i < FI; ++i) {
+      const int co = co0 + wi * WT_CO + i * 16 + (lane >> 4) * 4;
+      if (co >= a.Mrows) continue;
+      if (a.nsplit > 1) {
+        float* dst = a.part + ((long)split * a.P + p) * a.Mrows + co;
 #pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-      const int p = pix0 + wj * WT_PIX + j * 16 + fr;
-      if (p >= a.P) continue;
+        for (int r = 0; r < 4; ++r)
+          if (co + r < a.Mrows) dst[r] = acc[i][j][r];
+        continue;
+      }
       float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = act_fwd(acc[i][j][r] + bv[r], a.act, a.slope);
+      for (int r = 0; r < 4; ++r) {
+        const float bv = (a.bias && co + r < a.Mrows) ? a.bias[co + r] : 0.f;
+        v[r] = act_fwd(acc[i][j][r] + bv, a.act, a.slope);
+      }
       if (a.res) {
-        const bf16_t* rp = a.res + (long)p * a.ldres + co;
+        const bf16_t* rp = a.res + p * a.ldres + co;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (co + r < a.Mrows) v[r] = bf2f(rp[r]) + gam * v[r];
       }
       if (a.out_f32) {
-        float* op = reinterpret_cast<float*>(a.out) + (long)p * a.ldo + co;
+        float* op = reinterpret_cast<float*>(a.out) + p * a.ldo + co;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (co + r < a.Mrows) op[r] = v[r];
       } else {
-        bf16_t* op = reinterpret_cast<bf16_t*>(a.out) + (long)p * a.ldo + co;
-        if (co + 4 <= a.Mrows && ((a.ldo & 3) == 0)) {
+        bf16_t* op = reinterpret_cast<bf16_t*>(a.out) + p * a.ldo + co;
+        if (co + 4 <= a.Mrows) {
           *reinterpret_cast<uint2*>(op) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         } else {
 #pragma unroll
@@ -247,18 +277,36 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   }
 }
 
+// split-K reduction + epilogue: out[p][co] = res + gamma*act(sum_z part[z][p][co] + bias)
+__global__ void conv_splitk_reduce_kernel(ConvArgs a) {
+  const long total = (long)a.P * a.Mrows;
+  const float gam = a.res ? *a.gamma : 1.f;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long p = e / a.Mrows;
+    const int co = e - p * a.Mrows;
+    float v = 0.f;
+    for (int z = 0; z < a.nsplit; ++z) v += a.part[(long)z * total + e];
+    v = act_fwd(v + (a.bias ? a.bias[co] : 0.f), a.act, a.slope);
+    if (a.res) v = bf2f(a.res[p * a.ldres + co]) + gam * v;
+    if (a.out_f32) reinterpret_cast<float*>(a.out)[p * a.ldo + co] = v;
+    else reinterpret_cast<bf16_t*>(a.out)[p * a.ldo + co] = f2bf(v);
+  }
+}
+
 // ---------------------------------------------------------- WGRAD kernel --
 struct WgradArgs {
-  ConvArgs g;          // gather geometry of x (MODE_FWD), K = R*S*Cg
+  const bf16_t* x;     // [N][IH>>up2][IW>>up2][ldx]
   const bf16_t* dy;    // [P][lddy]
-  int lddy, Cout;
   float* ws;           // [nsplit][Cout][K]
-  int p_per_split;
+  int N, IH, IW, ldx, up2;
+  int OH, OW, R, S, st, ph, pw;
+  int Cg, Cin, K;      // K = R*S*Cg, Cg = round_up(Cin, 8)
+  int lddy, Cout, P, p_per_split;
 };
 
 constexpr int TRP = 4;  // row padding (elements) for transposed-read tiles
 
-template <bool VECX, bool VECDY, int TCO, int TK, int WCO>
+template <int TCO, int TK, int WCO>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs w) {
   constexpr int WKK = 4 / WCO;
   constexpr int WT_CO = TCO / WCO, WT_K = TK / WKK;
@@ -270,13 +318,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs w) {
   __shared__ __attribute__((aligned(16))) bf16_t lds_d[2][BK * DROW];
   __shared__ __attribute__((aligned(16))) bf16_t lds_x[2][BK * XROW];
 
-  const ConvArgs& a = w.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wi = wave / WKK, wj = wave % WKK;
   const int co0 = blockIdx.y * TCO, kb0 = blockIdx.x * TK;
   const int p_begin = blockIdx.z * w.p_per_split;
-  const int p_end = min(a.P, p_begin + w.p_per_split);
-  const int hw = a.OH * a.OW;
+  const int p_end = min(w.P, p_begin + w.p_per_split);
+  const int hw = w.OH * w.OW;
+  const int PH = w.IH >> w.up2, PW = w.IW >> w.up2;
 
   uint2 rd[D_PER][2];
   uint4 rx[X_PER];
@@ -288,18 +336,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs w) {
         const int pr = ch / (TCO / 8), cc = ch % (TCO / 8);
         const int p = p0 + pr, co = co0 + cc * 8;
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (p < p_end) {
-          const bf16_t* src = w.dy + (long)p * w.lddy + co;
-          if (VECDY && co + 8 <= w.Cout) {
-            v = *reinterpret_cast<const uint4*>(src);
-          } else {
-            uint16_t e[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) e[j] = (co + j < w.Cout) ? src[j] : 0;
-            v = make_uint4(e[0] | ((uint32_t)e[1] << 16), e[2] | ((uint32_t)e[3] << 16),
-                           e[4] | ((uint32_t)e[5] << 16), e[6] | ((uint32_t)e[7] << 16));
-          }
-        }
+        if (p < p_end && co < w.Cout) v = mask_chunk(*reinterpret_cast<const uint4*>(w.dy + (long)p * w.lddy + co), co, w.Cout);
         rd[i][0] = make_uint2(v.x, v.y);
         rd[i][1] = make_uint2(v.z, v.w);
       }
@@ -310,11 +347,20 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs w) {
       if (ch < X_CHUNKS) {
         const int pr = ch / (TK / 8), kc = ch % (TK / 8);
         const int p = p0 + pr;
-        const bool ok = p < p_end;
-        const int pp = ok ? p : 0;
-        const int n = pp / hw, rem = pp - n * hw;
-        const int y = rem / a.OW, x = rem - y * a.OW;
-        rx[i] = gather_chunk<MODE_FWD, VECX>(a, ok, n, y, x, kb0 + kc * 8);
+        const int k = kb0 + kc * 8;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (p < p_end && k < w.K) {
+          const int n = p / hw, rem = p - n * hw;
+          const int oy = rem / w.OW, ox = rem - oy * w.OW;
+          const int tap = k / w.Cg, c = k - tap * w.Cg;
+          const int r = tap / w.S, s = tap - r * w.S;
+          const int iy = oy * w.st - w.ph + r, ix = ox * w.st - w.pw + s;
+          if (c < w.Cin && (unsigned)iy < (unsigned)w.IH && (unsigned)ix < (unsigned)w.IW) {
+            const long off = ((long)(n * PH + (iy >> w.up2)) * PW + (ix >> w.up2)) * w.ldx + c;
+            v = mask_chunk(*reinterpret_cast<const uint4*>(w.x + off), c, w.Cin);
+          }
+        }
+        rx[i] = v;
       }
     }
   };
@@ -382,7 +428,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs w) {
       buf ^= 1;
     }
   }
-  float* ws = w.ws + (long)blockIdx.z * w.Cout * a.K;
+  float* ws = w.ws + (long)blockIdx.z * w.Cout * w.K;
 #pragma unroll
   for (int i = 0; i < FI; ++i) {
 #pragma unroll
@@ -392,7 +438,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs w) {
 #pragma unroll
       for (int j = 0; j < FJ; ++j) {
         const int k = kb0 + wj * WT_K + j * 16 + li;
-        if (k < a.K) ws[(long)co * a.K + k] = acc[i][j][r];
+        if (k < w.K) ws[(long)co * w.K + k] = acc[i][j][r];
       }
     }
   }
@@ -417,83 +463,168 @@ __global__ void wgrad_reduce_kernel(const float* ws, int nsplit, int Cout, int C
 }
 
 // ------------------------------------------------------- weight packing --
-// FWD pack:  out[co][(r*S+s)*Cg + c] = W[co][c][r][s] * scale[co]   (zero pad)
-// BWDD pack: out[ci][(r*S+s)*Cg + co] = W[co][ci][r][s]
+// FWD pack:  out[co][(r*S+s)*Cgp + c] = W[co][c][r][s] * scale[co]   (zero padded)
+// BWDD pack: out[ci][(r*S+s)*Cgp + co] = W[co][ci][r][s] * scale[co]
 __global__ void pack_weights_kernel(const float* w, const float* scale, int Cout, int Cin, int R, int S,
-                                    int transposed, int Cg, int rows_pad, int Kpad, bf16_t* out) {
-  const long total = (long)rows_pad * Kpad;
+                                    int transposed, int Cgp, int rows_pad, int Kw, bf16_t* out) {
+  const long total = (long)rows_pad * Kw;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int row = e / Kpad, k = e % Kpad;
+    const int row = e / Kw, k = e % Kw;
+    const int rs = k / Cgp, c = k - rs * Cgp;
+    const int r = rs / S, s = rs - r * S;
     float v = 0.f;
-    const int rs = k / Cg, c = k - rs * Cg;
-    if (rs < R * S) {
-      const int r = rs / S, s = rs - r * S;
-      if (!transposed) {
-        if (row < Cout && c < Cin) v = w[(((long)row * Cin + c) * R + r) * S + s] * (scale ? scale[row] : 1.f);
-      } else {
-        if (row < Cin && c < Cout) v = w[(((long)c * Cin + row) * R + r) * S + s] * (scale ? scale[c] : 1.f);
-      }
+    if (!transposed) {
+      if (row < Cout && c < Cin) v = w[(((long)row * Cin + c) * R + r) * S + s] * (scale ? scale[row] : 1.f);
+    } else {
+      if (row < Cin && c < Cout) v = w[(((long)c * Cin + row) * R + r) * S + s] * (scale ? scale[c] : 1.f);
     }
     out[e] = f2bf(v);
   }
 }
 
 // ------------------------------------------------------------ dispatch --
-int gather_channels(int C, int ld) { return (C >= 8 && (ld % 8) == 0) ? ee_round_up(C, 8) : C; }
-bool vec_ok(int C, int ld) { return C >= 8 && (ld % 8) == 0 && ld >= ee_round_up(C, 8); }
+int cgp_of(int C) { return ee_round_up(C, BK); }
 
-template <int MODE, bool VEC>
-int launch_igemm(const ConvArgs& a, hipStream_t s) {
+struct Plan {
+  int tco, tpix, nsplit, blocks;
+};
+
+Plan plan_igemm(const ConvArgs& a, int Pc_max) {
   const int rows = a.Mrows;
-  if (rows > 64) {
-    dim3 grid(ee_cdiv(a.P, 128), ee_cdiv(rows, 128));
-    conv_igemm_kernel<MODE, VEC, 128, 128, 2><<<grid, 256, 0, s>>>(a);
-  } else if (rows > 32) {
-    dim3 grid(ee_cdiv(a.P, 128), ee_cdiv(rows, 64));
-    conv_igemm_kernel<MODE, VEC, 64, 128, 2><<<grid, 256, 0, s>>>(a);
-  } else if (rows > 16) {
-    dim3 grid(ee_cdiv(a.P, 256), ee_cdiv(rows, 32));
-    conv_igemm_kernel<MODE, VEC, 32, 256, 1><<<grid, 256, 0, s>>>(a);
-  } else {
-    dim3 grid(ee_cdiv(a.P, 256), ee_cdiv(rows, 16));
-    conv_igemm_kernel<MODE, VEC, 16, 256, 1><<<grid, 256, 0, s>>>(a);
+  Plan p;
+  p.tco = rows > 64 ? 128 : rows > 32 ? 64 : rows > 16 ? 32 : 16;
+  const int co_t = ee_cdiv(rows, p.tco);
+  p.tpix = (p.tco <= 32) ? 256 : 128;
+  if ((long)ee_cdiv(Pc_max, p.tpix) * co_t * a.ncls < 512) p.tpix = 64;
+  p.blocks = ee_cdiv(Pc_max, p.tpix) * co_t * a.ncls;
+  // split K until the grid covers the chip twice, keeping >= 8 K-steps per split
+  int taps = a.R * a.S;
+  if (a.ncls > 1) taps = ee_cdiv(a.R, a.st) * ee_cdiv(a.S, a.st);
+  const int nk = taps * (a.Cgp / BK);
+  p.nsplit = 1;
+  while (p.blocks * p.nsplit < 512 && nk / (p.nsplit * 2) >= 8 && p.nsplit < 64) p.nsplit *= 2;
+  return p;
+}
+
+template <int MODE>
+int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s) {
+  Plan p = plan_igemm(a, Pc_max);
+  a.nsplit = p.nsplit;
+  a.part = p.nsplit > 1 ? part_ws : nullptr;
+  if (p.nsplit > 1 && !part_ws) {
+    ee_set_error("conv: split-K workspace missing");
+    return -22;
   }
-  return ee_check_launch(MODE == MODE_FWD ? "conv_fwd" : "conv_bwd_data");
+  dim3 grid(ee_cdiv(Pc_max, p.tpix), ee_cdiv(a.Mrows, p.tco), a.ncls * p.nsplit);
+#define IG(TC, TP, WC) conv_igemm_kernel<MODE, TC, TP, WC><<<grid, 256, 0, s>>>(a)
+  if (p.tco == 128) { if (p.tpix == 128) IG(128, 128, 2); else IG(128, 64, 2); }
+  else if (p.tco == 64) { if (p.tpix == 128) IG(64, 128, 2); else IG(64, 64, 2); }
+  else if (p.tco == 32) { if (p.tpix == 256) IG(32, 256, 1); else IG(32, 64, 1); }
+  else { if (p.tpix == 256) IG(16, 256, 1); else IG(16, 64, 1); }
+#undef IG
+  int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd" : "conv_bwd_data");
+  if (rc || p.nsplit == 1) return rc;
+  const long total = (long)a.P * a.Mrows;
+  conv_splitk_reduce_kernel<<<(int)std::min<long>((total + 255) / 256, 4096), 256, 0, s>>>(a);
+  return ee_check_launch("conv_splitk_reduce");
 }
 
-}  // namespace
-
-extern "C" {
-
-long eegan_conv_packed_elems(int Cout, int Cin, int R, int S, int transposed, int Cg) {
-  const int rows = transposed ? Cin : Cout;
-  return (long)ee_round_up(rows, 128) * ee_round_up(R * S * Cg, BK);
+long part_bytes(const ConvArgs& a, int Pc_max) {
+  Plan p = plan_igemm(a, Pc_max);
+  return p.nsplit > 1 ? (long)p.nsplit * a.P * a.Mrows * (long)sizeof(float) : 0;
 }
 
-int eegan_conv_gather_channels(int C, int ld) { return gather_channels(C, ld); }
-
-int eegan_conv_pack_weights(const float* w, const float* scale, int Cout, int Cin, int R, int S,
-                            int transposed, int Cg, bf16_t* out, hipStream_t stream) {
-  const int rows = transposed ? Cin : Cout;
-  const int rows_pad = ee_round_up(rows, 128), Kpad = ee_round_up(R * S * Cg, BK);
-  const long total = (long)rows_pad * Kpad;
-  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
-  pack_weights_kernel<<<blocks, 256, 0, stream>>>(w, scale, Cout, Cin, R, S, transposed, Cg, rows_pad, Kpad, out);
-  return ee_check_launch("pack_weights");
-}
-
-static void fill_geom(ConvArgs& a, const eegan_conv_desc* d) {
+void fill_fwd(ConvArgs& a, const eegan_conv_desc* d) {
+  a = ConvArgs{};
+  a.N = d->N;
+  a.IH = d->H;
+  a.IW = d->W;
+  a.lds_src = d->ldx;
+  a.up2 = d->up2;
+  a.OH = d->Ho;
+  a.OW = d->Wo;
   a.R = d->R;
   a.S = d->S;
   a.st = d->stride;
   a.ph = d->pad_h;
   a.pw = d->pad_w;
+  a.Cgp = cgp_of(d->C);
+  a.Cvalid = d->C;
+  a.Mrows = d->K;
+  a.Kw = d->R * d->S * a.Cgp;
+  a.P = d->N * d->Ho * d->Wo;
+  a.ncls = 1;
+  a.nsplit = 1;
+}
+
+void fill_bwdd(ConvArgs& a, const eegan_conv_desc* d) {
+  a = ConvArgs{};
+  a.N = d->N;
+  a.IH = d->Ho;  // source grid = dy grid
+  a.IW = d->Wo;
+  a.lds_src = d->ldy;
+  a.up2 = 0;
+  a.OH = d->H;   // GEMM pixels = input pixels
+  a.OW = d->W;
+  a.R = d->R;
+  a.S = d->S;
+  a.st = d->stride;
+  a.ph = d->pad_h;
+  a.pw = d->pad_w;
+  a.Cgp = cgp_of(d->K);
+  a.Cvalid = d->K;
+  a.Mrows = d->C;
+  a.Kw = d->R * d->S * a.Cgp;
+  a.P = d->N * d->H * d->W;
+  a.ncls = d->stride > 1 ? d->stride * d->stride : 1;
+  a.nsplit = 1;
+}
+
+int bwdd_pc_max(const eegan_conv_desc* d) {
+  if (d->stride == 1) return d->N * d->H * d->W;
+  return d->N * ee_cdiv(d->H, d->stride) * ee_cdiv(d->W, d->stride);
+}
+
+bool ld_ok(int ld, const void* p) { return (ld % 8) == 0 && ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+long eegan_conv_packed_elems(int Cout, int Cin, int R, int S, int transposed) {
+  const int rows = transposed ? Cin : Cout;
+  const int Cgp = cgp_of(transposed ? Cout : Cin);
+  return (long)ee_round_up(rows, 128) * R * S * Cgp;
+}
+
+int eegan_conv_pack_weights(const float* w, const float* scale, int Cout, int Cin, int R, int S, int transposed,
+                            bf16_t* out, hipStream_t stream) {
+  const int rows = transposed ? Cin : Cout;
+  const int Cgp = cgp_of(transposed ? Cout : Cin);
+  const int rows_pad = ee_round_up(rows, 128), Kw = R * S * Cgp;
+  const long total = (long)rows_pad * Kw;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+  pack_weights_kernel<<<blocks, 256, 0, stream>>>(w, scale, Cout, Cin, R, S, transposed, Cgp, rows_pad, Kw, out);
+  return ee_check_launch("pack_weights");
+}
+
+long eegan_conv_fwd_workspace(const eegan_conv_desc* d) {
+  ConvArgs a;
+  fill_fwd(a, d);
+  return part_bytes(a, a.P);
+}
+
+long eegan_conv_bwd_data_workspace(const eegan_conv_desc* d) {
+  ConvArgs a;
+  fill_bwdd(a, d);
+  return part_bytes(a, bwdd_pc_max(d));
 }
 
 int eegan_conv_fwd(const eegan_conv_desc* d, const bf16_t* x, const bf16_t* wpack, const float* bias, int act,
-                   float slope, const bf16_t* res, int ldres, const float* gamma, void* y, int y_f32,
+                   float slope, const bf16_t* res, int ldres, const float* gamma, void* y, int y_f32, float* ws,
                    hipStream_t stream) {
-  ConvArgs a = {};
+  ConvArgs a;
+  fill_fwd(a, d);
   a.src = x;
   a.wp = wpack;
   a.bias = bias;
@@ -505,64 +636,45 @@ int eegan_conv_fwd(const eegan_conv_desc* d, const bf16_t* x, const bf16_t* wpac
   a.out_f32 = y_f32;
   a.act = act;
   a.slope = slope;
-  a.N = d->N;
-  a.IH = d->H;
-  a.IW = d->W;
-  a.lds_src = d->ldx;
-  a.up2 = d->up2;
-  a.OH = d->Ho;
-  a.OW = d->Wo;
-  fill_geom(a, d);
-  a.Cvalid = d->C;
-  a.Cg = gather_channels(d->C, d->ldx);
-  a.Mrows = d->K;
-  a.P = d->N * d->Ho * d->Wo;
-  a.K = d->R * d->S * a.Cg;
-  a.Kpad = ee_round_up(a.K, BK);
   if (a.P == 0) return 0;
   if (res && !gamma) {
     ee_set_error("conv_fwd: residual without gamma");
     return -22;
   }
-  return vec_ok(d->C, d->ldx) ? launch_igemm<MODE_FWD, true>(a, stream) : launch_igemm<MODE_FWD, false>(a, stream);
+  if (!ld_ok(d->ldx, x)) {
+    ee_set_error("conv_fwd: input channel stride %d must be a multiple of 8 (16-B aligned rows)", d->ldx);
+    return -22;
+  }
+  return launch_igemm<MODE_FWD>(a, a.P, ws, stream);
 }
 
 int eegan_conv_bwd_data(const eegan_conv_desc* d, const bf16_t* dy, const bf16_t* wpackT, void* dx, int lddx,
-                        int dx_f32, hipStream_t stream) {
+                        int dx_f32, float* ws, hipStream_t stream) {
   if (d->up2) {
     ee_set_error("conv_bwd_data: up2 inputs take the hi-res gradient + sum-pool path");
     return -22;
   }
-  ConvArgs a = {};
+  ConvArgs a;
+  fill_bwdd(a, d);
   a.src = dy;
   a.wp = wpackT;
   a.out = dx;
   a.ldo = lddx;
   a.out_f32 = dx_f32;
   a.act = ACT_NONE;
-  a.N = d->N;
-  a.IH = d->Ho;  // source grid = dy grid
-  a.IW = d->Wo;
-  a.lds_src = d->ldy;
-  a.up2 = 0;
-  a.OH = d->H;   // GEMM pixels = input pixels
-  a.OW = d->W;
-  fill_geom(a, d);
-  a.Cvalid = d->K;
-  a.Cg = gather_channels(d->K, d->ldy);
-  a.Mrows = d->C;
-  a.P = d->N * d->H * d->W;
-  a.K = d->R * d->S * a.Cg;
-  a.Kpad = ee_round_up(a.K, BK);
   if (a.P == 0) return 0;
-  return vec_ok(d->K, d->ldy) ? launch_igemm<MODE_BWDD, true>(a, stream) : launch_igemm<MODE_BWDD, false>(a, stream);
+  if (!ld_ok(d->ldy, dy)) {
+    ee_set_error("conv_bwd_data: dy channel stride %d must be a multiple of 8", d->ldy);
+    return -22;
+  }
+  return launch_igemm<MODE_BWDD>(a, bwdd_pc_max(d), ws, stream);
 }
 
 static void wgrad_plan(const eegan_conv_desc* d, int& TCO, int& TK, int& nsplit, int& pps, int& K) {
-  const int Cg = gather_channels(d->C, d->ldx);
+  const int Cg = ee_round_up(d->C, 8);
   K = d->R * d->S * Cg;
   TCO = d->K > 64 ? 128 : (d->K > 16 ? 64 : 16);
-  TK = 128;
+  TK = K > 64 ? 128 : 64;
   const int P = d->N * d->Ho * d->Wo;
   const int tiles = ee_cdiv(d->K, TCO) * ee_cdiv(K, TK);
   int want = std::max(1, 1024 / std::max(tiles, 1));
@@ -582,39 +694,40 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
                           int accumulate, hipStream_t stream) {
   int TCO, TK, nsplit, pps, K;
   wgrad_plan(d, TCO, TK, nsplit, pps, K);
+  if (!ld_ok(d->ldx, x) || !ld_ok(d->ldy, dy)) {
+    ee_set_error("conv_bwd_weight: channel strides (%d, %d) must be multiples of 8", d->ldx, d->ldy);
+    return -22;
+  }
   WgradArgs w = {};
-  ConvArgs& a = w.g;
-  a.src = x;
-  a.N = d->N;
-  a.IH = d->H;
-  a.IW = d->W;
-  a.lds_src = d->ldx;
-  a.up2 = d->up2;
-  a.OH = d->Ho;
-  a.OW = d->Wo;
-  fill_geom(a, d);
-  a.Cvalid = d->C;
-  a.Cg = gather_channels(d->C, d->ldx);
-  a.P = d->N * d->Ho * d->Wo;
-  a.K = K;
+  w.x = x;
   w.dy = dy;
+  w.ws = ws;
+  w.N = d->N;
+  w.IH = d->H;
+  w.IW = d->W;
+  w.ldx = d->ldx;
+  w.up2 = d->up2;
+  w.OH = d->Ho;
+  w.OW = d->Wo;
+  w.R = d->R;
+  w.S = d->S;
+  w.st = d->stride;
+  w.ph = d->pad_h;
+  w.pw = d->pad_w;
+  w.Cg = ee_round_up(d->C, 8);
+  w.Cin = d->C;
+  w.K = K;
   w.lddy = d->ldy;
   w.Cout = d->K;
-  w.ws = ws;
+  w.P = d->N * d->Ho * d->Wo;
   w.p_per_split = pps;
-  if (a.P > 0) {
+  if (w.P > 0) {
     dim3 grid(ee_cdiv(K, TK), ee_cdiv(d->K, TCO), nsplit);
-    const bool vx = vec_ok(d->C, d->ldx);
-    const bool vd = (d->ldy % 8) == 0;
-#define WG_LAUNCH(VX, VD)                                                              \
-  if (TCO == 128) conv_wgrad_kernel<VX, VD, 128, 128, 2><<<grid, 256, 0, stream>>>(w); \
-  else if (TCO == 64) conv_wgrad_kernel<VX, VD, 64, 128, 2><<<grid, 256, 0, stream>>>(w); \
-  else conv_wgrad_kernel<VX, VD, 16, 128, 1><<<grid, 256, 0, stream>>>(w);
-    if (vx && vd) { WG_LAUNCH(true, true) }
-    else if (vx) { WG_LAUNCH(true, false) }
-    else if (vd) { WG_LAUNCH(false, true) }
-    else { WG_LAUNCH(false, false) }
-#undef WG_LAUNCH
+#define WG(TC, TKK, WC) conv_wgrad_kernel<TC, TKK, WC><<<grid, 256, 0, stream>>>(w)
+    if (TCO == 128) { if (TK == 128) WG(128, 128, 2); else WG(128, 64, 2); }
+    else if (TCO == 64) { if (TK == 128) WG(64, 128, 2); else WG(64, 64, 2); }
+    else { if (TK == 128) WG(16, 128, 1); else WG(16, 64, 1); }
+#undef WG
     int rc = ee_check_launch("conv_wgrad");
     if (rc) return rc;
   } else {
@@ -622,7 +735,7 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
   }
   const long total = (long)d->K * d->C * d->R * d->S;
   const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
-  wgrad_reduce_kernel<<<blocks, 256, 0, stream>>>(ws, nsplit, d->K, d->C, d->R, d->S, a.Cg, K, dw, accumulate);
+  wgrad_reduce_kernel<<<blocks, 256, 0, stream>>>(ws, nsplit, d->K, d->C, d->R, d->S, w.Cg, K, dw, accumulate);
   return ee_check_launch("wgrad_reduce");
 }
 

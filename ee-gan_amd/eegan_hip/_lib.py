@@ -33,11 +33,12 @@ CD, BD = C.POINTER(ConvDesc), C.POINTER(BnModDesc)
 _SIGS = {
     'eegan_last_error': ([], C.c_char_p),
     'eegan_abi_version': ([], I),
-    'eegan_conv_packed_elems': ([I, I, I, I, I, I], L),
-    'eegan_conv_gather_channels': ([I, I], I),
-    'eegan_conv_pack_weights': ([P, P, I, I, I, I, I, I, P, P], I),
-    'eegan_conv_fwd': ([CD, P, P, P, I, F, P, I, P, P, I, P], I),
-    'eegan_conv_bwd_data': ([CD, P, P, P, I, I, P], I),
+    'eegan_conv_packed_elems': ([I, I, I, I, I], L),
+    'eegan_conv_pack_weights': ([P, P, I, I, I, I, I, P, P], I),
+    'eegan_conv_fwd_workspace': ([CD], L),
+    'eegan_conv_bwd_data_workspace': ([CD], L),
+    'eegan_conv_fwd': ([CD, P, P, P, I, F, P, I, P, P, I, P, P], I),
+    'eegan_conv_bwd_data': ([CD, P, P, P, I, I, P, P], I),
     'eegan_conv_wgrad_workspace': ([CD], L),
     'eegan_conv_bwd_weight': ([CD, P, P, P, P, I, P], I),
     'eegan_bn_stats_workspace': ([L, I], L),
@@ -117,7 +118,7 @@ class HipError(RuntimeError):
 
 def _wrap(name):
     fn = getattr(LIB, name)
-    if _SIGS[name][1] is not I or name in ('eegan_conv_gather_channels', 'eegan_abi_version'):
+    if _SIGS[name][1] is not I or name == 'eegan_abi_version':
         return fn
 
     def call(*args):

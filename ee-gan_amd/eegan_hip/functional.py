@@ -54,38 +54,38 @@ class PackCache:
         self.scale = scale  # optional per-output-channel fp32 scale folded into the packs
 
     @staticmethod
-    def _key(W, Cg):
+    def _key(W):
         gen = getattr(W, '_eegan_gen', None)
-        return (W.data_ptr(), W._version, gen[0] if gen is not None else 0, Cg)
+        return (W.data_ptr(), W._version, gen[0] if gen is not None else 0)
 
-    def get(self, W, Cg, transposed):
-        key = self._key(W, Cg)
+    def get(self, W, transposed):
+        key = self._key(W)
         if transposed:
             if self.bwd_key != key:
-                self.bwd = pack_weight(W, Cg, True, self.scale)
+                self.bwd = pack_weight(W, True, self.scale)
                 self.bwd_key = key
             return self.bwd
         if self.fwd_key != key:
-            self.fwd = pack_weight(W, Cg, False, self.scale)
+            self.fwd = pack_weight(W, False, self.scale)
             self.fwd_key = key
         return self.fwd
 
 
-def pack_weight(W, Cg, transposed, scale=None):
+def pack_weight(W, transposed, scale=None):
     Cout, Cin, R, S = W.shape
-    n = ops.conv_packed_elems(Cout, Cin, R, S, int(transposed), Cg)
+    n = ops.conv_packed_elems(Cout, Cin, R, S, int(transposed))
     out = torch.empty(n, dtype=BF16, device=W.device)
     Wc = W.detach()
     if not Wc.is_contiguous() or Wc.dtype != F32:
         Wc = Wc.float().contiguous()
-    ops.conv_pack_weights(Wc.data_ptr(), ptr(scale), Cout, Cin, R, S, int(transposed), Cg, out.data_ptr(), stream())
+    ops.conv_pack_weights(Wc.data_ptr(), ptr(scale), Cout, Cin, R, S, int(transposed), out.data_ptr(), stream())
     return out
 
 
-def _pack(W, cache, Cg, transposed):
+def _pack(W, cache, transposed):
     if cache is not None:
-        return cache.get(W, Cg, transposed)
-    return pack_weight(W, Cg, transposed)
+        return cache.get(W, transposed)
+    return pack_weight(W, transposed)
 
 
 class Geom:
@@ -169,13 +169,14 @@ def conv_fwd_raw(x, W, b, g, act=0, slope=0.2, out_f32=False, cache=None, res=No
     Ho, Wo = g.out_hw(H, Wd)
     y = empty_nhwc(N, g.K, Ho, Wo, x.device, dtype=F32 if out_f32 else BF16)
     d = _desc_io(g, x.shape, ld_of(x), ld_of(y))
-    Cg = ops.conv_gather_channels(C, ld_of(x))
-    wp = _pack(W, cache, Cg, False)
+    wp = _pack(W, cache, False)
+    wsb = ops.conv_fwd_workspace(d)
+    ws = workspace(wsb, x.device) if wsb else None
     flops = 2.0 * N * Ho * Wo * g.K * C * g.R * g.S
     nbytes = 2.0 * (N * H * Wd * C + N * Ho * Wo * g.K * (2 if out_f32 else 1) + g.K * C * g.R * g.S)
     _launch('conv_fwd', flops, nbytes, lambda: ops.conv_fwd(
         d, x.data_ptr(), wp.data_ptr(), ptr(b), act, slope, ptr(res), ld_of(res) if res is not None else 0,
-        ptr(gamma), y.data_ptr(), int(out_f32), stream()), key=_shape_key(d) if TIMER is not None else None)
+        ptr(gamma), y.data_ptr(), int(out_f32), ptr(ws), stream()), key=_shape_key(d) if TIMER is not None else None)
     return y
 
 
@@ -184,16 +185,18 @@ def conv_bwd_data_raw(dz, W, g, x_shape, cache=None):
     N, C, H, Wd = x_shape
     Hl, Wl = (H * 2, Wd * 2) if g.up2 else (H, Wd)
     dx = empty_nhwc(N, C, Hl, Wl, dz.device)
+    dz = to_nhwc_bf16(dz)
     d = _desc_io(g, x_shape, T.ld_for(C), ld_of(dz))
     if g.up2:
         d.H, d.W, d.up2 = Hl, Wl, 0
-    Cg = ops.conv_gather_channels(g.K, ld_of(dz))
-    wp = _pack(W, cache, Cg, True)
+    wp = _pack(W, cache, True)
+    wsb = ops.conv_bwd_data_workspace(d)
+    ws = workspace(wsb, dz.device) if wsb else None
     Ho, Wo = d.Ho, d.Wo
     flops = 2.0 * N * Ho * Wo * g.K * C * g.R * g.S
     nbytes = 2.0 * (N * Hl * Wl * C + N * Ho * Wo * g.K + g.K * C * g.R * g.S)
     _launch('conv_bwd_data', flops, nbytes, lambda: ops.conv_bwd_data(
-        d, dz.data_ptr(), wp.data_ptr(), dx.data_ptr(), ld_of(dx), 0, stream()),
+        d, dz.data_ptr(), wp.data_ptr(), dx.data_ptr(), ld_of(dx), 0, ptr(ws), stream()),
         key=_shape_key(d) if TIMER is not None else None)
     if g.up2:
         lo = empty_nhwc(N, C, H, Wd, dz.device)

@@ -14,8 +14,12 @@ BF16 = torch.bfloat16
 F32 = torch.float32
 
 
-def ld_for(C):
-    return C if C < 8 else (C + 7) // 8 * 8
+def ld_for(C, dtype=BF16):
+    """bf16 activations: channel stride rounded up to 8 (16-byte pixel rows, so
+    even 3-channel images feed the vectorised gathers); fp32 tensors: dense."""
+    if dtype != BF16:
+        return C
+    return (C + 7) // 8 * 8
 
 
 def stream():
@@ -23,7 +27,7 @@ def stream():
 
 
 def empty_nhwc(N, C, H, W, device, dtype=BF16, ld=None):
-    ld = ld_for(C) if ld is None else ld
+    ld = ld_for(C, dtype) if ld is None else ld
     buf = torch.empty((N, H, W, ld), dtype=dtype, device=device)
     if ld != C:
         buf = buf[..., :C]
@@ -39,15 +43,19 @@ def ld_of(t):
         return t.stride(2)
     if N > 1:
         return t.stride(0)
-    return ld_for(C)
+    return ld_for(C, t.dtype)
 
 
 def is_nhwc(t):
+    """NHWC-stored activation usable by the kernels: bf16 needs ld % 8 == 0
+    and a 16-byte aligned base; fp32 is accepted dense or padded."""
     if t.dim() != 4 or t.stride(1) != 1 and t.shape[1] > 1:
         return False
     N, C, H, W = t.shape
     ld = ld_of(t)
-    if ld < C or (C >= 8 and ld % 8) or (C < 8 and ld != C):
+    if ld < C:
+        return False
+    if t.dtype == BF16 and (ld % 8 or t.data_ptr() % 16):
         return False
     if W > 1 and t.stride(3) != ld:
         return False

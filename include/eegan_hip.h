@@ -45,20 +45,24 @@ typedef struct eegan_conv_desc {
   int Ho, Wo, ldy;      /* output grid and channel stride */
 } eegan_conv_desc;
 
-/* elements of the packed bf16 weight image; Cg = eegan_conv_gather_channels(C_gathered, ld) */
-long eegan_conv_packed_elems(int Cout, int Cin, int R, int S, int transposed, int Cg);
-int eegan_conv_gather_channels(int C, int ld);
+/* elements of the packed bf16 weight image (rows padded to 128, each tap's channel run to 32) */
+long eegan_conv_packed_elems(int Cout, int Cin, int R, int S, int transposed);
 /* torch layout W[Cout][Cin][R][S] fp32 (x optional per-Cout scale) -> packed bf16.
- * transposed=0: forward image [Cout][R][S][Cg(Cin)]; 1: bwd-data image [Cin][R][S][Cg(Cout)] */
+ * transposed=0: forward image [Cout][R][S][Cin_32]; 1: bwd-data image [Cin][R][S][Cout_32] */
 int eegan_conv_pack_weights(const float* w, const float* scale, int Cout, int Cin, int R, int S,
-                            int transposed, int Cg, uint16_t* out, hipStream_t stream);
-/* y = res + gamma * act(conv(x, W) + bias)   (res/gamma optional; act: 0 none,1 relu,2 lrelu,3 tanh,4 sigmoid) */
+                            int transposed, uint16_t* out, hipStream_t stream);
+/* split-K partial-slab bytes the call needs (0 when the grid is large enough) */
+long eegan_conv_fwd_workspace(const eegan_conv_desc* d);
+long eegan_conv_bwd_data_workspace(const eegan_conv_desc* d);
+/* y = res + gamma * act(conv(x, W) + bias)   (res/gamma optional; act: 0 none,1 relu,2 lrelu,3 tanh,4 sigmoid)
+ * x channel stride must be a multiple of 8 (16-byte rows) */
 int eegan_conv_fwd(const eegan_conv_desc* d, const uint16_t* x, const uint16_t* wpack, const float* bias,
                    int act, float slope, const uint16_t* res, int ldres, const float* gamma, void* y,
-                   int y_f32, hipStream_t stream);
-/* dx (logical input grid, channel stride lddx) = conv_transpose(dy, W) */
+                   int y_f32, float* ws, hipStream_t stream);
+/* dx (logical input grid, channel stride lddx) = conv_transpose(dy, W); stride-s passes run as
+ * s*s parity classes that visit only their valid taps */
 int eegan_conv_bwd_data(const eegan_conv_desc* d, const uint16_t* dy, const uint16_t* wpackT, void* dx,
-                        int lddx, int dx_f32, hipStream_t stream);
+                        int lddx, int dx_f32, float* ws, hipStream_t stream);
 /* dW[Cout][Cin][R][S] (fp32, torch layout) = sum_pixels dy x im2col(x); split-K slabs in ws */
 long eegan_conv_wgrad_workspace(const eegan_conv_desc* d);
 int eegan_conv_bwd_weight(const eegan_conv_desc* d, const uint16_t* x, const uint16_t* dy, float* ws, float* dw,

@@ -25,6 +25,10 @@ TOL_BWD = 6e-2
 # gives: generator input grads 8-9% rel-L2, Inception-v3 input grads 29%; the
 # kernels here measure 9% and 30%.  Deep-gradient tolerances reflect that.
 TOL_DEEP = 0.15
+# Per-parameter generator gradients under the same simulation: median 8.8%,
+# worst 0.22 (blocks.0.conv_mask.1.bias, a 100-channel BN bias deep in the
+# mask head).  Each parameter is held to TOL_GEN_PARAM, the median to 0.12.
+TOL_GEN_PARAM = 0.3
 # entries whose reference value is ill-conditioned: attr_key.bias has an
 # identically-zero true gradient (softmax shift invariance); sagb_id's gamma
 # gradient is sum(dout*h) = -0.43 against sum|dout*h| = 193 (condition ~450).
@@ -46,6 +50,7 @@ def _check(name, got_t, ref_fp, tol):
     _LOG.append((name, e))
     print('PARITY %-50s rel_l2=%.3e (tol %.0e)' % (name, e, tol))
     assert e <= tol, (name, e)
+    return e
 
 
 @pytest.fixture(scope='module', autouse=True)
@@ -63,9 +68,10 @@ def _load(mod, name, seed, dev):
     return mod.to(dev)
 
 
-def _grads(tag, mod, tol=TOL_BWD, skip=()):
+def _grads(tag, mod, tol=TOL_BWD, skip=(), median_tol=None):
     g = golden()
     n = 0
+    errs = []
     for k, p in mod.named_parameters():
         key = tag + '/grad/' + k
         if key in g and not any(s in k for s in skip):
@@ -76,9 +82,11 @@ def _grads(tag, mod, tol=TOL_BWD, skip=()):
                 e = _rel_fp(p.grad, g[key])
                 print('PARITY %-50s rel_l2=%.3e (scalar reduction, reported only)' % (key, e))
                 continue
-            _check(key, p.grad, g[key], tol)
+            errs.append(_check(key, p.grad, g[key], tol))
             n += 1
     assert n > 0
+    if median_tol is not None:
+        assert float(np.median(errs)) <= median_tol, (tag, float(np.median(errs)))
 
 
 @pytest.mark.parametrize('tag,cin,cout,pm,res', [('sagb_sc', 16, 8, True, 8), ('sagb_id', 16, 16, True, 4),
@@ -189,7 +197,7 @@ def test_generator(gpu):
     loss.backward()
     _check('gen/ds', s.grad, g['gen/dinput/s'], TOL_DEEP)
     _check('gen/da', a.grad, g['gen/dinput/a'], TOL_DEEP)
-    _grads('gen', G, TOL_DEEP)
+    _grads('gen', G, TOL_GEN_PARAM, median_tol=0.12)
     for k, v in G.state_dict().items():
         if 'running' in k:
             _check('gen/' + k, v, g['gen/after/' + k], 2e-2)
