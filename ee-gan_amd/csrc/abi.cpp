@@ -6,8 +6,12 @@
 #include <string.h>
 
 #include "../../include/eegan_hip.h"
+#include "common.h"
 
 static thread_local char g_err[512];
+static thread_local EeTiming g_timing;
+
+EeTiming& ee_timing() { return g_timing; }
 
 void ee_set_error(const char* fmt, ...) {
   va_list ap;
@@ -25,7 +29,47 @@ int ee_check_launch(const char* what) {
   return 0;
 }
 
+static int ee_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    ee_set_error("%s: %s", what, hipGetErrorString(e));
+    return -(int)e;
+  }
+  return 0;
+}
+
 extern "C" {
 const char* eegan_last_error(void) { return g_err; }
 int eegan_abi_version(void) { return EEGAN_ABI_VERSION; }
+
+// Launch timing (bench.py's roofline).  A record on a stream that is being
+// captured becomes an external event-record node, so a replayed step graph
+// re-times every bracketed launch.
+int eegan_event_create(hipEvent_t* ev) { return ee_hip(hipEventCreate(ev), "hipEventCreate"); }
+int eegan_event_destroy(hipEvent_t ev) { return ee_hip(hipEventDestroy(ev), "hipEventDestroy"); }
+int eegan_event_record(hipEvent_t ev, hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  int rc = ee_hip(hipStreamIsCapturing(s, &st), "hipStreamIsCapturing");
+  if (rc) return rc;
+  if (st == hipStreamCaptureStatusActive)
+    return ee_hip(hipEventRecordWithFlags(ev, s, hipEventRecordExternal), "hipEventRecordWithFlags");
+  return ee_hip(hipEventRecord(ev, s), "hipEventRecord");
+}
+int eegan_event_elapsed(hipEvent_t a, hipEvent_t b, float* ms) {
+  return ee_hip(hipEventElapsedTime(ms, a, b), "hipEventElapsedTime");
+}
+int eegan_timing_arm(hipEvent_t start0, hipEvent_t stop0, hipEvent_t start1, hipEvent_t stop1) {
+  g_timing.ev[0] = start0;
+  g_timing.ev[1] = stop0;
+  g_timing.ev[2] = start1;
+  g_timing.ev[3] = stop1;
+  g_timing.used = 0;
+  g_timing.armed = 1;
+  return 0;
+}
+int eegan_timing_disarm(int* kernels_timed) {
+  *kernels_timed = g_timing.armed ? g_timing.used : 0;
+  g_timing.armed = 0;
+  g_timing.used = 0;
+  return 0;
+}
 }

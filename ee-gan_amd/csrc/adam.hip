@@ -6,14 +6,25 @@
 // calls of train.py:452-459, 500-502.  Arithmetic follows torch's Adam:
 //   m = lerp(m, g, 1-b1); v = b2 v + (1-b2) g^2;
 //   p -= step_size * m / (sqrt(v)/sqrt(bc2) + eps),  step_size = lr / bc1.
+// The step count lives on the device (a tick kernel increments it before the
+// update reads it), so a captured step graph replays with the right bias
+// corrections.
 #include "common.h"
 #include "../../include/eegan_hip.h"
 
 namespace {
 
+__global__ void adam_tick_kernel(double* step) { *step += 1.0; }
+
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long n, float b1,
-                                                   float b2, float step_size, float bc2_sqrt, float eps, float wd) {
+                                                   float b2, float lr, float eps, float wd,
+                                                   const double* __restrict__ step) {
+  // bias corrections in double from the device step count, as torch's
+  // python-float arithmetic does
+  const double t = *step;
+  const float step_size = (float)((double)lr / (1.0 - pow((double)b1, t)));
+  const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, t));
   const long n4 = n / 4;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n4; e += (long)gridDim.x * blockDim.x) {
     float4 pp = reinterpret_cast<float4*>(p)[e];
@@ -50,15 +61,18 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 
 extern "C" {
 
-int eegan_adam(float* p, const float* g, float* m, float* v, long n, float beta1, float beta2, float step_size,
-               float bc2_sqrt, float eps, float weight_decay, hipStream_t s) {
+int eegan_adam(float* p, const float* g, float* m, float* v, long n, float beta1, float beta2, float lr, float eps,
+               float weight_decay, double* step, hipStream_t s) {
   if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
        reinterpret_cast<uintptr_t>(v)) & 15) {
     ee_set_error("adam: buffers must be 16-byte aligned");
     return -22;
   }
   const int blocks = (int)std::max<long>(1, std::min<long>(2048, (n / 4 + 255) / 256));
-  adam_kernel<<<blocks, 256, 0, s>>>(p, g, m, v, n, beta1, beta2, step_size, bc2_sqrt, eps, weight_decay);
+  adam_tick_kernel<<<1, 1, 0, s>>>(step);
+  int rc = ee_check_launch("adam_tick");
+  if (rc) return rc;
+  adam_kernel<<<blocks, 256, 0, s>>>(p, g, m, v, n, beta1, beta2, lr, eps, weight_decay, step);
   return ee_check_launch("adam");
 }
 

@@ -78,14 +78,6 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(const bf16_t* __restrict
   }
 }
 
-__global__ void bn_reduce_kernel(const float* __restrict__ ws, int nblk, int C, double* __restrict__ sums) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * C) return;
-  double acc = 0.0;
-  for (int b = 0; b < nblk; ++b) acc += (double)ws[(long)b * 2 * C + c];
-  sums[c] = acc;
-}
-
 // stats[0..C) mean, [C..2C) inv_std, [2C..3C) 1 if d(inv_std)/d(var) != 0
 __global__ void bn_finalize_kernel(const double* __restrict__ sums, int C, double count, double sum_scale, float eps,
                                    float mom, int clamp_mode, float* __restrict__ rmean, float* __restrict__ rvar,
@@ -136,62 +128,83 @@ struct ModArgs {
   float slope;
 };
 
-EE_DEV void mod_coeffs(const ModArgs& a, int n, int c, float m, float& mul, float& add) {
-  // t = act(xhat * mul + add)
-  if (a.mode == 0) {
-    mul = a.w ? a.w[c] : 1.f;
-    add = a.b ? a.b[c] : 0.f;
-  } else {
-    const float g = a.gam[(long)n * a.C + c], be = a.bet[(long)n * a.C + c];
-    mul = g * m + 1.f;
-    add = be * m;
+// Blocks cover (pixel chunk, sample); a thread owns 8 consecutive channels
+// (one 16-byte NHWC load) for every pixel it visits, so the per-channel
+// statistics / modulation parameters of its sample stay in registers.
+struct ChanParams {
+  float mean[8], istd[8], pm[8], pa[8];  // mode 0: w, b ; mode 1: gam[n], bet[n]
+};
+
+EE_DEV void load_params(const ModArgs& a, int n, int c0, ChanParams& q) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = min(c0 + j, a.C - 1);
+    q.mean[j] = a.stats[c];
+    q.istd[j] = a.stats[a.C + c];
+    if (a.mode == 0) {
+      q.pm[j] = a.w ? a.w[c] : 1.f;
+      q.pa[j] = a.b ? a.b[c] : 0.f;
+    } else {
+      q.pm[j] = a.gam[(long)n * a.C + c];
+      q.pa[j] = a.bet[(long)n * a.C + c];
+    }
   }
 }
 
-__global__ __launch_bounds__(NT) void bnmod_fwd_kernel(ModArgs a, bf16_t* __restrict__ y, int ldy) {
+// t = act(xhat * mul + add)
+EE_DEV void coeffs(const ModArgs& a, const ChanParams& q, int j, float m, float& mul, float& add) {
+  if (a.mode == 0) {
+    mul = q.pm[j];
+    add = q.pa[j];
+  } else {
+    mul = q.pm[j] * m + 1.f;
+    add = q.pa[j] * m;
+  }
+}
+
+EE_DEV void unpack8(uint4 v, float (&f)[8]) {
+  const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[2 * j] = lo_f(w4[j]);
+    f[2 * j + 1] = hi_f(w4[j]);
+  }
+}
+
+EE_DEV void store8(bf16_t* dst, const float (&o)[8], int nvalid) {
+  if (nvalid >= 8) {
+    *reinterpret_cast<uint4*>(dst) = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < nvalid) dst[j] = f2bf(o[j]);
+  }
+}
+
+// grid (chunks, N): output pixels [chunk*ppc, ...) of sample n
+__global__ __launch_bounds__(NT) void bnmod_fwd_kernel(ModArgs a, bf16_t* __restrict__ y, int ldy, int ppc) {
+  const int C8 = (a.C + 7) / 8, rows = NT / C8;
+  const int row = threadIdx.x / C8, cg = threadIdx.x - row * C8;
+  if (row >= rows) return;
+  const int n = blockIdx.y, c0 = cg * 8, nv = a.C - c0;
   const int Ho = a.H << a.up2, Wo = a.W << a.up2;
-  const int C8 = (a.C + 7) / 8;
-  const long total = (long)a.N * Ho * Wo * C8;
-  for (long e = blockIdx.x * (long)NT + threadIdx.x; e < total; e += (long)gridDim.x * NT) {
-    const int cg = e % C8;
-    const long p = e / C8;
-    const int ox = p % Wo;
-    const long t = p / Wo;
-    const int oy = t % Ho;
-    const int n = t / Ho;
+  const long HWo = (long)Ho * Wo;
+  const long q1 = min(HWo, (long)(blockIdx.x + 1) * ppc);
+  ChanParams P;
+  load_params(a, n, c0, P);
+  for (long q = (long)blockIdx.x * ppc + row; q < q1; q += rows) {
+    const int oy = q / Wo, ox = q - (long)oy * Wo;
     const long ip = ((long)n * a.H + (oy >> a.up2)) * a.W + (ox >> a.up2);
-    const int c0 = cg * 8;
-    const float m = a.mode == 1 ? a.mask[(long)n * Ho * Wo + (long)oy * Wo + ox] : 0.f;
-    float xv[8];
-    if ((a.ldx % 8) == 0) {
-      uint4 v = *reinterpret_cast<const uint4*>(a.x + ip * a.ldx + c0);
-      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        xv[2 * j] = lo_f(w4[j]);
-        xv[2 * j + 1] = hi_f(w4[j]);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) xv[j] = (c0 + j < a.C) ? bf2f(a.x[ip * a.ldx + c0 + j]) : 0.f;
-    }
-    float o[8];
+    const float m = a.mode == 1 ? a.mask[(long)n * HWo + q] : 0.f;
+    float xv[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(a.x + ip * a.ldx + c0), xv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = min(c0 + j, a.C - 1);
       float mul, add;
-      mod_coeffs(a, n, c, m, mul, add);
-      const float xh = (xv[j] - a.stats[c]) * a.stats[a.C + c];
-      o[j] = act_fwd(xh * mul + add, a.act, a.slope);
+      coeffs(a, P, j, m, mul, add);
+      o[j] = act_fwd((xv[j] - P.mean[j]) * P.istd[j] * mul + add, a.act, a.slope);
     }
-    bf16_t* dst = y + p * ldy + c0;
-    if ((ldy % 8) == 0 && c0 + 8 <= ldy) {
-      *reinterpret_cast<uint4*>(dst) = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (c0 + j < a.C) dst[j] = f2bf(o[j]);
-    }
+    store8(y + ((long)n * HWo + q) * ldy + c0, o, nv);
   }
 }
 
@@ -221,6 +234,8 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_reduce_kernel(ModArgs a, const b
     for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
   const int c0 = cg * 8;
   float* red = sh;                 // [rows][C8] for dmask
+  ChanParams P;
+  if (row < rows) load_params(a, n, c0, P);
   // base of the pixel loop must be block-uniform for the dmask reduction
   for (long qb = q0; qb < q1; qb += rows) {
     const long q = qb + row;
@@ -230,31 +245,30 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_reduce_kernel(ModArgs a, const b
       const long ip = ((long)n * a.H + (oy >> a.up2)) * a.W + (ox >> a.up2);
       const long op = (long)n * HWo + q;
       const float m = a.mode == 1 ? a.mask[op] : 0.f;
+      float xv[8], gv[8];
+      unpack8(*reinterpret_cast<const uint4*>(a.x + ip * a.ldx + c0), xv);
+      unpack8(*reinterpret_cast<const uint4*>(dt + op * lddt + c0), gv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int c = c0 + j;
-        if (c < C) {
-          const float xv = bf2f(a.x[ip * a.ldx + c]);
-          const float gv = bf2f(dt[op * lddt + c]);
-          const float xh = (xv - a.stats[c]) * a.stats[C + c];
-          float mul, add;
-          mod_coeffs(a, n, c, m, mul, add);
-          const float tv = xh * mul + add;
-          float g = gv;
-          if (a.act == ACT_RELU) g = tv > 0.f ? g : 0.f;
-          else if (a.act == ACT_LRELU) g = tv > 0.f ? g : g * a.slope;
-          const float dxh = g * mul;
-          if (a.mode == 1) {
-            acc[0][j] += g * m * xh;
-            acc[1][j] += g * m;
-            dm += g * (a.gam[(long)n * C + c] * xh + a.bet[(long)n * C + c]);
-          } else {
-            acc[0][j] += g * xh;
-            acc[1][j] += g;
-          }
-          acc[2][j] += dxh;
-          acc[3][j] += dxh * xh;
+        const bool ok = c0 + j < C;  // channel padding may hold anything
+        const float xh = ok ? (xv[j] - P.mean[j]) * P.istd[j] : 0.f;
+        float mul, add;
+        coeffs(a, P, j, m, mul, add);
+        const float tv = xh * mul + add;
+        float g = ok ? gv[j] : 0.f;
+        if (a.act == ACT_RELU) g = tv > 0.f ? g : 0.f;
+        else if (a.act == ACT_LRELU) g = tv > 0.f ? g : g * a.slope;
+        const float dxh = g * mul;
+        if (a.mode == 1) {
+          acc[0][j] += g * m * xh;
+          acc[1][j] += g * m;
+          dm += g * (P.pm[j] * xh + P.pa[j]);
+        } else {
+          acc[0][j] += g * xh;
+          acc[1][j] += g;
         }
+        acc[2][j] += dxh;
+        acc[3][j] += dxh * xh;
       }
     }
     if (a.mode == 1 && dmask) {
@@ -287,92 +301,84 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_reduce_kernel(ModArgs a, const b
   }
 }
 
-// sum the chunks: dparam0/dparam1 ([C] for affine (summed over n), [N][C] for ssa),
-// chan[0..C) = sum dxhat, chan[C..2C) = sum dxhat*xhat (double)
-__global__ void bnmod_bwd_sums_kernel(const float* __restrict__ ws, int N, int nchunk, int C, int mode,
-                                      float* __restrict__ d0, float* __restrict__ d1, double* __restrict__ chan) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+// per-sample chunk sums tmp[n][4C] (double, deterministic column reduce) ->
+// dparam0/dparam1 ([C] for affine (summed over n), [N][C] for ssa),
+// chan[0..C) = sum dxhat, chan[C..2C) = sum dxhat*xhat
+__global__ void bnmod_bwd_sums_kernel(const double* __restrict__ tmp, int N, int C, int mode, float* __restrict__ d0,
+                                      float* __restrict__ d1, double* __restrict__ chan) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 4 * C) return;
+  const int i = j / C, c = j - i * C;
+  double s = 0;
   for (int n = 0; n < N; ++n) {
-    double p0 = 0, p1 = 0;
-    for (int k = 0; k < nchunk; ++k) {
-      const float* w = ws + ((long)n * nchunk + k) * 4 * C;
-      p0 += w[c];
-      p1 += w[C + c];
-      s2 += w[2 * C + c];
-      s3 += w[3 * C + c];
+    const double v = tmp[(long)n * 4 * C + j];
+    s += v;
+    if (mode == 1 && i < 2) {
+      float* d = i == 0 ? d0 : d1;
+      if (d) d[(long)n * C + c] = (float)v;
     }
-    if (mode == 1) {
-      if (d0) d0[(long)n * C + c] = (float)p0;
-      if (d1) d1[(long)n * C + c] = (float)p1;
-    }
-    s0 += p0;
-    s1 += p1;
   }
-  if (mode == 0) {
-    if (d0) d0[c] = (float)s0;
-    if (d1) d1[c] = (float)s1;
+  if (i >= 2) chan[(i - 2) * C + c] = s;
+  else if (mode == 0) {
+    float* d = i == 0 ? d0 : d1;
+    if (d) d[c] = (float)s;
   }
-  chan[c] = s2;
-  chan[C + c] = s3;
 }
 
 // ------------------------------------------------------ backward, pass 2 --
 // dx (physical input grid) = istd * (dxhat - mean(dxhat) - xhat*mean(dxhat*xhat)), summed
-// over the 2x2 children when the forward upsampled.
+// over the 2x2 children when the forward upsampled.  grid (chunks, N) over
+// input pixels of sample n.
 __global__ __launch_bounds__(NT) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_t* __restrict__ dt, int lddt,
                                                           const double* __restrict__ chan, double count,
-                                                          bf16_t* __restrict__ dx, int lddx) {
-  const int C8 = (a.C + 7) / 8;
+                                                          bf16_t* __restrict__ dx, int lddx, int ppc) {
+  const int C8 = (a.C + 7) / 8, rows = NT / C8;
+  const int row = threadIdx.x / C8, cg = threadIdx.x - row * C8;
+  if (row >= rows) return;
+  const int n = blockIdx.y, c0 = cg * 8, nv = a.C - c0;
   const int Ho = a.H << a.up2, Wo = a.W << a.up2;
-  const long total = (long)a.N * a.H * a.W * C8;
+  const long HW = (long)a.H * a.W;
+  const long q1 = min(HW, (long)(blockIdx.x + 1) * ppc);
   const int nch = a.up2 ? 4 : 1;
-  for (long e = blockIdx.x * (long)NT + threadIdx.x; e < total; e += (long)gridDim.x * NT) {
-    const int cg = e % C8;
-    const long ip = e / C8;
-    const int ix = ip % a.W;
-    const long tt = ip / a.W;
-    const int iy = tt % a.H;
-    const int n = tt / a.H;
-    const int c0 = cg * 8;
-    float o[8];
+  ChanParams P;
+  load_params(a, n, c0, P);
+  float vg[8], m1[8], m2[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = 0.f;
+  for (int j = 0; j < 8; ++j) {
+    const int c = min(c0 + j, a.C - 1);
+    vg[j] = a.stats[2 * a.C + c];
+    m1[j] = (float)(chan[c] / count);
+    m2[j] = (float)(chan[a.C + c] / count);
+  }
+  for (long q = (long)blockIdx.x * ppc + row; q < q1; q += rows) {
+    const int iy = q / a.W, ix = q - (long)iy * a.W;
+    const long ip = (long)n * HW + q;
+    float xh[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(a.x + ip * a.ldx + c0), xh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xh[j] = (xh[j] - P.mean[j]) * P.istd[j];
+      o[j] = 0.f;
+    }
     for (int ch = 0; ch < nch; ++ch) {
       const int oy = (iy << a.up2) + (ch >> 1), ox = (ix << a.up2) + (ch & 1);
       const long op = ((long)n * Ho + oy) * Wo + ox;
       const float m = a.mode == 1 ? a.mask[op] : 0.f;
+      float gv[8];
+      unpack8(*reinterpret_cast<const uint4*>(dt + op * lddt + c0), gv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int c = c0 + j;
-        if (c < a.C) {
-          const float xv = bf2f(a.x[ip * a.ldx + c]);
-          const float gv = bf2f(dt[op * lddt + c]);
-          const float mean = a.stats[c], istd = a.stats[a.C + c], vg = a.stats[2 * a.C + c];
-          const float xh = (xv - mean) * istd;
-          float mul, add;
-          mod_coeffs(a, n, c, m, mul, add);
-          const float tv = xh * mul + add;
-          float g = gv;
-          if (a.act == ACT_RELU) g = tv > 0.f ? g : 0.f;
-          else if (a.act == ACT_LRELU) g = tv > 0.f ? g : g * a.slope;
-          const float dxh = g * mul;
-          const float m1 = (float)(chan[c] / count), m2 = (float)(chan[a.C + c] / count);
-          o[j] += istd * (dxh - m1 - vg * xh * m2);
-        }
+        float mul, add;
+        coeffs(a, P, j, m, mul, add);
+        const float tv = xh[j] * mul + add;
+        float g = gv[j];
+        if (a.act == ACT_RELU) g = tv > 0.f ? g : 0.f;
+        else if (a.act == ACT_LRELU) g = tv > 0.f ? g : g * a.slope;
+        o[j] += P.istd[j] * (g * mul - m1[j] - vg[j] * xh[j] * m2[j]);
       }
     }
-    bf16_t* dst = dx + ip * lddx + c0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (c0 + j < a.C) dst[j] = f2bf(o[j]);
+    store8(dx + ip * lddx + c0, o, nv);
   }
-}
-
-int grid_for(long work, int per_block = NT) {
-  long b = (work + per_block - 1) / per_block;
-  return (int)std::max<long>(1, std::min<long>(b, 8192));
 }
 
 ModArgs make_args(const eegan_bnmod_desc* d) {
@@ -394,6 +400,22 @@ ModArgs make_args(const eegan_bnmod_desc* d) {
   a.act = d->act;
   a.slope = d->slope;
   return a;
+}
+
+// chunks of a per-sample pixel range: ~2048 blocks overall, >= 8 pixel rows per block
+int pix_chunks(int N, long HW, int C, int& ppc) {
+  const int rows = NT / ((C + 7) / 8);
+  ppc = (int)std::max<long>((long)rows * 8, (HW * N + 2047) / 2048);
+  return std::max(1, ee_cdiv(HW, ppc));
+}
+
+bool vec_ok(const eegan_bnmod_desc* d, int ld, const void* p, const char* what) {
+  if ((d->ldx % 8) || (ld % 8) || ((uintptr_t)d->x & 15) || ((uintptr_t)p & 15) || (d->C + 7) / 8 > NT) {
+    ee_set_error("%s: bf16 rows must be 16-byte aligned with channel strides multiple of 8 (ldx %d, ld %d, C %d)",
+                 what, d->ldx, ld, d->C);
+    return false;
+  }
+  return true;
 }
 
 int bwd_chunks(const eegan_bnmod_desc* d, int& ppc) {
@@ -430,7 +452,7 @@ int eegan_bn_stats(const uint16_t* x, long P, int C, int ld, float* ws, double* 
   bn_partial_kernel<<<nblk, NT, shm, stream>>>(x, P, C, ld, rpb, ws);
   int rc = ee_check_launch("bn_partial");
   if (rc) return rc;
-  bn_reduce_kernel<<<ee_cdiv(2 * C, 256), 256, 0, stream>>>(ws, nblk, C, sums);
+  launch_colsum<double, double>(ws, nblk, 2 * C, 2 * C, 0, sums, 0, 1, 0, stream);
   return ee_check_launch("bn_reduce");
 }
 
@@ -443,20 +465,24 @@ int eegan_bn_finalize(const double* sums, int C, double count, double sum_scale,
 
 int eegan_bnmod_fwd(const eegan_bnmod_desc* d, uint16_t* y, int ldy, hipStream_t stream) {
   ModArgs a = make_args(d);
-  const long work = (long)d->N * (d->H << d->up2) * (d->W << d->up2) * ((d->C + 7) / 8);
-  bnmod_fwd_kernel<<<grid_for(work), NT, 0, stream>>>(a, y, ldy);
+  if (!vec_ok(d, ldy, y, "bnmod_fwd")) return -22;
+  int ppc;
+  const int chunks = pix_chunks(d->N, (long)(d->H << d->up2) * (d->W << d->up2), d->C, ppc);
+  bnmod_fwd_kernel<<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc);
   return ee_check_launch("bnmod_fwd");
 }
 
 long eegan_bnmod_bwd_workspace(const eegan_bnmod_desc* d) {
   int ppc;
   const int chunks = bwd_chunks(d, ppc);
-  return (long)d->N * chunks * 4 * d->C * (long)sizeof(float);
+  // chunk partials (fp32) + per-sample sums (fp64)
+  return (long)d->N * chunks * 4 * d->C * (long)sizeof(float) + (long)d->N * 4 * d->C * (long)sizeof(double);
 }
 
 int eegan_bnmod_bwd(const eegan_bnmod_desc* d, const uint16_t* dt, int lddt, float* ws, float* dparam0,
                     float* dparam1, float* dmask, double* chan, hipStream_t stream) {
   ModArgs a = make_args(d);
+  if (!vec_ok(d, lddt, dt, "bnmod_bwd")) return -22;
   int ppc;
   const int chunks = bwd_chunks(d, ppc);
   const int C8 = (d->C + 7) / 8;
@@ -470,16 +496,22 @@ int eegan_bnmod_bwd(const eegan_bnmod_desc* d, const uint16_t* dt, int lddt, flo
   bnmod_bwd_reduce_kernel<<<grid, NT, shm, stream>>>(a, dt, lddt, ppc, ws, dmask);
   int rc = ee_check_launch("bnmod_bwd_reduce");
   if (rc) return rc;
-  bnmod_bwd_sums_kernel<<<ee_cdiv(d->C, 64), 64, 0, stream>>>(ws, d->N, chunks, d->C, d->mode, dparam0, dparam1,
-                                                               chan);
+  double* tmp = reinterpret_cast<double*>(ws + (long)d->N * chunks * 4 * d->C);
+  launch_colsum<double, double>(ws, chunks, 4L * d->C, 4L * d->C, (long)chunks * 4 * d->C, tmp, 4L * d->C, d->N, 0,
+                                stream);
+  rc = ee_check_launch("bnmod_bwd_colsum");
+  if (rc) return rc;
+  bnmod_bwd_sums_kernel<<<ee_cdiv(4 * d->C, 256), 256, 0, stream>>>(tmp, d->N, d->C, d->mode, dparam0, dparam1, chan);
   return ee_check_launch("bnmod_bwd_sums");
 }
 
 int eegan_bnmod_bwd_dx(const eegan_bnmod_desc* d, const uint16_t* dt, int lddt, const double* chan, double count,
                        uint16_t* dx, int lddx, hipStream_t stream) {
   ModArgs a = make_args(d);
-  const long work = (long)d->N * d->H * d->W * ((d->C + 7) / 8);
-  bnmod_bwd_dx_kernel<<<grid_for(work), NT, 0, stream>>>(a, dt, lddt, chan, count, dx, lddx);
+  if (!vec_ok(d, lddt, dt, "bnmod_bwd_dx") || !vec_ok(d, lddx, dx, "bnmod_bwd_dx")) return -22;
+  int ppc;
+  const int chunks = pix_chunks(d->N, (long)d->H * d->W, d->C, ppc);
+  bnmod_bwd_dx_kernel<<<dim3(chunks, d->N), NT, 0, stream>>>(a, dt, lddt, chan, count, dx, lddx, ppc);
   return ee_check_launch("bnmod_bwd_dx");
 }
 

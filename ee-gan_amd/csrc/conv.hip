@@ -302,6 +302,19 @@ struct WgradArgs {
   int OH, OW, R, S, st, ph, pw;
   int Cg, Cin, K;      // K = R*S*Cg, Cg = round_up(Cin, 8)
   int lddy, Cout, P, p_per_split;
+  float* dw;           // nsplit == 1: epilogue writes the torch layout directly
+  int accumulate;
+};
+
+// split-slab column (co, (tap, c)) -> torch layout [Cout][Cin][R][S]; padded channels dropped
+struct WgradMap {
+  int K, Cg, Cin, RS;
+  EE_DEV long operator()(long col) const {  // col < Cout*K < 2^31
+    const int ci = (int)col;
+    const int co = ci / K, k = ci - co * K;
+    const int tap = k / Cg, c = k - tap * Cg;
+    return c < Cin ? ((long)co * Cin + c) * RS + tap : -1;
+  }
 };
 
 constexpr int TRP = 4;  // row padding (elements) for transposed-read tiles
@@ -428,6 +441,24 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs w) {
       buf ^= 1;
     }
   }
+  if (w.dw) {
+    const WgradMap map{w.K, w.Cg, w.Cin, w.R * w.S};
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wi * WT_CO + i * 16 + g * 4 + r;
+        if (co >= w.Cout) continue;
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+          const int k = kb0 + wj * WT_K + j * 16 + li;
+          if (k >= w.K) continue;
+          const long o = map((long)co * w.K + k);
+          if (o >= 0) w.dw[o] = w.accumulate ? w.dw[o] + acc[i][j][r] : acc[i][j][r];
+        }
+      }
+    return;
+  }
   float* ws = w.ws + (long)blockIdx.z * w.Cout * w.K;
 #pragma unroll
   for (int i = 0; i < FI; ++i) {
@@ -441,24 +472,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs w) {
         if (k < w.K) ws[(long)co * w.K + k] = acc[i][j][r];
       }
     }
-  }
-}
-
-// sum the split slabs and scatter into the torch layout [Cout][Cin][R][S] (fp32)
-__global__ void wgrad_reduce_kernel(const float* ws, int nsplit, int Cout, int Cin, int R, int S,
-                                    int Cg, int K, float* dw, int accumulate) {
-  const long total = (long)Cout * Cin * R * S;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int s = e % S;
-    long t = e / S;
-    const int r = t % R;
-    t /= R;
-    const int c = t % Cin;
-    const int co = t / Cin;
-    const long k = (long)(r * S + s) * Cg + c;
-    float acc = 0.f;
-    for (int z = 0; z < nsplit; ++z) acc += ws[((long)z * Cout + co) * K + k];
-    dw[e] = accumulate ? dw[e] + acc : acc;
   }
 }
 
@@ -516,7 +529,7 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s) {
     return -22;
   }
   dim3 grid(ee_cdiv(Pc_max, p.tpix), ee_cdiv(a.Mrows, p.tco), a.ncls * p.nsplit);
-#define IG(TC, TP, WC) conv_igemm_kernel<MODE, TC, TP, WC><<<grid, 256, 0, s>>>(a)
+#define IG(TC, TP, WC) ee_launch(conv_igemm_kernel<MODE, TC, TP, WC>, grid, dim3(256), 0, s, a)
   if (p.tco == 128) { if (p.tpix == 128) IG(128, 128, 2); else IG(128, 64, 2); }
   else if (p.tco == 64) { if (p.tpix == 128) IG(64, 128, 2); else IG(64, 64, 2); }
   else if (p.tco == 32) { if (p.tpix == 256) IG(32, 256, 1); else IG(32, 64, 1); }
@@ -525,7 +538,7 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s) {
   int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd" : "conv_bwd_data");
   if (rc || p.nsplit == 1) return rc;
   const long total = (long)a.P * a.Mrows;
-  conv_splitk_reduce_kernel<<<(int)std::min<long>((total + 255) / 256, 4096), 256, 0, s>>>(a);
+  ee_launch(conv_splitk_reduce_kernel, dim3((int)std::min<long>((total + 255) / 256, 4096)), dim3(256), 0, s, a);
   return ee_check_launch("conv_splitk_reduce");
 }
 
@@ -677,8 +690,10 @@ static void wgrad_plan(const eegan_conv_desc* d, int& TCO, int& TK, int& nsplit,
   TK = K > 64 ? 128 : 64;
   const int P = d->N * d->Ho * d->Wo;
   const int tiles = ee_cdiv(d->K, TCO) * ee_cdiv(K, TK);
-  int want = std::max(1, 1024 / std::max(tiles, 1));
-  const int maxsplit = std::max(1, ee_cdiv(P, 256));
+  // ~2 blocks per CU, >= 16 K-steps (512 pixels) per split: the fp32 slab
+  // (nsplit x Cout x K) is written once and read once by the column reduce
+  int want = std::max(1, 512 / std::max(tiles, 1));
+  const int maxsplit = std::max(1, ee_cdiv(P, 512));
   nsplit = std::min(want, maxsplit);
   pps = ee_round_up(ee_cdiv(P, nsplit), BK);
   nsplit = ee_cdiv(P, pps);
@@ -721,21 +736,25 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
   w.Cout = d->K;
   w.P = d->N * d->Ho * d->Wo;
   w.p_per_split = pps;
+  if (nsplit == 1 && w.P > 0) {
+    w.dw = dw;
+    w.accumulate = accumulate;
+  }
   if (w.P > 0) {
     dim3 grid(ee_cdiv(K, TK), ee_cdiv(d->K, TCO), nsplit);
-#define WG(TC, TKK, WC) conv_wgrad_kernel<TC, TKK, WC><<<grid, 256, 0, stream>>>(w)
+#define WG(TC, TKK, WC) ee_launch(conv_wgrad_kernel<TC, TKK, WC>, grid, dim3(256), 0, stream, w)
     if (TCO == 128) { if (TK == 128) WG(128, 128, 2); else WG(128, 64, 2); }
     else if (TCO == 64) { if (TK == 128) WG(64, 128, 2); else WG(64, 64, 2); }
     else { if (TK == 128) WG(16, 128, 1); else WG(16, 64, 1); }
 #undef WG
     int rc = ee_check_launch("conv_wgrad");
-    if (rc) return rc;
+    if (rc || w.dw) return rc;
   } else {
     nsplit = 0;
   }
-  const long total = (long)d->K * d->C * d->R * d->S;
-  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
-  wgrad_reduce_kernel<<<blocks, 256, 0, stream>>>(ws, nsplit, d->K, d->C, d->R, d->S, w.Cg, K, dw, accumulate);
+  const long cols = (long)d->K * K;
+  launch_colsum<float, float>(ws, nsplit, cols, cols, 0, dw, 0, 1, accumulate, stream,
+                              WgradMap{K, w.Cg, d->C, d->R * d->S});
   return ee_check_launch("wgrad_reduce");
 }
 

@@ -152,14 +152,6 @@ __global__ __launch_bounds__(NT) void chansum_partial_kernel(const bf16_t* x, in
   }
 }
 
-__global__ void chansum_final_kernel(const float* ws, int nblk, int C, float* out, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float a = 0.f;
-  for (int b = 0; b < nblk; ++b) a += ws[(long)b * C + c];
-  out[c] = accumulate ? out[c] + a : a;
-}
-
 // 2x2 average pool (stride 2) and its adjoint
 __global__ void avgpool2_kernel(const bf16_t* x, int N, int H, int W, int C, int ld, bf16_t* y, int ldy) {
   const int Ho = H / 2, Wo = W / 2, C8 = (C + 7) / 8;
@@ -304,30 +296,71 @@ __global__ void bilinear_fwd_kernel(const void* x, int x_f32, int N, int H, int 
   }
 }
 
-// adjoint (scatter with fp32 atomics into a zeroed dx32 [N][H][W][C]); dy pre-scaled by
-// the sigmoid derivative when post == 1 (y = sigmoid output)
+// first output index whose sample pair (i0, i1) can touch input i, and one past the last
+EE_DEV void bil_range(int i, int in_size, int out_size, int align, int& lo, int& hi) {
+  int y0, y1;
+  float l;
+  float scale = align ? (out_size > 1 ? (float)(in_size - 1) / (float)(out_size - 1) : 0.f)
+                      : (float)in_size / (float)out_size;
+  int o = scale > 0.f ? (int)((float)(i - 1) / scale) - 2 : 0;
+  o = max(0, min(out_size - 1, o));
+  while (o > 0) {
+    bil_coord(o - 1, in_size, out_size, align, y0, y1, l);
+    if (y0 < i - 1) break;
+    --o;
+  }
+  while (o < out_size) {
+    bil_coord(o, in_size, out_size, align, y0, y1, l);
+    if (y0 >= i - 1) break;
+    ++o;
+  }
+  lo = o;
+  while (o < out_size) {
+    bil_coord(o, in_size, out_size, align, y0, y1, l);
+    if (y0 > i) break;
+    ++o;
+  }
+  hi = o;
+}
+
+// adjoint as a gather (deterministic, no atomics): every input element sums
+// the weighted output gradients of the output pixels that sampled it; dy is
+// pre-scaled by the sigmoid derivative when post == 1 (y = sigmoid output).
+// dx32 is [N][H][W][C] fp32.
 __global__ void bilinear_bwd_kernel(const void* dy, int dy_f32, const void* y, int y_f32, int lddy, int N, int H,
                                     int W, int C, int Ho, int Wo, int align, int post, float* dx32) {
-  GRID_LOOP(e, (long)N * Ho * Wo * C) {
+  GRID_LOOP(e, (long)N * H * W * C) {
     const int c = e % C;
     const long p = e / C;
-    const int ox = p % Wo;
-    const long t = p / Wo;
-    const int oy = t % Ho, n = t / Ho;
-    float g = rd(dy, p * lddy + c, dy_f32);
-    if (post == 1) {
-      const float s = rd(y, p * lddy + c, y_f32);
-      g *= s * (1.f - s);
+    const int ix = p % W;
+    const long t = p / W;
+    const int iy = t % H, n = t / H;
+    int oy0, oy1, ox0, ox1;
+    bil_range(iy, H, Ho, align, oy0, oy1);
+    bil_range(ix, W, Wo, align, ox0, ox1);
+    float acc = 0.f;
+    for (int oy = oy0; oy < oy1; ++oy) {
+      int y0, y1;
+      float ly;
+      bil_coord(oy, H, Ho, align, y0, y1, ly);
+      const float wy = (y0 == iy ? 1.f - ly : 0.f) + (y1 == iy ? ly : 0.f);
+      if (wy == 0.f) continue;
+      for (int ox = ox0; ox < ox1; ++ox) {
+        int x0, x1;
+        float lx;
+        bil_coord(ox, W, Wo, align, x0, x1, lx);
+        const float wx = (x0 == ix ? 1.f - lx : 0.f) + (x1 == ix ? lx : 0.f);
+        if (wx == 0.f) continue;
+        const long op = ((long)n * Ho + oy) * Wo + ox;
+        float g = rd(dy, op * lddy + c, dy_f32);
+        if (post == 1) {
+          const float sg = rd(y, op * lddy + c, y_f32);
+          g *= sg * (1.f - sg);
+        }
+        acc += g * (wy * wx);
+      }
     }
-    int y0, y1, x0, x1;
-    float ly, lx;
-    bil_coord(oy, H, Ho, align, y0, y1, ly);
-    bil_coord(ox, W, Wo, align, x0, x1, lx);
-    const long b = (long)n * H;
-    atomicAdd(dx32 + ((b + y0) * W + x0) * C + c, g * (1.f - ly) * (1.f - lx));
-    atomicAdd(dx32 + ((b + y0) * W + x1) * C + c, g * (1.f - ly) * lx);
-    atomicAdd(dx32 + ((b + y1) * W + x0) * C + c, g * ly * (1.f - lx));
-    atomicAdd(dx32 + ((b + y1) * W + x1) * C + c, g * ly * lx);
+    dx32[e] = acc;
   }
 }
 
@@ -511,7 +544,7 @@ int eegan_chansum(const uint16_t* x, int ld, long P, int C, float* ws, float* ou
   chansum_partial_kernel<<<nblk, NT, rows * C8 * 8 * sizeof(float), s>>>(x, ld, P, C, rpb, ws);
   int rc = ee_check_launch("chansum_partial");
   if (rc) return rc;
-  chansum_final_kernel<<<ee_cdiv(C, 256), 256, 0, s>>>(ws, nblk, C, out, accumulate);
+  launch_colsum<float, float>(ws, nblk, C, C, 0, out, 0, 1, accumulate, s);
   return ee_check_launch("chansum_final");
 }
 
@@ -553,8 +586,7 @@ int eegan_bilinear(const void* x, int x_f32, int N, int H, int W, int C, int ld,
 
 int eegan_bilinear_bwd(const void* dy, int dy_f32, const void* y, int y_f32, int lddy, int N, int H, int W, int C,
                        int Ho, int Wo, int align_corners, int post, float* dx32, hipStream_t s) {
-  (void)hipMemsetAsync(dx32, 0, (size_t)N * H * W * C * sizeof(float), s);
-  bilinear_bwd_kernel<<<grid_for((long)N * Ho * Wo * C), NT, 0, s>>>(dy, dy_f32, y, y_f32, lddy, N, H, W, C, Ho, Wo,
+  bilinear_bwd_kernel<<<grid_for((long)N * H * W * C), NT, 0, s>>>(dy, dy_f32, y, y_f32, lddy, N, H, W, C, Ho, Wo,
                                                                       align_corners, post, dx32);
   return ee_check_launch("bilinear_bwd");
 }

@@ -12,53 +12,56 @@
 
 namespace {
 
-constexpr int TM = 32, TN = 64, TKK = 16;
+// 16x16 output tile per 256-thread block (one output per thread).  Each K
+// chunk of 256 is staged into LDS with every thread issuing all its loads at
+// once (the operands are tiny; these GEMMs are latency-, not throughput-bound),
+// with the lane order chosen so the unit-stride axis of each operand is the
+// coalesced one.
+constexpr int T = 16, KC = 256;
 
-__global__ __launch_bounds__(256) void gemm_f32_kernel(const float* A, long sai, long sak, const float* B, long sbk,
-                                                       long sbj, float* C, long ldc, int M, int N, int K,
-                                                       const float* bias, int act, float alpha, float beta) {
-  __shared__ float As[TKK][TM + 1];
-  __shared__ float Bs[TKK][TN + 1];
-  const int tx = threadIdx.x % 16, ty = threadIdx.x / 16;  // 16 x 16 threads, each 2 (i) x 4 (j)
-  const int i0 = blockIdx.y * TM, j0 = blockIdx.x * TN;
-  float acc[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-  for (int k0 = 0; k0 < K; k0 += TKK) {
-    for (int e = threadIdx.x; e < TKK * TM; e += 256) {
-      const int kk = e % TKK, ii = e / TKK;
-      const int gi = i0 + ii, gk = k0 + kk;
-      As[kk][ii] = (gi < M && gk < K) ? A[gi * sai + gk * sak] : 0.f;
+__global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ A, long sai, long sak,
+                                                       const float* __restrict__ B, long sbk, long sbj,
+                                                       float* __restrict__ C, long ldc, int M, int N, int K,
+                                                       const float* __restrict__ bias, int act, float alpha,
+                                                       float beta) {
+  __shared__ float As[T][KC + 1];
+  __shared__ float Bs[KC][T + 1];
+  const int t = threadIdx.x, ti = t / T, tj = t % T;
+  const int i0 = blockIdx.y * T, j0 = blockIdx.x * T;
+  const bool a_k_fast = sak == 1, b_j_fast = sbj == 1;
+  float acc = 0.f;
+  for (int k0 = 0; k0 < K; k0 += KC) {
+    const int kc = min(KC, K - k0);
+    float av[T], bv[T];
+#pragma unroll
+    for (int r = 0; r < T; ++r) {
+      const int e = t + 256 * r;  // 0 .. 4095 over the 16 x 256 tile
+      int ii, kk;
+      if (a_k_fast) { ii = e / KC; kk = e % KC; } else { kk = e / T; ii = e % T; }
+      const int gi = i0 + ii;
+      av[r] = (gi < M && kk < kc) ? A[gi * sai + (long)(k0 + kk) * sak] : 0.f;
+      int jj, kb;
+      if (b_j_fast) { kb = e / T; jj = e % T; } else { jj = e / KC; kb = e % KC; }
+      const int gj = j0 + jj;
+      bv[r] = (gj < N && kb < kc) ? B[(long)(k0 + kb) * sbk + gj * sbj] : 0.f;
     }
-    for (int e = threadIdx.x; e < TKK * TN; e += 256) {
-      const int jj = e % TN, kk = e / TN;
-      const int gj = j0 + jj, gk = k0 + kk;
-      Bs[kk][jj] = (gj < N && gk < K) ? B[gk * sbk + gj * sbj] : 0.f;
+#pragma unroll
+    for (int r = 0; r < T; ++r) {
+      const int e = t + 256 * r;
+      if (a_k_fast) As[e / KC][e % KC] = av[r]; else As[e % T][e / T] = av[r];
+      if (b_j_fast) Bs[e / T][e % T] = bv[r]; else Bs[e % KC][e / KC] = bv[r];
     }
     __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < TKK; ++kk) {
-      const float a0 = As[kk][ty * 2], a1 = As[kk][ty * 2 + 1];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float b = Bs[kk][tx + 16 * q];
-        acc[0][q] += a0 * b;
-        acc[1][q] += a1 * b;
-      }
-    }
+#pragma unroll 8
+    for (int k = 0; k < kc; ++k) acc += As[ti][k] * Bs[k][tj];
     __syncthreads();
   }
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int gi = i0 + ty * 2 + p;
-    if (gi >= M) continue;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int gj = j0 + tx + 16 * q;
-      if (gj >= N) continue;
-      float v = alpha * acc[p][q] + (bias ? bias[gj] : 0.f);
-      v = act_fwd(v, act, 0.2f);
-      float* dst = C + gi * ldc + gj;
-      *dst = beta != 0.f ? beta * *dst + v : v;
-    }
+  const int gi = i0 + ti, gj = j0 + tj;
+  if (gi < M && gj < N) {
+    float v = alpha * acc + (bias ? bias[gj] : 0.f);
+    v = act_fwd(v, act, 0.2f);
+    float* dst = C + gi * ldc + gj;
+    *dst = beta != 0.f ? beta * *dst + v : v;
   }
 }
 
@@ -84,8 +87,8 @@ extern "C" {
 int eegan_gemm_f32(const float* A, long sai, long sak, const float* B, long sbk, long sbj, float* C, long ldc, int M,
                    int N, int K, const float* bias, int act, float alpha, float beta, hipStream_t s) {
   if (M == 0 || N == 0) return 0;
-  dim3 grid(ee_cdiv(N, TN), ee_cdiv(M, TM));
-  gemm_f32_kernel<<<grid, 256, 0, s>>>(A, sai, sak, B, sbk, sbj, C, ldc, M, N, K, bias, act, alpha, beta);
+  dim3 grid(ee_cdiv(N, T), ee_cdiv(M, T));
+  ee_launch(gemm_f32_kernel, grid, dim3(256), 0, s, A, sai, sak, B, sbk, sbj, C, ldc, M, N, K, bias, act, alpha, beta);
   return ee_check_launch("gemm_f32");
 }
 

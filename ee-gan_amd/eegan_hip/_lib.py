@@ -33,6 +33,12 @@ CD, BD = C.POINTER(ConvDesc), C.POINTER(BnModDesc)
 _SIGS = {
     'eegan_last_error': ([], C.c_char_p),
     'eegan_abi_version': ([], I),
+    'eegan_event_create': ([P], I),
+    'eegan_event_destroy': ([P], I),
+    'eegan_event_record': ([P, P], I),
+    'eegan_event_elapsed': ([P, P, P], I),
+    'eegan_timing_arm': ([P, P, P, P], I),
+    'eegan_timing_disarm': ([P], I),
     'eegan_conv_packed_elems': ([I, I, I, I, I], L),
     'eegan_conv_pack_weights': ([P, P, I, I, I, I, I, P, P], I),
     'eegan_conv_fwd_workspace': ([CD], L),
@@ -90,7 +96,7 @@ _SIGS = {
     'eegan_class_onehot': ([P, I, I, P, P, P], I),
     'eegan_attr_attn': ([P, P, P, I, I, I, F, P, P, P, P], I),
     'eegan_attr_attn_bwd': ([P, P, P, P, P, I, I, I, F, P, P, P, P], I),
-    'eegan_adam': ([P, P, P, P, L, F, F, F, F, F, F, P], I),
+    'eegan_adam': ([P, P, P, P, L, F, F, F, F, F, P, P], I),
     'eegan_embedding': ([P, L, P, I, P, P], I),
     'eegan_lstm_bidir': ([P, P, P, I, I, I, I, P, P, P], I),
 }

@@ -9,6 +9,7 @@ so they are differentiable to any order -- needed by the MA gradient penalty
 Generator-side Functions (BN modulation, upsample-fused convs, linears,
 mask resize) are first-order, as the reference only differentiates G once.
 """
+import ctypes
 import math
 
 import torch
@@ -42,11 +43,34 @@ def _needed(ctx, i):
         return True
 
 
+# When autograd would only add a parameter gradient into an existing fp32
+# p.grad (FlatAdam keeps p.grad as a view of its flat gradient buffer), the
+# kernels accumulate straight into p.grad and the Function returns None for
+# it: no temporary dW and no separate add launch.  Off under create_graph
+# (the gradient penalty's double backward) and for non-leaf inputs.
+DIRECT_PARAM_GRADS = True
+
+
+def _grad_sink(ctx, i):
+    if not DIRECT_PARAM_GRADS or torch.is_grad_enabled():
+        return None
+    node = ctx.next_functions[i][0]
+    var = getattr(node, 'variable', None)
+    if var is None:
+        return None
+    g = var.grad
+    if g is None or g.dtype != F32 or not g.is_contiguous() or g.shape != var.shape:
+        return None
+    return g
+
+
 # ============================================================== weights ===
 class PackCache:
     """bf16 packed images of one conv weight (forward and bwd-data layouts),
     rebuilt whenever the fp32 parameter changes (torch in-place version or
-    the flat-Adam generation counter)."""
+    the flat-Adam generation counter).  Rebuilds write into the SAME buffer:
+    a captured step graph keeps reading the address it captured, so a pack
+    refreshed later in the step (or by the next replay) must land there."""
 
     def __init__(self, scale=None):
         self.fwd_key = self.bwd_key = None
@@ -62,19 +86,20 @@ class PackCache:
         key = self._key(W)
         if transposed:
             if self.bwd_key != key:
-                self.bwd = pack_weight(W, True, self.scale)
+                self.bwd = pack_weight(W, True, self.scale, out=self.bwd)
                 self.bwd_key = key
             return self.bwd
         if self.fwd_key != key:
-            self.fwd = pack_weight(W, False, self.scale)
+            self.fwd = pack_weight(W, False, self.scale, out=self.fwd)
             self.fwd_key = key
         return self.fwd
 
 
-def pack_weight(W, transposed, scale=None):
+def pack_weight(W, transposed, scale=None, out=None):
     Cout, Cin, R, S = W.shape
     n = ops.conv_packed_elems(Cout, Cin, R, S, int(transposed))
-    out = torch.empty(n, dtype=BF16, device=W.device)
+    if out is None or out.numel() != n or out.device != W.device:
+        out = torch.empty(n, dtype=BF16, device=W.device)
     Wc = W.detach()
     if not Wc.is_contiguous() or Wc.dtype != F32:
         Wc = Wc.float().contiguous()
@@ -117,34 +142,59 @@ def _desc_io(g, x_shape, ldx, ldy):
 
 # ====================================================== launch timing ====
 class LaunchTimer(object):
-    """Brackets every launch of the conv kernels with HIP events on the stream
-    they run on (bench.py's roofline): records (kind, algorithmic flops,
-    algorithmic bytes, start, end)."""
+    """Times every launch of the conv / linear GEMM kernels (bench.py's
+    roofline): each op is armed with HIP timing events that its kernels
+    (the GEMM and, with split-K, its reduce) take through hipExtLaunchKernel,
+    so the events carry the dispatches' own begin/end stamps on the stream
+    they run on, with no host launch gap inside.  Records (kind, algorithmic
+    flops, algorithmic bytes, [(start, stop), ...]).  Not usable inside a
+    graph capture (bench.py times an eager pass of the same step)."""
 
     def __init__(self, detail=False):
         self.rec = []
         self.detail = detail
+        self._pool = []
+
+    def _event(self):
+        ev = ctypes.c_void_p()
+        ops.event_create(ctypes.byref(ev))
+        self._pool.append(ev)
+        return ev
 
     def __call__(self, kind, flops, nbytes, fn, key=None):
-        s = torch.cuda.current_stream()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        fn()
-        e1.record(s)
-        self.rec.append((kind if not self.detail else (kind, key), flops, nbytes, e0, e1))
+        ev = [self._event() for _ in range(4)]
+        ops.timing_arm(*ev)
+        try:
+            fn()
+        finally:
+            n = ctypes.c_int()
+            ops.timing_disarm(ctypes.byref(n))
+        self.rec.append((kind if not self.detail else (kind, key), flops, nbytes,
+                         [(ev[2 * i], ev[2 * i + 1]) for i in range(n.value)]))
 
     def summary(self):
+        """{kind: [launches, flops, bytes, seconds]} (seconds = summed kernel time)."""
         torch.cuda.synchronize()
         out = {}
-        for kind, fl, nb, e0, e1 in self.rec:
-            t = e0.elapsed_time(e1) * 1e-3
+        ms = ctypes.c_float()
+        for kind, fl, nb, pairs in self.rec:
+            t = 0.0
+            for e0, e1 in pairs:
+                ops.event_elapsed(e0, e1, ctypes.byref(ms))
+                t += ms.value * 1e-3
             o = out.setdefault(kind, [0, 0.0, 0.0, 0.0])
             o[0] += 1
             o[1] += fl
             o[2] += nb
             o[3] += t
         return out
+
+    def __del__(self):
+        for ev in getattr(self, '_pool', []):
+            try:
+                ops.event_destroy(ev)
+            except Exception:
+                pass
 
 
 TIMER = None
@@ -205,26 +255,29 @@ def conv_bwd_data_raw(dz, W, g, x_shape, cache=None):
     return dx
 
 
-def conv_bwd_weight_raw(x, dz, g, W_shape):
+def conv_bwd_weight_raw(x, dz, g, W_shape, out=None):
+    """dW (fresh tensor), or accumulated into `out` when given."""
     x = to_nhwc_bf16(x)
     d = _desc_io(g, x.shape, ld_of(x), ld_of(dz))
     ws = workspace(ops.conv_wgrad_workspace(d), x.device)
-    dW = torch.empty(W_shape, dtype=F32, device=x.device)
+    dW = torch.empty(W_shape, dtype=F32, device=x.device) if out is None else out
     N, C, H, Wd = x.shape
     flops = 2.0 * N * d.Ho * d.Wo * g.K * C * g.R * g.S
     nbytes = 2.0 * (N * H * Wd * C + N * d.Ho * d.Wo * g.K) + 4.0 * g.K * C * g.R * g.S
     _launch('conv_bwd_weight', flops, nbytes, lambda: ops.conv_bwd_weight(
-        d, x.data_ptr(), dz.data_ptr(), ws.data_ptr(), dW.data_ptr(), 0, stream()),
+        d, x.data_ptr(), dz.data_ptr(), ws.data_ptr(), dW.data_ptr(), int(out is not None), stream()),
         key=_shape_key(d) if TIMER is not None else None)
     return dW
 
 
-def chansum_raw(dz):
+def chansum_raw(dz, out=None):
     N, C, H, W = dz.shape
     P = N * H * W
     ws = workspace(ops.chansum_workspace(P, C), dz.device)
-    out = torch.empty(C, dtype=F32, device=dz.device)
-    ops.chansum(dz.data_ptr(), ld_of(dz), P, C, ws.data_ptr(), out.data_ptr(), 0, stream())
+    acc = out is not None
+    if out is None:
+        out = torch.empty(C, dtype=F32, device=dz.device)
+    ops.chansum(dz.data_ptr(), ld_of(dz), P, C, ws.data_ptr(), out.data_ptr(), int(acc), stream())
     return out
 
 
@@ -267,9 +320,17 @@ class Conv2dFn(torch.autograd.Function):
             else:
                 dx = ConvBwdDataFn.apply(dz, W, g, ctx.x_shape, ctx.cache)
         if _needed(ctx, 1):
-            dW = ConvBwdWeightFn.apply(x, dz, g) if not g.up2 else conv_bwd_weight_raw(x, dz, g, W.shape)
+            sink = _grad_sink(ctx, 1)
+            if sink is not None:
+                conv_bwd_weight_raw(x, dz, g, W.shape, out=sink)
+            else:
+                dW = ConvBwdWeightFn.apply(x, dz, g) if not g.up2 else conv_bwd_weight_raw(x, dz, g, W.shape)
         if ctx.needs_input_grad[2] and _needed(ctx, 2):
-            db = ChanSumFn.apply(dz)
+            sink = _grad_sink(ctx, 2)
+            if sink is not None:
+                chansum_raw(dz, out=sink)
+            else:
+                db = ChanSumFn.apply(dz)
         return dx, dW, db, None, None, None, None, None
 
 
@@ -591,6 +652,12 @@ class CatChannelsFn(torch.autograd.Function):
 
 
 # ================================================================ linear ===
+def _gemm(tag, A, sai, sak, B, sbk, sbj, C, ldc, M, N, K, bias, act, alpha, beta):
+    _launch('gemm_f32', 2.0 * M * N * K, 4.0 * (M * K + K * N + M * N), lambda: ops.gemm_f32(
+        A, sai, sak, B, sbk, sbj, C, ldc, M, N, K, bias, act, alpha, beta, stream()),
+        key='%s M%d N%d K%d' % (tag, M, N, K) if TIMER is not None else None)
+
+
 class LinearFn(torch.autograd.Function):
     """y = act(x W^T + b), fp32 (first order)."""
 
@@ -600,8 +667,7 @@ class LinearFn(torch.autograd.Function):
         M, K = x2.shape
         N = W.shape[0]
         y = torch.empty((M, N), dtype=F32, device=x.device)
-        ops.gemm_f32(x2.data_ptr(), K, 1, W.data_ptr(), 1, K, y.data_ptr(), N, M, N, K, ptr(b), act, 1.0, 0.0,
-                     stream())
+        _gemm('linear_fwd', x2.data_ptr(), K, 1, W.data_ptr(), 1, K, y.data_ptr(), N, M, N, K, ptr(b), act, 1.0, 0.0)
         ctx.act = act
         ctx.in_shape = tuple(x.shape)
         ctx.save_for_backward(x2, W, y if act else None)
@@ -620,14 +686,19 @@ class LinearFn(torch.autograd.Function):
         dx = dW = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty((M, K), dtype=F32, device=g.device)
-            ops.gemm_f32(g.data_ptr(), N, 1, W.data_ptr(), K, 1, dx.data_ptr(), K, M, K, N, 0, 0, 1.0, 0.0, stream())
+            _gemm('linear_dx', g.data_ptr(), N, 1, W.data_ptr(), K, 1, dx.data_ptr(), K, M, K, N, 0, 0, 1.0, 0.0)
             dx = dx.reshape(ctx.in_shape)
         if _needed(ctx, 1):
-            dW = torch.empty((N, K), dtype=F32, device=g.device)
-            ops.gemm_f32(g.data_ptr(), 1, N, x2.data_ptr(), K, 1, dW.data_ptr(), K, N, K, M, 0, 0, 1.0, 0.0, stream())
+            sink = _grad_sink(ctx, 1)
+            dst = sink if sink is not None else torch.empty((N, K), dtype=F32, device=g.device)
+            _gemm('linear_dw', g.data_ptr(), 1, N, x2.data_ptr(), K, 1, dst.data_ptr(), K, N, K, M, 0, 0, 1.0,
+                  1.0 if sink is not None else 0.0)
+            dW = dst if sink is None else None
         if ctx.needs_input_grad[2] and _needed(ctx, 2):
-            db = torch.empty(N, dtype=F32, device=g.device)
-            ops.colsum_f32(g.data_ptr(), N, M, N, db.data_ptr(), 0, stream())
+            sink = _grad_sink(ctx, 2)
+            dst = sink if sink is not None else torch.empty(N, dtype=F32, device=g.device)
+            ops.colsum_f32(g.data_ptr(), N, M, N, dst.data_ptr(), int(sink is not None), stream())
+            db = dst if sink is None else None
         return dx, dW, db, None
 
 

@@ -52,7 +52,8 @@ class FlatAdam(torch.optim.Optimizer):
                 p.grad = g
                 p._eegan_gen = self._gen
                 self._views.append((p, o, k, g))
-        self.step_count = 0
+        self.step_count = 0   # host mirror (state_dict); the kernels use step_dev
+        self.step_dev = torch.zeros(1, dtype=torch.float64, device=dev)
 
     def zero_grad(self, set_to_none=False):
         ops.fill_f32(self.gflat.data_ptr(), self.numel, 0.0, stream())
@@ -87,10 +88,7 @@ class FlatAdam(torch.optim.Optimizer):
         g = self.param_groups[0]
         b1, b2 = g['betas']
         self.step_count += 1
-        t = self.step_count
-        bc1 = 1 - b1 ** t
-        bc2 = 1 - b2 ** t
         ops.adam(self.flat.data_ptr(), self.gflat.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.numel, b1, b2,
-                 g['lr'] / bc1, bc2 ** 0.5, g['eps'], g['weight_decay'], stream())
+                 g['lr'], g['eps'], g['weight_decay'], self.step_dev.data_ptr(), stream())
         self._gen[0] += 1
         return loss

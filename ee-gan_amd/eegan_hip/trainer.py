@@ -224,3 +224,37 @@ class Trainer(object):
         g = self.g_update(fake_imgs, sent, words, attn_attr_emb, cls_ids, B, match_labels, batch['cap_lens'],
                           class_labels, iter_rec)
         return fake_imgs, g
+
+
+class StepGraph(object):
+    """The whole train_step captured once as a HIP graph (torch.cuda.CUDAGraph
+    is hipGraph on ROCm) and replayed: each iteration is one graph launch
+    instead of ~3000 kernel launches issued through Python autograd, which
+    otherwise bounds the step on the host.
+
+    Requirements the step already meets: no host reads of device values, a
+    batch held in fixed device storage (refill it in place between replays),
+    noise drawn inside the graph (graph-safe philox offsets), Adam bias
+    corrections from device step counters, and weight packs refreshed by
+    kernels that are part of the graph.  Learning rates are baked in.
+    """
+
+    def __init__(self, trainer, batch, warmup=2, timer=None, **step_kw):
+        from . import functional as Fn
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                trainer.train_step(batch, **step_kw)
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        prev, Fn.TIMER = Fn.TIMER, timer
+        try:
+            with torch.cuda.graph(self.graph):
+                self.out = trainer.train_step(batch, **step_kw)
+        finally:
+            Fn.TIMER = prev
+
+    def replay(self):
+        self.graph.replay()
+        return self.out

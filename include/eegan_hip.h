@@ -31,6 +31,18 @@ extern "C" {
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
 
+/* launch timing for the benchmark's roofline: timing events; a record on a
+ * capturing stream becomes an external event-record graph node */
+int eegan_event_create(hipEvent_t* ev);
+int eegan_event_destroy(hipEvent_t ev);
+int eegan_event_record(hipEvent_t ev, hipStream_t s);
+int eegan_event_elapsed(hipEvent_t start, hipEvent_t stop, float* ms);
+/* arm per-dispatch timing for the next op on this host thread: its first
+ * (up to two) kernels launch through hipExtLaunchKernel with (start_i, stop_i),
+ * stamped at the dispatch's begin and end; disarm returns how many were used */
+int eegan_timing_arm(hipEvent_t start0, hipEvent_t stop0, hipEvent_t start1, hipEvent_t stop1);
+int eegan_timing_disarm(int* kernels_timed);
+
 /* ------------------------------------------------------------------ conv --
  * replaces: every nn.Conv2d / nn.Linear forward+backward of models.py:14-403
  * (conv1x1/conv3x3/conv4x4 helpers 14-23, SAGB c1/c2/c_sc 97-103, Cum_Block
@@ -200,9 +212,11 @@ int eegan_lstm_bidir(const float* xproj, const float* whhT, const long* lens, in
                      float* words, float* sent, hipStream_t s);
 
 /* -------------------------------------------------------------------- adam --
- * replaces: torch.optim.Adam(betas=(0.0, 0.9)) of train.py:252-263 on one flat buffer */
-int eegan_adam(float* p, const float* g, float* m, float* v, long n, float beta1, float beta2, float step_size,
-               float bc2_sqrt, float eps, float weight_decay, hipStream_t s);
+ * replaces: torch.optim.Adam(betas=(0.0, 0.9)) of train.py:252-263 on one flat buffer.
+ * `step` is a device double: incremented on the stream, then read for the bias
+ * corrections (graph-replay safe). */
+int eegan_adam(float* p, const float* g, float* m, float* v, long n, float beta1, float beta2, float lr, float eps,
+               float weight_decay, double* step, hipStream_t s);
 
 #ifdef __cplusplus
 }

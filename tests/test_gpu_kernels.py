@@ -215,6 +215,27 @@ def test_elementwise_ops(gpu):
     rr.backward(g2)
     r.backward(_nhwc(g2, gpu))
     assert rel_l2(imd.grad.float().cpu(), imr.grad) < 1e-2
+    # gather-form adjoint over up/down ratios and both corner modes (fp32 path)
+    for (hi, ho) in [(4, 64), (8, 13), (37, 16), (5, 1), (16, 16)]:
+        m = torch.randn(2, 1, hi, hi)
+        md = m.to(gpu).requires_grad_()
+        s = Fn.MaskResizeSigmoidFn.apply(md, ho)
+        mr = m.clone().requires_grad_()
+        sr = torch.sigmoid(F.interpolate(mr, size=ho, mode='bilinear', align_corners=True))
+        gs = torch.randn(sr.shape)
+        sr.backward(gs)
+        s.backward(gs.to(gpu))
+        assert rel_l2(md.grad.cpu(), mr.grad) < 1e-5, (hi, ho)
+    for (hi, ho) in [(37, 16), (16, 16), (7, 19), (32, 299)]:
+        im = _bf(torch.rand(1, 3, hi, hi) * 2 - 1)
+        imd = _nhwc(im, gpu).requires_grad_()
+        r = Fn.BilinearFn.apply(imd, ho, ho)
+        imr = im.clone().requires_grad_()
+        rr = F.interpolate(imr, size=(ho, ho), mode='bilinear', align_corners=False)
+        g2 = _bf(torch.randn(rr.shape))
+        rr.backward(g2)
+        r.backward(_nhwc(g2, gpu))
+        assert rel_l2(imd.grad.float().cpu(), imr.grad) < 1e-2, (hi, ho)
     # max pool 3x3 s2 / avg pool 3x3 s1 p1 / global average pool
     z = _bf(torch.randn(2, 16, 11, 11))
     zd = _nhwc(z, gpu).requires_grad_()

@@ -414,3 +414,33 @@ def test_full_step(gpu):
     print('PARITY step/params worst rel_l2 %.3e; Adam-update sign agreement %.4f over %d entries' % (worst, frac, tot))
     _LOG.append(('step/update_sign_agreement', frac))
     assert frac > 0.8
+
+
+def test_step_graph_matches_eager(gpu):
+    """The captured step graph (bench.py's execution mode) replays the eager
+    step bit for bit.  Only the DAMSM region/word gradients accumulate with
+    fp32 atomics (order-dependent last bits, which Adam with beta1=0 turns
+    into lr-sized steps on near-zero gradients), so DAMSM is weighted 0 here:
+    every other kernel is deterministic and the runs must agree exactly."""
+    import bench
+    from eegan_hip.trainer import StepGraph
+    from eegan_hip.synthetic import make_batch
+    state = {}
+    for mode in ('eager', 'graph'):
+        T, B, ncls = bench.build('T8', gpu, sim_coe=0.0)
+        batch = make_batch(B, gpu, seed=11, class_num=ncls, with_class=True)
+        noise = seeded_tensor('graph:noise', (B, 100), 1).to(gpu)
+        if mode == 'eager':
+            for _ in range(3):
+                T.train_step(batch, noise=noise)
+        else:
+            sg = StepGraph(T, batch, warmup=1, noise=noise)
+            sg.replay()
+            sg.replay()
+        torch.cuda.synchronize()
+        state[mode] = torch.cat([o.flat for o in [T.optimizerG] + list(T.optimizerDs)] +
+                                [o.v for o in [T.optimizerG] + list(T.optimizerDs)])
+        del T
+    d = (state['graph'] - state['eager']).abs()
+    print('STEPGRAPH max |graph - eager| over params and Adam moments: %.3e' % float(d.max()))
+    assert torch.equal(state['graph'], state['eager'])

@@ -1,0 +1,20 @@
+#!/bin/bash
+# rocprofv3 evidence for bench.py (run on the GPU box from the repo root):
+# kernel-trace + stats pass, then one PMC pass per counter (never combined
+# with sys/runtime tracing).  Outputs under gpurun_out/prof_<tag>/.
+TAG=${1:-r01}
+STEPS=${2:-6}
+source "$(dirname "$0")/../run_gpu_steps.sh"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/prof_$TAG
+mkdir -p $O
+step 900 prof_trace rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
+  python3 bench.py --steps $STEPS --warmup 2 --no-cpu-baseline
+step 900 prof_fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- \
+  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline
+step 900 prof_write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- \
+  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline
+python3 tools/rocprof_families.py --trace $O/trace --fetch $O/fetch --write $O/write \
+  --steps $((STEPS + 2)) --out $O/families.json > /dev/null
+for d in trace fetch write; do find $O/$d -name '*.csv' -size +20M -delete; done
+ls -la $O
