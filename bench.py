@@ -71,6 +71,20 @@ def build(cfg_name, device, sim_coe=0.05):
     return T, B, ncls
 
 
+def pmc_traffic(kind):
+    """HBM bytes per launch of kernel family `kind` from the newest committed
+    rocprofv3 PMC summary (profiles/rNN_families.json, written by
+    tools/rocprof_families.py: FETCH_SIZE x2 (gfx950 wide-read correction) +
+    WRITE_SIZE, separate counter passes)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_families.json')))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        fam = json.load(f).get('families', {}).get(kind, {})
+    return fam.get('hbm_bytes_per_call'), 'profiles/' + os.path.basename(files[-1])
+
+
 def cpu_baseline(seconds_budget=20.0):
     """Time the CPU oracle's full step (oracle.eegan_oracle.train_step incl.
     the Inception-v3 encoder restatement) at B=4, W=32 (BASELINE.md CPU plan)."""
@@ -184,8 +198,12 @@ def main():
     dom = max(((k, v) for k, v in kern.items() if k.startswith('conv')), key=lambda kv: kv[1][3])
     kind, (n, fl, nb, tsec) = dom
     achieved = fl / tsec / 1e12
+    traffic, traffic_src = pmc_traffic(kind)
     roof = {'kernel': kind, 'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': MFMA_PEAK_TFLOPS,
-            'unit': 'TFLOP/s', 'frac': round(achieved / MFMA_PEAK_TFLOPS, 4), 'traffic': None,
+            'unit': 'TFLOP/s', 'frac': round(achieved / MFMA_PEAK_TFLOPS, 4), 'traffic': traffic,
+            'traffic_unit': 'HBM bytes per launch (rocprofv3 PMC)', 'traffic_source': traffic_src,
+            'algorithmic_bytes_per_launch': round(nb / n),
+            'algorithmic_flops_per_launch': round(fl / n),
             'launches_per_step': n // per, 'avg_launch_us': round(tsec / n * 1e6, 2),
             'timing': 'HIP start/stop events per dispatch (hipExtLaunchKernel) over %d eager step(s) of the same '
                       'workload right after the timed region' % per,

@@ -278,6 +278,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 }
 
 // split-K reduction + epilogue: out[p][co] = res + gamma*act(sum_z part[z][p][co] + bias)
+template <int MODE>  // MODE only tags the kernel name (profiles tell fwd / bwd-data apart)
 __global__ void conv_splitk_reduce_kernel(ConvArgs a) {
   const long total = (long)a.P * a.Mrows;
   const float gam = a.res ? *a.gamma : 1.f;
@@ -538,7 +539,7 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s) {
   int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd" : "conv_bwd_data");
   if (rc || p.nsplit == 1) return rc;
   const long total = (long)a.P * a.Mrows;
-  ee_launch(conv_splitk_reduce_kernel, dim3((int)std::min<long>((total + 255) / 256, 4096)), dim3(256), 0, s, a);
+  ee_launch(conv_splitk_reduce_kernel<MODE>, dim3((int)std::min<long>((total + 255) / 256, 4096)), dim3(256), 0, s, a);
   return ee_check_launch("conv_splitk_reduce");
 }
 

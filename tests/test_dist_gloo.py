@@ -1,0 +1,126 @@
+"""Data-parallel plumbing on CPU: world_size-2 process groups over gloo
+(127.0.0.1).  Covers what the N>1 bench path adds on top of the 1-GPU step:
+the differentiable all-gather behind global-batch DAMSM, gradient averaging
+(FlatAdam's bucketed all-reduce and GradReducer), and the cross-rank SyncBN
+statistics combine (fp64 sums all-reduced, then the reference's multi-device
+formula, sync_batchnorm/batchnorm.py:113-125) against the oracle."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from _util import REPO
+
+WORLD = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _run(fn, *args):
+    port = _free_port()
+    mp.spawn(_entry, args=(fn, port, args), nprocs=WORLD, join=True)
+
+
+def _entry(rank, fn, port, args):
+    sys.path.insert(0, os.path.join(REPO, 'ee-gan_amd'))
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
+    torch.set_num_threads(1)
+    dist.init_process_group('gloo', rank=rank, world_size=WORLD)
+    try:
+        fn(rank, *args)
+    finally:
+        dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------- cases ---
+def _case_all_gather(rank):
+    from eegan_hip import dist as D
+    torch.manual_seed(100 + rank)
+    x = torch.randn(3, 5, requires_grad=True)
+    g = D.all_gather(x)
+    parts = [torch.empty(3, 5) for _ in range(WORLD)]
+    dist.all_gather(parts, x.detach())
+    assert torch.equal(g.detach(), torch.cat(parts, 0))
+    # every rank's loss reads the whole gathered batch with its own weights;
+    # d(sum of all ranks' losses)/dx_r = sum over ranks of their weight slice r
+    w = torch.arange(WORLD * 15, dtype=torch.float32).reshape(WORLD * 3, 5) * (rank + 1)
+    (g * w).sum().backward()
+    wsum = torch.arange(WORLD * 15, dtype=torch.float32).reshape(WORLD * 3, 5) * sum(r + 1 for r in range(WORLD))
+    assert torch.allclose(x.grad, wsum[rank * 3:(rank + 1) * 3])
+    # non-differentiable path (lengths / class ids are int64 and must arrive bit-exact)
+    ids = torch.tensor([7 + rank, 200 - rank], dtype=torch.int64)
+    got = D.all_gather(ids, differentiable=False)
+    assert got.tolist() == [7, 200, 8, 199]
+
+
+def _case_flat_adam_allreduce(rank):
+    from eegan_hip.optim import FlatAdam
+    torch.manual_seed(7)
+    ps = [torch.nn.Parameter(torch.randn(s)) for s in [(5, 3), (7,), (1,), (4, 4, 2)]]
+    opt = FlatAdam(ps, lr=1e-3, betas=(0.0, 0.9), process_group=dist.group.WORLD, bucket_bytes=24)  # 6-float buckets
+    torch.manual_seed(1000 + rank)
+    local = [torch.randn(p.shape) for p in ps]
+    for p, g in zip(ps, local):
+        p.grad.copy_(g)
+    opt._allreduce()
+    allg = [torch.empty(opt.numel) for _ in range(WORLD)]
+    dist.all_gather(allg, torch.cat([torch.cat([g.reshape(-1), torch.zeros((-g.numel()) % 4)]) for g in local]))
+    mean = sum(allg) / WORLD
+    assert torch.allclose(opt.gflat, mean, atol=1e-6)
+    for p in ps:  # parameter .grad stays a view into the averaged flat buffer
+        assert p.grad.data_ptr() >= opt.gflat.data_ptr()
+
+
+def _case_grad_reducer(rank):
+    from eegan_hip.dist import GradReducer
+    m = torch.nn.Linear(4, 3)
+    for p in m.parameters():
+        p.grad = torch.full_like(p, float(rank + 1))
+    GradReducer(m).sync()
+    for p in m.parameters():
+        assert torch.allclose(p.grad, torch.full_like(p, (1 + WORLD) / 2.0))
+
+
+def _case_syncbn_stats(rank):
+    """Per-rank fp64 (sum, sumsq) -> all-reduce -> mean / clamp(var, eps)^-1/2
+    on the global count, as the SyncBN Functions combine them across ranks,
+    equals the oracle's multi-device BN on the concatenated batch."""
+    from eegan_hip import dist as D
+    from oracle import eegan_oracle as O
+    D.install_syncbn_hook()
+    from eegan_hip import functional as Fn
+    assert Fn.SYNC_BN_WORLD == WORLD and Fn.SYNC_BN_ALLREDUCE is not None
+    torch.manual_seed(55)
+    full = torch.randn(2 * WORLD, 6, 5, 5) * 3 + 1
+    full[:, 2] = 0.25  # constant channel: variance below eps exercises the clamp
+    x = full[rank * 2:(rank + 1) * 2]
+    sums = torch.cat([x.double().sum((0, 2, 3)), (x.double() ** 2).sum((0, 2, 3))])
+    Fn.SYNC_BN_ALLREDUCE(sums)
+    C = 6
+    count = full.shape[0] * 25
+    mean = sums[:C] / count
+    var = (sums[C:] - sums[:C] * mean).clamp_min(0) / count
+    istd = var.clamp_min(1e-5).rsqrt()
+    y = (x.double() - mean.view(1, C, 1, 1)) * istd.view(1, C, 1, 1)
+    sd = {'bn.weight': torch.ones(C), 'bn.bias': torch.zeros(C), 'bn.running_mean': torch.zeros(C),
+          'bn.running_var': torch.ones(C)}
+    ref = O.sync_bn(full, sd, 'bn.', affine=True, training=True, mode='multi')
+    assert np.allclose(y.numpy(), ref[rank * 2:(rank + 1) * 2].detach().double().numpy(), atol=1e-5)
+    # running statistics: unbiased variance of the global batch, momentum 0.1
+    rv = 0.9 + 0.1 * var * count / (count - 1)
+    assert torch.allclose(rv.float(), sd['bn.running_var'], atol=1e-5)
+
+
+@pytest.mark.parametrize('case', ['all_gather', 'flat_adam_allreduce', 'grad_reducer', 'syncbn_stats'])
+def test_gloo_world2(case):
+    _run(globals()['_case_' + case])

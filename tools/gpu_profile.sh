@@ -11,10 +11,10 @@ mkdir -p $O
 step 900 prof_trace rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
   python3 bench.py --steps $STEPS --warmup 2 --no-cpu-baseline
 step 900 prof_fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- \
-  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline
+  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --graph off --no-timer
 step 900 prof_write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- \
-  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline
+  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --graph off --no-timer
 python3 tools/rocprof_families.py --trace $O/trace --fetch $O/fetch --write $O/write \
-  --steps $((STEPS + 2)) --out $O/families.json > /dev/null
+  --steps $((STEPS + 4)) --out $O/families.json > /dev/null
 for d in trace fetch write; do find $O/$d -name '*.csv' -size +20M -delete; done
 ls -la $O

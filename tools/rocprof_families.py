@@ -25,11 +25,11 @@ from collections import defaultdict
 # (family, is_primary): the primary kernel counts calls; secondaries add time
 _FAMILIES = [
     (re.compile(r'conv_igemm_kernel<0,'), 'conv_fwd', True),
-    (re.compile(r'conv_splitk_reduce_kernel.*ConvArgs'), 'conv_fwd', False),
+    (re.compile(r'conv_splitk_reduce_kernel<0>'), 'conv_fwd', False),
     (re.compile(r'conv_igemm_kernel<1,'), 'conv_bwd_data', True),
     (re.compile(r'conv_splitk_reduce_kernel<1>'), 'conv_bwd_data', False),
     (re.compile(r'conv_wgrad_kernel<'), 'conv_bwd_weight', True),
-    (re.compile(r'wgrad_reduce_kernel'), 'conv_bwd_weight', False),
+    (re.compile(r'colsum_rows_kernel<.*WgradMap'), 'conv_bwd_weight', False),
 ]
 
 
