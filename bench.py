@@ -141,6 +141,8 @@ def main():
     from eegan_hip import functional as Fn
     from eegan_hip.synthetic import make_batch
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if os.environ.get('EEGAN_SHARE_GPU') == '1':   # rehearsal only: several ranks on one GPU (gloo)
+        local_rank %= torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
     device = torch.device('cuda', local_rank)
     rank, world = D.init_from_env()

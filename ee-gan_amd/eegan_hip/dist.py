@@ -39,7 +39,7 @@ def init_from_env(backend=None):
         install_syncbn_hook()
         return rank(), world_size()
     if backend is None:
-        backend = 'nccl' if torch.cuda.is_available() else 'gloo'
+        backend = os.environ.get('EEGAN_DIST_BACKEND') or ('nccl' if torch.cuda.is_available() else 'gloo')
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
     dist.init_process_group(backend=backend)
     install_syncbn_hook()
