@@ -65,6 +65,67 @@ struct ConvArgs {
   int ncls, nsplit;             // parity classes (BWDD stride>1), K splits
 };
 
+// Epilogue shared by the GEMM kernels: fragment (i, j) of wave (wi, wj) holds 4
+// consecutive output channels of one pixel -> bias, activation, residual,
+// 8-byte NHWC store (or the fp32 split-K slab).
+template <int MODE, int FI, int FJ, int WT_CO, int WT_PIX>
+EE_DEV void igemm_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], int pix0, int co0, int wi, int wj,
+                           int lane, int split, int Pc, int CH, int CW, int qy, int qx, int stc) {
+  const int fr = lane & 15;
+  const float gam = a.res ? *a.gamma : 1.f;
+#pragma unroll
+  for (int j = 0; j < FJ; ++j) {
+    const int pc = pix0 + wj * WT_PIX + j * 16 + fr;
+    if (pc >= Pc) continue;
+    long p = pc;
+    if (MODE == MODE_BWDD && a.ncls > 1) {
+      const int hw = CH * CW;
+      const int n = pc / hw, rem = pc - n * hw;
+      const int yy = rem / CW, xx = rem - yy * CW;
+      p = ((long)n * a.OH + qy + stc * yy) * a.OW + qx + stc * xx;
+    }
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const int co = co0 + wi * WT_CO + i * 16 + (lane >> 4) * 4;
+      if (co >= a.Mrows) continue;
+      if (a.nsplit > 1) {
+        float* dst = a.part + ((long)split * a.P + p) * a.Mrows + co;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (co + r < a.Mrows) dst[r] = acc[i][j][r];
+        continue;
+      }
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float bv = (a.bias && co + r < a.Mrows) ? a.bias[co + r] : 0.f;
+        v[r] = act_fwd(acc[i][j][r] + bv, a.act, a.slope);
+      }
+      if (a.res) {
+        const bf16_t* rp = a.res + p * a.ldres + co;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (co + r < a.Mrows) v[r] = bf2f(rp[r]) + gam * v[r];
+      }
+      if (a.out_f32) {
+        float* op = reinterpret_cast<float*>(a.out) + p * a.ldo + co;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (co + r < a.Mrows) op[r] = v[r];
+      } else {
+        bf16_t* op = reinterpret_cast<bf16_t*>(a.out) + p * a.ldo + co;
+        if (co + 4 <= a.Mrows) {
+          *reinterpret_cast<uint2*>(op) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (co + r < a.Mrows) op[r] = f2bf(v[r]);
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------- FWD / BWDD kernel --
 template <int MODE, int TCO, int TPIX, int WCO>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
@@ -222,59 +283,171 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     }
   }
 
-  // ------------------------------------------------------------ epilogue --
-  const float gam = a.res ? *a.gamma : 1.f;
-#pragma unroll
-  for (int j = 0; j < FJ; ++j) {
-    const int pc = pix0 + wj * WT_PIX + j * 16 + fr;
-    if (pc >= Pc) continue;
-    long p = pc;
-    if (MODE == MODE_BWDD && a.ncls > 1) {
-      const int hw = CH * CW;
-      const int n = pc / hw, rem = pc - n * hw;
-      const int yy = rem / CW, xx = rem - yy * CW;
-      p = ((long)n * a.OH + qy + stc * yy) * a.OW + qx + stc * xx;
+  igemm_epilogue<MODE, FI, FJ, WT_CO, WT_PIX>(a, acc, pix0, co0, wi, wj, lane, split, Pc, CH, CW, qy, qx, stc);
+}
+
+// ------------------------------------- FWD / BWDD, pipelined LDS-DMA kernel --
+// Same GEMM as conv_igemm_kernel, but both operand tiles go global -> LDS by
+// buffer_load ... lds (16 B per lane, no VGPR staging) into a STAGES-deep ring:
+// STAGES-1 K-steps are in flight while one is multiplied, one raw s_barrier per
+// K-step, counted vmcnt waits (never 0 inside the steady state).  The LDS image
+// is lane-linear (64-B rows of 32 bf16), so the bank-conflict swizzle is
+// applied to the SOURCE chunk: LDS slot q of row r holds K-chunk q ^ ((r>>2)&3).
+// Out-of-range taps / channels use an out-of-bounds buffer offset, which the
+// hardware bounds check turns into zeros.  Requires C % 8 == 0 (whole 16-B
+// chunks valid or invalid) and TCO >= 64.
+constexpr unsigned OOB = 0x80000000u;
+constexpr int CONV_STAGES = 4;
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+EE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* p, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)min(bytes, 0x7fffffffL), 0x00020000);
+}
+
+template <int N>
+EE_DEV void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int MODE, int TCO, int TPIX>
+__global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a, long src_bytes, long w_bytes) {
+  constexpr int S = CONV_STAGES;
+  constexpr int WT_CO = TCO / 2, WT_PIX = TPIX / 2;
+  constexpr int FI = WT_CO / 16, FJ = WT_PIX / 16;
+  constexpr int A_INS = TCO / 64, B_INS = TPIX / 64;  // 16-B chunks per thread per K-step
+  constexpr int NLOAD = A_INS + B_INS;
+  constexpr int STAGE = (TCO + TPIX) * BK;           // bf16 elements per stage
+  static_assert(A_INS >= 1 && B_INS >= 1, "tile");
+
+  __shared__ __attribute__((aligned(16))) bf16_t lds[S * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wi = wave >> 1, wj = wave & 1;
+  const int cls = blockIdx.z % a.ncls, split = blockIdx.z / a.ncls;
+  const int co0 = blockIdx.y * TCO;
+
+  int qy = 0, qx = 0, CH = a.OH, CW = a.OW, stc = 1;
+  int r0 = 0, s0 = 0, TR = a.R, TS = a.S, dqy = 0, dqx = 0;
+  if (MODE == MODE_BWDD) {
+    if (a.ncls > 1) {
+      qy = cls / a.st;
+      qx = cls - qy * a.st;
+      CH = (a.OH - qy + a.st - 1) / a.st;
+      CW = (a.OW - qx + a.st - 1) / a.st;
+      stc = a.st;
     }
+    r0 = (qy + a.ph) % a.st;
+    s0 = (qx + a.pw) % a.st;
+    TR = r0 < a.R ? (a.R - r0 + a.st - 1) / a.st : 0;
+    TS = s0 < a.S ? (a.S - s0 + a.st - 1) / a.st : 0;
+    dqy = (qy + a.ph - r0) / a.st;
+    dqx = (qx + a.pw - s0) / a.st;
+  }
+  const int Pc = a.N * CH * CW;
+  const int pix0 = blockIdx.x * TPIX;
+  if (pix0 >= Pc) return;  // block-uniform
+  const int nc = a.Cgp / BK;
+  const int nk_all = TR * TS * nc;
+  const int kchunk = (nk_all + a.nsplit - 1) / a.nsplit;
+  const int kt0 = min(nk_all, split * kchunk), kt1 = min(nk_all, kt0 + kchunk);
+  const int nk = kt1 - kt0;
+
+  // this thread's 16-B chunk of every staged row: rows i*64 + tid/4, K-chunk swizzled
+  const int rsub = tid >> 2;
+  const int kc = (tid & 3) ^ ((tid >> 4) & 3);
+  int b_n[B_INS], b_y[B_INS], b_x[B_INS];
+  bool b_ok[B_INS];
 #pragma unroll
-    for (int i = 0; i < FI; ++i) {
-      const int co = co0 + wi * WT_CO + i * 16 + (lane >> 4) * 4;
-      if (co >= a.Mrows) continue;
-      if (a.nsplit > 1) {
-        float* dst = a.part + ((long)split * a.P + p) * a.Mrows + co;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (co + r < a.Mrows) dst[r] = acc[i][j][r];
-        continue;
-      }
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float bv = (a.bias && co + r < a.Mrows) ? a.bias[co + r] : 0.f;
-        v[r] = act_fwd(acc[i][j][r] + bv, a.act, a.slope);
-      }
-      if (a.res) {
-        const bf16_t* rp = a.res + p * a.ldres + co;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (co + r < a.Mrows) v[r] = bf2f(rp[r]) + gam * v[r];
-      }
-      if (a.out_f32) {
-        float* op = reinterpret_cast<float*>(a.out) + p * a.ldo + co;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (co + r < a.Mrows) op[r] = v[r];
-      } else {
-        bf16_t* op = reinterpret_cast<bf16_t*>(a.out) + p * a.ldo + co;
-        if (co + 4 <= a.Mrows) {
-          *reinterpret_cast<uint2*>(op) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (co + r < a.Mrows) op[r] = f2bf(v[r]);
-        }
-      }
+  for (int i = 0; i < B_INS; ++i) {
+    const int p = pix0 + i * 64 + rsub;
+    b_ok[i] = p < Pc;
+    const int pp = b_ok[i] ? p : 0;
+    const int hw = CH * CW;
+    const int n = pp / hw;
+    const int rem = pp - n * hw;
+    const int yy = rem / CW;
+    const int xx = rem - yy * CW;
+    b_n[i] = n;
+    if (MODE == MODE_FWD) {
+      b_y[i] = yy * a.st - a.ph;
+      b_x[i] = xx * a.st - a.pw;
+    } else {
+      b_y[i] = yy + dqy;
+      b_x[i] = xx + dqx;
     }
   }
+  const int PH = a.IH >> a.up2, PW = a.IW >> a.up2;
+  const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, src_bytes);
+  const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(a.wp, w_bytes);
+
+  auto issue = [&](int kt, int buf) {
+    const int tap = kt / nc;
+    const int cc = kt - tap * nc;
+    const int ta = tap / TS, tb = tap - ta * TS;
+    const int r = (MODE == MODE_FWD) ? ta : r0 + a.st * ta;
+    const int s = (MODE == MODE_FWD) ? tb : s0 + a.st * tb;
+    const int kbase = (r * a.S + s) * a.Cgp + cc * BK + kc * 8;
+    bf16_t* base = lds + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < A_INS; ++i) {
+      const unsigned off = (unsigned)(((co0 + i * 64 + rsub) * a.Kw + kbase) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_void_t*)(base + (i * 256 + wave * 64) * 8), 16, off, 0, 0, 0);
+    }
+    const int c = cc * BK + kc * 8;
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i) {
+      unsigned off = OOB;
+      if (b_ok[i] && c < a.Cvalid) {
+        if (MODE == MODE_FWD) {
+          const int iy = b_y[i] + r, ix = b_x[i] + s;
+          if ((unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW)
+            off = (unsigned)((((b_n[i] * PH + (iy >> a.up2)) * PW + (ix >> a.up2)) * a.lds_src + c) * 2);
+        } else {
+          const int oy = b_y[i] - ta, ox = b_x[i] - tb;
+          if ((unsigned)oy < (unsigned)a.IH && (unsigned)ox < (unsigned)a.IW)
+            off = (unsigned)((((b_n[i] * a.IH + oy) * a.IW + ox) * a.lds_src + c) * 2);
+        }
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_src, (lds_void_t*)(base + TCO * BK + (i * 256 + wave * 64) * 8), 16,
+                                               off, 0, 0, 0);
+    }
+  };
+
+  f32x4_t acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int st = 0; st < S - 1; ++st)
+    if (st < nk) issue(kt0 + st, st);
+  for (int it = 0; it < nk; ++it) {
+    if (it + S - 2 < nk) wait_vmcnt<(S - 2) * NLOAD>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (it + S - 1 < nk) issue(kt0 + it + S - 1, (it + S - 1) % S);
+    const bf16_t* base = lds + (it % S) * STAGE;
+    bf16x8_t fa[FI], fb[FJ];
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const int row = wi * WT_CO + i * 16 + fr;
+      fa[i] = as_frag(*reinterpret_cast<const uint4*>(base + row * BK + ((fq ^ ((row >> 2) & 3)) * 8)));
+    }
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const int row = wj * WT_PIX + j * 16 + fr;
+      fb[j] = as_frag(*reinterpret_cast<const uint4*>(base + TCO * BK + row * BK + ((fq ^ ((row >> 2) & 3)) * 8)));
+    }
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+  }
+  igemm_epilogue<MODE, FI, FJ, WT_CO, WT_PIX>(a, acc, pix0, co0, wi, wj, lane, split, Pc, CH, CW, qy, qx, stc);
 }
 
 // split-K reduction + epilogue: out[p][co] = res + gamma*act(sum_z part[z][p][co] + bias)
@@ -521,7 +694,7 @@ Plan plan_igemm(const ConvArgs& a, int Pc_max) {
 }
 
 template <int MODE>
-int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s) {
+int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src_bytes) {
   Plan p = plan_igemm(a, Pc_max);
   a.nsplit = p.nsplit;
   a.part = p.nsplit > 1 ? part_ws : nullptr;
@@ -530,12 +703,20 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s) {
     return -22;
   }
   dim3 grid(ee_cdiv(Pc_max, p.tpix), ee_cdiv(a.Mrows, p.tco), a.ncls * p.nsplit);
+  const long w_bytes = (long)ee_round_up(a.Mrows, 128) * a.Kw * 2;
+#define GL(TC, TP) ee_launch(conv_glds_kernel<MODE, TC, TP>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
 #define IG(TC, TP, WC) ee_launch(conv_igemm_kernel<MODE, TC, TP, WC>, grid, dim3(256), 0, s, a)
-  if (p.tco == 128) { if (p.tpix == 128) IG(128, 128, 2); else IG(128, 64, 2); }
+  const bool glds = (a.Cvalid % 8) == 0 && p.tco >= 64 && src_bytes < 0x7fffffffL && w_bytes < 0x7fffffffL;
+  if (glds) {
+    if (p.tco == 128) { if (p.tpix == 128) GL(128, 128); else GL(128, 64); }
+    else { if (p.tpix == 128) GL(64, 128); else GL(64, 64); }
+  }
+  else if (p.tco == 128) { if (p.tpix == 128) IG(128, 128, 2); else IG(128, 64, 2); }
   else if (p.tco == 64) { if (p.tpix == 128) IG(64, 128, 2); else IG(64, 64, 2); }
   else if (p.tco == 32) { if (p.tpix == 256) IG(32, 256, 1); else IG(32, 64, 1); }
   else { if (p.tpix == 256) IG(16, 256, 1); else IG(16, 64, 1); }
 #undef IG
+#undef GL
   int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd" : "conv_bwd_data");
   if (rc || p.nsplit == 1) return rc;
   const long total = (long)a.P * a.Mrows;
@@ -659,7 +840,7 @@ int eegan_conv_fwd(const eegan_conv_desc* d, const bf16_t* x, const bf16_t* wpac
     ee_set_error("conv_fwd: input channel stride %d must be a multiple of 8 (16-B aligned rows)", d->ldx);
     return -22;
   }
-  return launch_igemm<MODE_FWD>(a, a.P, ws, stream);
+  return launch_igemm<MODE_FWD>(a, a.P, ws, stream, (long)d->N * (d->H >> d->up2) * (d->W >> d->up2) * d->ldx * 2);
 }
 
 int eegan_conv_bwd_data(const eegan_conv_desc* d, const bf16_t* dy, const bf16_t* wpackT, void* dx, int lddx,
@@ -681,7 +862,7 @@ int eegan_conv_bwd_data(const eegan_conv_desc* d, const bf16_t* dy, const bf16_t
     ee_set_error("conv_bwd_data: dy channel stride %d must be a multiple of 8", d->ldy);
     return -22;
   }
-  return launch_igemm<MODE_BWDD>(a, bwdd_pc_max(d), ws, stream);
+  return launch_igemm<MODE_BWDD>(a, bwdd_pc_max(d), ws, stream, (long)d->N * d->Ho * d->Wo * d->ldy * 2);
 }
 
 static void wgrad_plan(const eegan_conv_desc* d, int& TCO, int& TK, int& nsplit, int& pps, int& K) {
