@@ -493,6 +493,54 @@ struct WgradMap {
 
 constexpr int TRP = 4;  // row padding (elements) for transposed-read tiles
 
+// dW tile epilogue: lane (g, li) of fragment (i, j) holds dW[co0 + ... + 4g + r][kb0 + ... + li];
+// written straight into torch's layout when unsplit, else into the split slab
+template <int FI, int FJ, int WT_CO, int WT_K>
+EE_DEV void wgrad_epilogue(const WgradArgs& w, const f32x4_t (&acc)[FI][FJ], int co0, int kb0, int wi, int wj,
+                           int lane) {
+  const int g = lane >> 4, li = lane & 15;
+  if (w.dw) {
+    // one fragment row block at a time: all 4*FJ old values are loaded before any
+    // is added, so accumulation costs one memory round trip per block, not per element
+    const WgradMap map{w.K, w.Cg, w.Cin, w.R * w.S};
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      long o[4][FJ];
+      float old[4][FJ];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wi * WT_CO + i * 16 + g * 4 + r;
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+          const int k = kb0 + wj * WT_K + j * 16 + li;
+          o[r][j] = (co < w.Cout && k < w.K) ? map((long)co * w.K + k) : -1;
+          old[r][j] = (w.accumulate && o[r][j] >= 0) ? w.dw[o[r][j]] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+          if (o[r][j] >= 0) w.dw[o[r][j]] = old[r][j] + acc[i][j][r];
+    }
+    return;
+  }
+  float* ws = w.ws + (long)blockIdx.z * w.Cout * w.K;
+#pragma unroll
+  for (int i = 0; i < FI; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + wi * WT_CO + i * 16 + g * 4 + r;
+      if (co >= w.Cout) continue;
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) {
+        const int k = kb0 + wj * WT_K + j * 16 + li;
+        if (k < w.K) ws[(long)co * w.K + k] = acc[i][j][r];
+      }
+    }
+  }
+}
+
 template <int TCO, int TK, int WCO>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs w) {
   constexpr int WKK = 4 / WCO;
@@ -615,38 +663,163 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs w) {
       buf ^= 1;
     }
   }
-  if (w.dw) {
-    const WgradMap map{w.K, w.Cg, w.Cin, w.R * w.S};
+  wgrad_epilogue<FI, FJ, WT_CO, WT_K>(w, acc, co0, kb0, wi, wj, lane);
+}
+
+// XOR swizzle of the 16-B chunk index for [32 pixel][NCH chunk] LDS images
+// read with ds_read_b64_tr_b16 (two 4-row blocks 8 rows apart per 32-lane
+// half): conflict-free for NCH = 4, 8, 16 (exhaustive bank check).
+template <int NCH>
+EE_DEV int tr_swz(int row) {
+  if (NCH == 16) return ((row & 3) << 1) ^ (((row >> 3) & 1) << 3);
+  if (NCH == 8) return (row & 3) ^ (((row >> 3) & 1) << 2);
+  return (row & 3) ^ (((row >> 3) & 1) << 1);
+}
+
+// Pipelined weight gradient: dy [32 pixel][TCO] and the gathered x [32 pixel][TK]
+// K-steps go global -> LDS by buffer_load ... lds into a 4-deep ring (as
+// conv_glds_kernel), fragments by transposed reads of the swizzled images.
+// Padding channels of dy / x only reach dW rows / columns that are dropped;
+// halo taps and pixels past the split read as zeros (bounds-checked offsets).
+template <int TCO, int TK>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_glds_kernel(WgradArgs w, long x_bytes, long dy_bytes) {
+  constexpr int S = CONV_STAGES;
+  constexpr int WCO = TCO >= 64 ? 2 : 1, WKK = 4 / WCO;
+  constexpr int WT_CO = TCO / WCO, WT_K = TK / WKK;
+  constexpr int FI = WT_CO / 16, FJ = WT_K / 16;
+  constexpr int DCH = TCO / 8, XCH = TK / 8;           // 16-B chunks per pixel row
+  constexpr int D_TOT = BK * DCH, X_TOT = BK * XCH;    // chunks per K-step
+  constexpr int D_INS = (D_TOT + 255) / 256, X_INS = X_TOT / 256;
+  constexpr int STAGE = BK * (TCO + TK);
+  static_assert(X_INS >= 1 && FI >= 1 && FJ >= 1, "tile");
+
+  __shared__ __attribute__((aligned(16))) bf16_t lds[S * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wi = wave / WKK, wj = wave % WKK;
+  const int co0 = blockIdx.y * TCO, kb0 = blockIdx.x * TK;
+  const int p_begin = blockIdx.z * w.p_per_split;
+  const int p_end = min(w.P, p_begin + w.p_per_split);
+  const int nk = p_begin < p_end ? (p_end - p_begin + BK - 1) / BK : 0;
+  const int PH = w.IH >> w.up2, PW = w.IW >> w.up2;
+  const int hw = w.OH * w.OW;
+  // waves that stage no dy chunk (TCO = 32) count fewer loads per K-step
+  const bool d_wave = D_TOT >= 256 || tid < D_TOT;
+  const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(w.x, x_bytes);
+  const __amdgpu_buffer_rsrc_t rs_d = make_rsrc(w.dy, dy_bytes);
+
+  // dy chunks: fixed pixel row / channel per thread
+  int d_row[D_INS], d_co[D_INS];
+#pragma unroll
+  for (int i = 0; i < D_INS; ++i) {
+    const int idx = i * 256 + tid;
+    d_row[i] = idx / DCH;
+    d_co[i] = co0 + (((idx % DCH) ^ tr_swz<DCH>(d_row[i])) * 8);
+  }
+  // x chunks: fixed (tap, channel) and pixel row per thread; pixel tracked incrementally
+  int x_row[X_INS], x_r[X_INS], x_s[X_INS], x_c[X_INS], x_n[X_INS], x_oy[X_INS], x_ox[X_INS];
+  bool x_kok[X_INS];
+#pragma unroll
+  for (int i = 0; i < X_INS; ++i) {
+    const int idx = i * 256 + tid;
+    x_row[i] = idx / XCH;
+    const int k = kb0 + (((idx % XCH) ^ tr_swz<XCH>(x_row[i])) * 8);
+    x_kok[i] = k < w.K;
+    const int tap = k / w.Cg;
+    x_c[i] = k - tap * w.Cg;
+    x_r[i] = tap / w.S;
+    x_s[i] = tap - x_r[i] * w.S;
+    const int p = p_begin + x_row[i];
+    x_n[i] = p / hw;
+    const int rem = p - x_n[i] * hw;
+    x_oy[i] = rem / w.OW;
+    x_ox[i] = rem - x_oy[i] * w.OW;
+  }
+
+  auto issue = [&](int step, int buf) {
+    const int pb = p_begin + step * BK;
+    bf16_t* base = lds + buf * STAGE;
+    if (d_wave) {
+#pragma unroll
+      for (int i = 0; i < D_INS; ++i) {
+        const int p = pb + d_row[i];
+        const unsigned off = (p < p_end && d_co[i] < w.Cout) ? (unsigned)(((long)p * w.lddy + d_co[i]) * 2) : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_d, (lds_void_t*)(base + (i * 256 + wave * 64) * 8), 16, off, 0,
+                                                 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < X_INS; ++i) {
+      unsigned off = OOB;
+      if (pb + x_row[i] < p_end && x_kok[i]) {
+        const int iy = x_oy[i] * w.st - w.ph + x_r[i], ix = x_ox[i] * w.st - w.pw + x_s[i];
+        if ((unsigned)iy < (unsigned)w.IH && (unsigned)ix < (unsigned)w.IW)
+          off = (unsigned)(((((long)x_n[i] * PH + (iy >> w.up2)) * PW + (ix >> w.up2)) * w.ldx + x_c[i]) * 2);
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_x, (lds_void_t*)(base + BK * TCO + (i * 256 + wave * 64) * 8), 16,
+                                               off, 0, 0, 0);
+      // advance this row's pixel by one K-step
+      x_ox[i] += BK;
+      while (x_ox[i] >= w.OW) {
+        x_ox[i] -= w.OW;
+        if (++x_oy[i] == w.OH) {
+          x_oy[i] = 0;
+          ++x_n[i];
+        }
+      }
+    }
+  };
+
+  f32x4_t acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pq = li & 3;
+  typedef __attribute__((address_space(3))) s16x4_t lds_s4;
+  // transposed fragment: rows (pixels) 8g+q and 8g+q+4, columns col + 4*pq .. +3
+  auto tr_frag = [&](const bf16_t* img, int nch_shift, int col, auto swz) -> bf16x8_t {
+    const int ch = (col >> 3) + (pq >> 1);
+    const int r0 = 8 * g + q, r1 = r0 + 4;
+    const bf16_t* p0 = img + (r0 << nch_shift) * 8 + ((ch ^ swz(r0)) * 8) + 4 * (pq & 1);
+    const bf16_t* p1 = img + (r1 << nch_shift) * 8 + ((ch ^ swz(r1)) * 8) + 4 * (pq & 1);
+    s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(p0));
+    s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(p1));
+    typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+    s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  };
+  constexpr int DSH = DCH == 16 ? 4 : DCH == 8 ? 3 : 2;
+  constexpr int XSH = XCH == 16 ? 4 : 3;
+  auto dswz = [](int r) { return tr_swz<DCH>(r); };
+  auto xswz = [](int r) { return tr_swz<XCH>(r); };
+
+#pragma unroll
+  for (int st = 0; st < S - 1; ++st)
+    if (st < nk) issue(st, st);
+  for (int it = 0; it < nk; ++it) {
+    if (it + S - 2 < nk) {
+      if (d_wave) wait_vmcnt<(S - 2) * (D_INS + X_INS)>();
+      else wait_vmcnt<(S - 2) * X_INS>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (it + S - 1 < nk) issue(it + S - 1, (it + S - 1) % S);
+    const bf16_t* base = lds + (it % S) * STAGE;
+    bf16x8_t fa[FI], fb[FJ];
+#pragma unroll
+    for (int i = 0; i < FI; ++i) fa[i] = tr_frag(base, DSH, wi * WT_CO + i * 16, dswz);
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) fb[j] = tr_frag(base + BK * TCO, XSH, wj * WT_K + j * 16, xswz);
 #pragma unroll
     for (int i = 0; i < FI; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wi * WT_CO + i * 16 + g * 4 + r;
-        if (co >= w.Cout) continue;
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) {
-          const int k = kb0 + wj * WT_K + j * 16 + li;
-          if (k >= w.K) continue;
-          const long o = map((long)co * w.K + k);
-          if (o >= 0) w.dw[o] = w.accumulate ? w.dw[o] + acc[i][j][r] : acc[i][j][r];
-        }
-      }
-    return;
+      for (int j = 0; j < FJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
   }
-  float* ws = w.ws + (long)blockIdx.z * w.Cout * w.K;
-#pragma unroll
-  for (int i = 0; i < FI; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = co0 + wi * WT_CO + i * 16 + g * 4 + r;
-      if (co >= w.Cout) continue;
-#pragma unroll
-      for (int j = 0; j < FJ; ++j) {
-        const int k = kb0 + wj * WT_K + j * 16 + li;
-        if (k < w.K) ws[(long)co * w.K + k] = acc[i][j][r];
-      }
-    }
-  }
+  wgrad_epilogue<FI, FJ, WT_CO, WT_K>(w, acc, co0, kb0, wi, wj, lane);
 }
 
 // ------------------------------------------------------- weight packing --
@@ -865,10 +1038,19 @@ int eegan_conv_bwd_data(const eegan_conv_desc* d, const bf16_t* dy, const bf16_t
   return launch_igemm<MODE_BWDD>(a, bwdd_pc_max(d), ws, stream, (long)d->N * d->Ho * d->Wo * d->ldy * 2);
 }
 
+static long wgrad_x_bytes(const eegan_conv_desc* d) {
+  return (long)d->N * (d->H >> d->up2) * (d->W >> d->up2) * d->ldx * 2;
+}
+static long wgrad_dy_bytes(const eegan_conv_desc* d) { return (long)d->N * d->Ho * d->Wo * d->ldy * 2; }
+// the pipelined kernel addresses its operands with 32-bit buffer offsets
+static bool wgrad_glds_ok(const eegan_conv_desc* d) {
+  return d->K > 16 && wgrad_x_bytes(d) < 0x7fffffffL && wgrad_dy_bytes(d) < 0x7fffffffL;
+}
+
 static void wgrad_plan(const eegan_conv_desc* d, int& TCO, int& TK, int& nsplit, int& pps, int& K) {
   const int Cg = ee_round_up(d->C, 8);
   K = d->R * d->S * Cg;
-  TCO = d->K > 64 ? 128 : (d->K > 16 ? 64 : 16);
+  TCO = d->K > 64 ? 128 : d->K > 32 ? 64 : (d->K > 16 && wgrad_glds_ok(d)) ? 32 : d->K > 16 ? 64 : 16;
   TK = K > 64 ? 128 : 64;
   const int P = d->N * d->Ho * d->Wo;
   const int tiles = ee_cdiv(d->K, TCO) * ee_cdiv(K, TK);
@@ -924,11 +1106,19 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
   }
   if (w.P > 0) {
     dim3 grid(ee_cdiv(K, TK), ee_cdiv(d->K, TCO), nsplit);
+    const long x_bytes = wgrad_x_bytes(d), dy_bytes = wgrad_dy_bytes(d);
 #define WG(TC, TKK, WC) ee_launch(conv_wgrad_kernel<TC, TKK, WC>, grid, dim3(256), 0, stream, w)
-    if (TCO == 128) { if (TK == 128) WG(128, 128, 2); else WG(128, 64, 2); }
+#define WL(TC, TKK) ee_launch(conv_wgrad_glds_kernel<TC, TKK>, grid, dim3(256), 0, stream, w, x_bytes, dy_bytes)
+    if (wgrad_glds_ok(d)) {
+      if (TCO == 128) { if (TK == 128) WL(128, 128); else WL(128, 64); }
+      else if (TCO == 64) { if (TK == 128) WL(64, 128); else WL(64, 64); }
+      else { if (TK == 128) WL(32, 128); else WL(32, 64); }
+    }
+    else if (TCO == 128) { if (TK == 128) WG(128, 128, 2); else WG(128, 64, 2); }
     else if (TCO == 64) { if (TK == 128) WG(64, 128, 2); else WG(64, 64, 2); }
     else { if (TK == 128) WG(16, 128, 1); else WG(16, 64, 1); }
 #undef WG
+#undef WL
     int rc = ee_check_launch("conv_wgrad");
     if (rc || w.dw) return rc;
   } else {

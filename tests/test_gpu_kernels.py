@@ -51,6 +51,9 @@ CONV_CASES = [
     (2, 16, 8, 8, 24, 1, 1, 0, True, None, True),
     (4, 128, 32, 32, 256, 3, 1, 1, False, 'lrelu', False),
     (2, 48, 9, 9, 40, 3, 1, 1, False, None, False),
+    # many pixel splits of the weight gradient; odd widths (pixel walk wraps rows mid-step)
+    (8, 32, 64, 64, 32, 3, 1, 1, True, None, False),
+    (2, 32, 37, 23, 64, 4, 2, 1, False, 'lrelu', False),
 ]
 
 
@@ -87,6 +90,12 @@ def test_conv_fwd_bwd(gpu, case):
     assert rel_l2(m.weight.grad.cpu(), wr.grad) < 2e-2
     if bias:
         assert rel_l2(m.bias.grad.cpu(), br.grad) < 2e-2
+    # a second backward accumulates into the existing .grad in place (direct
+    # accumulation path of the weight / bias gradient kernels)
+    wg0 = m.weight.grad.clone()
+    y2 = m(xd.detach(), act=act, up2=up2)
+    y2.backward(_nhwc(gy, gpu))
+    assert rel_l2(m.weight.grad.cpu(), 2 * wg0.cpu()) < 1e-5
 
 
 def test_conv_double_backward(gpu):
