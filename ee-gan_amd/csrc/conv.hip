@@ -65,6 +65,39 @@ struct ConvArgs {
   int ncls, nsplit;             // parity classes (BWDD stride>1), K splits
 };
 
+// K step kt, 8-channel chunk kc -> kernel tap and channel.  Normal mode: the
+// step is one tap's 32-channel slice (block-uniform).  Packed mode (Cgp == 8,
+// inputs with <= 8 channels): the step covers 4 consecutive taps of 8 channels,
+// chunk kc being tap 4*kt + kc.  `kw` is the column in the packed weight row.
+struct TapPos {
+  int r, s, ta, tb, c, kw;
+  bool ok;
+};
+
+template <int MODE>
+EE_DEV TapPos tap_pos(const ConvArgs& a, int kt, int kc, int nc, int TS, int ntaps, int r0, int s0) {
+  TapPos t;
+  int tap, c;
+  if (a.Cgp == 8) {
+    tap = kt * 4 + kc;
+    c = 0;
+  } else {
+    tap = kt / nc;
+    c = (kt - tap * nc) * BK + kc * 8;
+  }
+  t.ok = tap < ntaps;
+  if (!t.ok) tap = 0;
+  t.ta = tap / TS;
+  t.tb = tap - t.ta * TS;
+  t.r = (MODE == MODE_FWD) ? t.ta : r0 + a.st * t.ta;
+  t.s = (MODE == MODE_FWD) ? t.tb : s0 + a.st * t.tb;
+  t.c = c;
+  t.kw = (t.r * a.S + t.s) * a.Cgp + c;
+  return t;
+}
+
+EE_DEV int k_steps(const ConvArgs& a, int ntaps) { return a.Cgp == 8 ? (ntaps + 3) / 4 : ntaps * (a.Cgp / BK); }
+
 // Epilogue shared by the GEMM kernels: fragment (i, j) of wave (wi, wj) holds 4
 // consecutive output channels of one pixel -> bias, activation, residual,
 // 8-byte NHWC store (or the fp32 split-K slab).
@@ -169,7 +202,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   const int pix0 = blockIdx.x * TPIX;
   if (pix0 >= Pc) return;  // block-uniform
   const int nc = a.Cgp / BK;
-  const int nk_all = TR * TS * nc;
+  const int ntaps = TR * TS;
+  const int nk_all = k_steps(a, ntaps);
   const int kchunk = (nk_all + a.nsplit - 1) / a.nsplit;
   const int kt0 = min(nk_all, split * kchunk), kt1 = min(nk_all, kt0 + kchunk);
 
@@ -200,32 +234,28 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 
   uint4 ra[A_PER], rb[B_PER];
   auto load_stage = [&](int kt) {
-    const int tap = kt / nc;
-    const int cc = kt - tap * nc;
-    const int ta = tap / TS, tb = tap - ta * TS;
-    const int r = (MODE == MODE_FWD) ? ta : r0 + a.st * ta;
-    const int s = (MODE == MODE_FWD) ? tb : s0 + a.st * tb;
-    const int kbase = (r * a.S + s) * a.Cgp + cc * BK;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int ch = tid + i * 256;
       if (ch < A_CHUNKS) {
         const int row = ch >> 2, kc = ch & 3;
-        ra[i] = *reinterpret_cast<const uint4*>(a.wp + (long)(co0 + row) * a.Kw + kbase + kc * 8);
+        const TapPos tp = tap_pos<MODE>(a, kt, kc, nc, TS, ntaps, r0, s0);
+        ra[i] = *reinterpret_cast<const uint4*>(a.wp + (long)(co0 + row) * a.Kw + tp.kw);
       }
     }
-    const int c = cc * BK + b_kc * 8;
+    const TapPos tp = tap_pos<MODE>(a, kt, b_kc, nc, TS, ntaps, r0, s0);
+    const int c = tp.c;
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (b_ok[i] && c < a.Cvalid) {
+      if (b_ok[i] && tp.ok && c < a.Cvalid) {
         long off = -1;
         if (MODE == MODE_FWD) {
-          const int iy = b_y[i] + r, ix = b_x[i] + s;
+          const int iy = b_y[i] + tp.r, ix = b_x[i] + tp.s;
           if ((unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW)
             off = ((long)(b_n[i] * PH + (iy >> a.up2)) * PW + (ix >> a.up2)) * a.lds_src;
         } else {
-          const int oy = b_y[i] - ta, ox = b_x[i] - tb;
+          const int oy = b_y[i] - tp.ta, ox = b_x[i] - tp.tb;
           if ((unsigned)oy < (unsigned)a.IH && (unsigned)ox < (unsigned)a.IW)
             off = ((long)(b_n[i] * a.IH + oy) * a.IW + ox) * a.lds_src;
         }
@@ -313,19 +343,21 @@ EE_DEV void wait_vmcnt() {
 template <int MODE, int TCO, int TPIX>
 __global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a, long src_bytes, long w_bytes) {
   constexpr int S = CONV_STAGES;
-  constexpr int WT_CO = TCO / 2, WT_PIX = TPIX / 2;
+  constexpr int WCO = TCO >= 64 ? 2 : 1, WPIX = 4 / WCO;
+  constexpr int WT_CO = TCO / WCO, WT_PIX = TPIX / WPIX;
   constexpr int FI = WT_CO / 16, FJ = WT_PIX / 16;
-  constexpr int A_INS = TCO / 64, B_INS = TPIX / 64;  // 16-B chunks per thread per K-step
-  constexpr int NLOAD = A_INS + B_INS;
-  constexpr int STAGE = (TCO + TPIX) * BK;           // bf16 elements per stage
-  static_assert(A_INS >= 1 && B_INS >= 1, "tile");
+  constexpr int A_TOT = TCO * 4, B_TOT = TPIX * 4;     // 16-B chunks per K-step
+  constexpr int A_INS = (A_TOT + 255) / 256, B_INS = B_TOT / 256;
+  constexpr int STAGE = (TCO + TPIX) * BK;             // bf16 elements per stage
+  static_assert(B_INS >= 1 && FI >= 1 && FJ >= 1, "tile");
 
   __shared__ __attribute__((aligned(16))) bf16_t lds[S * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wi = wave >> 1, wj = wave & 1;
+  const int wi = wave / WPIX, wj = wave % WPIX;
   const int cls = blockIdx.z % a.ncls, split = blockIdx.z / a.ncls;
   const int co0 = blockIdx.y * TCO;
+  const bool a_wave = A_TOT >= 256 || tid < A_TOT;      // waves that stage weight chunks
 
   int qy = 0, qx = 0, CH = a.OH, CW = a.OW, stc = 1;
   int r0 = 0, s0 = 0, TR = a.R, TS = a.S, dqy = 0, dqx = 0;
@@ -348,7 +380,8 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a, long src_
   const int pix0 = blockIdx.x * TPIX;
   if (pix0 >= Pc) return;  // block-uniform
   const int nc = a.Cgp / BK;
-  const int nk_all = TR * TS * nc;
+  const int ntaps = TR * TS;
+  const int nk_all = k_steps(a, ntaps);
   const int kchunk = (nk_all + a.nsplit - 1) / a.nsplit;
   const int kt0 = min(nk_all, split * kchunk), kt1 = min(nk_all, kt0 + kchunk);
   const int nk = kt1 - kt0;
@@ -382,29 +415,27 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a, long src_
   const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(a.wp, w_bytes);
 
   auto issue = [&](int kt, int buf) {
-    const int tap = kt / nc;
-    const int cc = kt - tap * nc;
-    const int ta = tap / TS, tb = tap - ta * TS;
-    const int r = (MODE == MODE_FWD) ? ta : r0 + a.st * ta;
-    const int s = (MODE == MODE_FWD) ? tb : s0 + a.st * tb;
-    const int kbase = (r * a.S + s) * a.Cgp + cc * BK + kc * 8;
+    const TapPos tp = tap_pos<MODE>(a, kt, kc, nc, TS, ntaps, r0, s0);
     bf16_t* base = lds + buf * STAGE;
+    if (a_wave) {
 #pragma unroll
-    for (int i = 0; i < A_INS; ++i) {
-      const unsigned off = (unsigned)(((co0 + i * 64 + rsub) * a.Kw + kbase) * 2);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_void_t*)(base + (i * 256 + wave * 64) * 8), 16, off, 0, 0, 0);
+      for (int i = 0; i < A_INS; ++i) {
+        const unsigned off = (unsigned)(((co0 + i * 64 + rsub) * a.Kw + tp.kw) * 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_void_t*)(base + (i * 256 + wave * 64) * 8), 16, off, 0,
+                                                 0, 0);
+      }
     }
-    const int c = cc * BK + kc * 8;
+    const int c = tp.c;
 #pragma unroll
     for (int i = 0; i < B_INS; ++i) {
       unsigned off = OOB;
-      if (b_ok[i] && c < a.Cvalid) {
+      if (b_ok[i] && tp.ok && c < a.Cvalid) {
         if (MODE == MODE_FWD) {
-          const int iy = b_y[i] + r, ix = b_x[i] + s;
+          const int iy = b_y[i] + tp.r, ix = b_x[i] + tp.s;
           if ((unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW)
             off = (unsigned)((((b_n[i] * PH + (iy >> a.up2)) * PW + (ix >> a.up2)) * a.lds_src + c) * 2);
         } else {
-          const int oy = b_y[i] - ta, ox = b_x[i] - tb;
+          const int oy = b_y[i] - tp.ta, ox = b_x[i] - tp.tb;
           if ((unsigned)oy < (unsigned)a.IH && (unsigned)ox < (unsigned)a.IW)
             off = (unsigned)((((b_n[i] * a.IH + oy) * a.IW + ox) * a.lds_src + c) * 2);
         }
@@ -420,13 +451,27 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a, long src_
 #pragma unroll
     for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  // packed-tap mode with < 8 valid channels: the staged chunks carry the
+  // tensor's padding channels, zero them in the B fragments (element e = channel e)
+  uint4 bmask = make_uint4(~0u, ~0u, ~0u, ~0u);
+  if (a.Cvalid < 8) {
+    uint32_t* m = reinterpret_cast<uint32_t*>(&bmask);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      m[j] = (2 * j < a.Cvalid ? 0xffffu : 0u) | (2 * j + 1 < a.Cvalid ? 0xffff0000u : 0u);
+  }
+
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
   for (int st = 0; st < S - 1; ++st)
     if (st < nk) issue(kt0 + st, st);
   for (int it = 0; it < nk; ++it) {
-    if (it + S - 2 < nk) wait_vmcnt<(S - 2) * NLOAD>();
-    else wait_vmcnt<0>();
+    if (it + S - 2 < nk) {
+      if (a_wave) wait_vmcnt<(S - 2) * (A_INS + B_INS)>();
+      else wait_vmcnt<(S - 2) * B_INS>();
+    } else {
+      wait_vmcnt<0>();
+    }
     __builtin_amdgcn_s_barrier();
     if (it + S - 1 < nk) issue(kt0 + it + S - 1, (it + S - 1) % S);
     const bf16_t* base = lds + (it % S) * STAGE;
@@ -439,7 +484,12 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a, long src_
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
       const int row = wj * WT_PIX + j * 16 + fr;
-      fb[j] = as_frag(*reinterpret_cast<const uint4*>(base + TCO * BK + row * BK + ((fq ^ ((row >> 2) & 3)) * 8)));
+      uint4 v = *reinterpret_cast<const uint4*>(base + TCO * BK + row * BK + ((fq ^ ((row >> 2) & 3)) * 8));
+      v.x &= bmask.x;
+      v.y &= bmask.y;
+      v.z &= bmask.z;
+      v.w &= bmask.w;
+      fb[j] = as_frag(v);
     }
 #pragma unroll
     for (int i = 0; i < FI; ++i)
@@ -833,7 +883,9 @@ __global__ void pack_weights_kernel(const float* w, const float* scale, int Cout
     const int rs = k / Cgp, c = k - rs * Cgp;
     const int r = rs / S, s = rs - r * S;
     float v = 0.f;
-    if (!transposed) {
+    if (rs >= R * S) {
+      // zero columns padding the row to whole 32-deep K steps
+    } else if (!transposed) {
       if (row < Cout && c < Cin) v = w[(((long)row * Cin + c) * R + r) * S + s] * (scale ? scale[row] : 1.f);
     } else {
       if (row < Cin && c < Cout) v = w[(((long)c * Cin + row) * R + r) * S + s] * (scale ? scale[c] : 1.f);
@@ -843,7 +895,8 @@ __global__ void pack_weights_kernel(const float* w, const float* scale, int Cout
 }
 
 // ------------------------------------------------------------ dispatch --
-int cgp_of(int C) { return ee_round_up(C, BK); }
+int cgp_of(int C) { return C <= 8 ? 8 : ee_round_up(C, BK); }
+int kw_of(int R, int S, int Cgp) { return ee_round_up(R * S * Cgp, BK); }
 
 struct Plan {
   int tco, tpix, nsplit, blocks;
@@ -860,7 +913,7 @@ Plan plan_igemm(const ConvArgs& a, int Pc_max) {
   // split K until the grid covers the chip twice, keeping >= 8 K-steps per split
   int taps = a.R * a.S;
   if (a.ncls > 1) taps = ee_cdiv(a.R, a.st) * ee_cdiv(a.S, a.st);
-  const int nk = taps * (a.Cgp / BK);
+  const int nk = a.Cgp == 8 ? (taps + 3) / 4 : taps * (a.Cgp / BK);
   p.nsplit = 1;
   while (p.blocks * p.nsplit < 512 && nk / (p.nsplit * 2) >= 8 && p.nsplit < 64) p.nsplit *= 2;
   return p;
@@ -879,10 +932,12 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   const long w_bytes = (long)ee_round_up(a.Mrows, 128) * a.Kw * 2;
 #define GL(TC, TP) ee_launch(conv_glds_kernel<MODE, TC, TP>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
 #define IG(TC, TP, WC) ee_launch(conv_igemm_kernel<MODE, TC, TP, WC>, grid, dim3(256), 0, s, a)
-  const bool glds = (a.Cvalid % 8) == 0 && p.tco >= 64 && src_bytes < 0x7fffffffL && w_bytes < 0x7fffffffL;
+  const bool glds = ((a.Cvalid % 8) == 0 || a.Cgp == 8) && src_bytes < 0x7fffffffL && w_bytes < 0x7fffffffL;
   if (glds) {
     if (p.tco == 128) { if (p.tpix == 128) GL(128, 128); else GL(128, 64); }
-    else { if (p.tpix == 128) GL(64, 128); else GL(64, 64); }
+    else if (p.tco == 64) { if (p.tpix == 128) GL(64, 128); else GL(64, 64); }
+    else if (p.tco == 32) { if (p.tpix == 256) GL(32, 256); else GL(32, 64); }
+    else { if (p.tpix == 256) GL(16, 256); else GL(16, 64); }
   }
   else if (p.tco == 128) { if (p.tpix == 128) IG(128, 128, 2); else IG(128, 64, 2); }
   else if (p.tco == 64) { if (p.tpix == 128) IG(64, 128, 2); else IG(64, 64, 2); }
@@ -919,7 +974,7 @@ void fill_fwd(ConvArgs& a, const eegan_conv_desc* d) {
   a.Cgp = cgp_of(d->C);
   a.Cvalid = d->C;
   a.Mrows = d->K;
-  a.Kw = d->R * d->S * a.Cgp;
+  a.Kw = kw_of(d->R, d->S, a.Cgp);
   a.P = d->N * d->Ho * d->Wo;
   a.ncls = 1;
   a.nsplit = 1;
@@ -942,7 +997,7 @@ void fill_bwdd(ConvArgs& a, const eegan_conv_desc* d) {
   a.Cgp = cgp_of(d->K);
   a.Cvalid = d->K;
   a.Mrows = d->C;
-  a.Kw = d->R * d->S * a.Cgp;
+  a.Kw = kw_of(d->R, d->S, a.Cgp);
   a.P = d->N * d->H * d->W;
   a.ncls = d->stride > 1 ? d->stride * d->stride : 1;
   a.nsplit = 1;
@@ -962,14 +1017,14 @@ extern "C" {
 long eegan_conv_packed_elems(int Cout, int Cin, int R, int S, int transposed) {
   const int rows = transposed ? Cin : Cout;
   const int Cgp = cgp_of(transposed ? Cout : Cin);
-  return (long)ee_round_up(rows, 128) * R * S * Cgp;
+  return (long)ee_round_up(rows, 128) * kw_of(R, S, Cgp);
 }
 
 int eegan_conv_pack_weights(const float* w, const float* scale, int Cout, int Cin, int R, int S, int transposed,
                             bf16_t* out, hipStream_t stream) {
   const int rows = transposed ? Cin : Cout;
   const int Cgp = cgp_of(transposed ? Cout : Cin);
-  const int rows_pad = ee_round_up(rows, 128), Kw = R * S * Cgp;
+  const int rows_pad = ee_round_up(rows, 128), Kw = kw_of(R, S, Cgp);
   const long total = (long)rows_pad * Kw;
   const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
   pack_weights_kernel<<<blocks, 256, 0, stream>>>(w, scale, Cout, Cin, R, S, transposed, Cgp, rows_pad, Kw, out);

@@ -21,9 +21,12 @@ def test_library_exports_header_symbols():
         assert name in _lib._SIGS, name               # bound with a ctypes signature
     assert set(_lib._SIGS) == set(declared)
     assert eegan_hip.ABI_VERSION == 1
-    # rows padded to 128, every tap's channel run padded to 32
-    assert _lib.ops.conv_packed_elems(100, 3, 3, 3, 0) == 128 * 9 * 32
+    # rows padded to 128; every tap's channel run padded to 32 (to 8 for <= 8
+    # channels: 4 taps per K step), rows padded to whole 32-deep steps
+    assert _lib.ops.conv_packed_elems(100, 3, 3, 3, 0) == 128 * 96
     assert _lib.ops.conv_packed_elems(100, 3, 3, 3, 1) == 128 * 9 * 128
+    assert _lib.ops.conv_packed_elems(3, 32, 3, 3, 1) == 128 * 96
+    assert _lib.ops.conv_packed_elems(64, 48, 4, 4, 0) == 128 * 16 * 64
     from eegan_hip.tensor import ld_for
     assert ld_for(3) == 8 and ld_for(100) == 104 and ld_for(1, torch.float32) == 1
 
