@@ -14,6 +14,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 typedef __attribute__((ext_vector_type(4))) short s16x4_t;
 
 #define EE_DEV __device__ __forceinline__
+#define EE_HOST_DEV_INLINE __host__ __device__ __forceinline__
 
 EE_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 EE_DEV bf16_t f2bf(float f) {

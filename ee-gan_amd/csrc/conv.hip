@@ -19,6 +19,8 @@
 // naive MFMA work).  Small grids are split along K (fp32 partial slab +
 // a reduce kernel that applies the epilogue).
 // Replaces every nn.Conv2d of models.py:14-403 and DAMSM.py.
+#include <stdlib.h>
+
 #include "common.h"
 #include "../../include/eegan_hip.h"
 
@@ -894,6 +896,128 @@ __global__ void pack_weights_kernel(const float* w, const float* scale, int Cout
   }
 }
 
+// Batched re-pack after an optimizer step: one launch for every conv weight of a
+// model (fwd and bwd-data images), staged through LDS so both the fp32 reads
+// and the bf16 writes are contiguous.  `table` (device, int64): njobs rows of
+// {w, scale, out, Cout, Cin, R, S, transposed}, then njobs+1 prefix offsets of
+// BLOCKS per job (pack_multi_blocks).  Forward image: one block per output row
+// (w[co] is one contiguous Cin*R*S run); bwd-data image: one block per 8 input
+// channels, streaming the output channels in chunks of 128.
+constexpr int PK_LDS = 9344;   // floats of staging (128 x 73)
+
+EE_HOST_DEV_INLINE int pk_cgp(int C) { return C <= 8 ? 8 : (C + BK - 1) / BK * BK; }
+// output channels per bwd-image block: 8 input channels x RS taps x CO fit the staging
+EE_HOST_DEV_INLINE int pk_bwd_co(int RS) { return min(128, PK_LDS / (8 * RS + 1)); }
+
+__global__ __launch_bounds__(256) void pack_weights_multi_kernel(const long* __restrict__ table, int njobs) {
+  __shared__ float buf[PK_LDS];
+  const long* pre = table + 8L * njobs;
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pre[mid] <= blockIdx.x) lo = mid;
+    else hi = mid - 1;
+  }
+  const long* j = table + 8L * lo;
+  const int lb = (int)(blockIdx.x - pre[lo]);
+  const float* w = reinterpret_cast<const float*>(j[0]);
+  const float* scale = reinterpret_cast<const float*>(j[1]);
+  bf16_t* out = reinterpret_cast<bf16_t*>(j[2]);
+  const int Cout = (int)j[3], Cin = (int)j[4], RS = (int)(j[5] * j[6]), tr = (int)j[7];
+  const int t = threadIdx.x;
+  if (!tr) {
+    // ---- forward image: row co = lb, out[co][tap*Cgp + c] = w[co][c][tap]
+    const int Cgp = pk_cgp(Cin), Kw = (RS * Cgp + BK - 1) / BK * BK;
+    bf16_t* orow = out + (long)lb * Kw;
+    if (lb >= Cout) {
+      for (int k = t; k < Kw; k += 256) orow[k] = 0;
+      return;
+    }
+    const float sc = scale ? scale[lb] : 1.f;
+    const int RSP = RS | 1;  // odd LDS row stride: conflict-free column reads
+    const int cc = max(1, PK_LDS / RSP);
+    for (int c0 = 0; c0 < Cin; c0 += cc) {
+      const int nc = min(cc, Cin - c0);
+      __syncthreads();
+      // 8 independent loads in flight per thread before their LDS stores
+      const float* src = w + ((long)lb * Cin + c0) * RS;
+      for (int e0 = t; e0 < nc * RS; e0 += 256 * 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int e = e0 + u * 256;
+          v[u] = e < nc * RS ? src[e] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int e = e0 + u * 256;
+          if (e < nc * RS) {
+            const int c = e / RS, tap = e - c * RS;
+            buf[c * RSP + tap] = v[u];
+          }
+        }
+      }
+      __syncthreads();
+      for (int e = t; e < nc * RS; e += 256) {
+        const int tap = e / nc, c = e - tap * nc;
+        orow[tap * Cgp + c0 + c] = f2bf(buf[c * RSP + tap] * sc);
+      }
+    }
+    for (int e = t; e < RS * (Cgp - Cin); e += 256) {  // channel padding of every tap
+      const int tap = e / (Cgp - Cin), c = Cin + e - tap * (Cgp - Cin);
+      orow[tap * Cgp + c] = 0;
+    }
+    for (int k = RS * Cgp + t; k < Kw; k += 256) orow[k] = 0;
+  } else {
+    // ---- bwd-data image: rows ci0..ci0+7 x one chunk of CO output channels,
+    // out[ci][tap*Cgp + co] = w[co][ci][tap]
+    constexpr int TI = 8;
+    const int Cgp = pk_cgp(Cout), Kw = (RS * Cgp + BK - 1) / BK * BK;
+    const int RW = TI * RS + 1;  // odd LDS row stride
+    const int CO = pk_bwd_co(RS);
+    const int nchunk = (Cgp + CO - 1) / CO;
+    const int ci0 = (lb / nchunk) * TI, co0 = (lb % nchunk) * CO;
+    const int ni = max(0, min(TI, Cin - ci0));
+    {
+      const int nco = min(CO, Cout - co0);  // may be <= 0 in the channel padding
+      const int nload = max(nco, 0) * ni * RS;
+      for (int e0 = t; e0 < nload; e0 += 256 * 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int e = e0 + u * 256;
+          v[u] = 0.f;
+          if (e < nload) {
+            const int co = e / (ni * RS), q = e - co * (ni * RS);
+            v[u] = w[((long)(co0 + co) * Cin + ci0) * RS + q] * (scale ? scale[co0 + co] : 1.f);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int e = e0 + u * 256;
+          if (e < nload) {
+            const int co = e / (ni * RS), q = e - co * (ni * RS);
+            buf[co * RW + q] = v[u];
+          }
+        }
+      }
+      __syncthreads();
+      const int ncol = min(CO, Cgp - co0);
+      for (int e = t; e < TI * RS * ncol; e += 256) {
+        const int row = e / (RS * ncol), rem = e - row * (RS * ncol);
+        const int tap = rem / ncol, co = rem - tap * ncol;
+        const float v = (row < ni && co < nco) ? buf[co * RW + row * RS + tap] : 0.f;
+        out[(long)(ci0 + row) * Kw + tap * Cgp + co0 + co] = f2bf(v);
+      }
+    }
+    if (co0 + CO < Cgp) return;  // the last channel chunk also zeroes the row tail
+    for (int e = t; e < TI * (Kw - RS * Cgp); e += 256) {
+      const int row = e / (Kw - RS * Cgp), k = RS * Cgp + e - row * (Kw - RS * Cgp);
+      out[(long)(ci0 + row) * Kw + k] = 0;
+    }
+  }
+}
+
 // ------------------------------------------------------------ dispatch --
 int cgp_of(int C) { return C <= 8 ? 8 : ee_round_up(C, BK); }
 int kw_of(int R, int S, int Cgp) { return ee_round_up(R * S * Cgp, BK); }
@@ -902,20 +1026,34 @@ struct Plan {
   int tco, tpix, nsplit, blocks;
 };
 
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
 Plan plan_igemm(const ConvArgs& a, int Pc_max) {
+  // tuning knobs (benchmark sweeps only): grid target, min K-steps per split,
+  // and whether 64-row tiles are tried before splitting K
+  const int target = env_int("EEGAN_CONV_TARGET", 512);
+  const int mink = env_int("EEGAN_CONV_MINK", 8);
+  const int small_co = env_int("EEGAN_CONV_SMALLCO", 0);
   const int rows = a.Mrows;
   Plan p;
   p.tco = rows > 64 ? 128 : rows > 32 ? 64 : rows > 16 ? 32 : 16;
-  const int co_t = ee_cdiv(rows, p.tco);
+  int co_t = ee_cdiv(rows, p.tco);
   p.tpix = (p.tco <= 32) ? 256 : 128;
-  if ((long)ee_cdiv(Pc_max, p.tpix) * co_t * a.ncls < 512) p.tpix = 64;
+  if ((long)ee_cdiv(Pc_max, p.tpix) * co_t * a.ncls < target) p.tpix = 64;
+  if (small_co && p.tco == 128 && (long)ee_cdiv(Pc_max, p.tpix) * co_t * a.ncls < target) {
+    p.tco = 64;
+    co_t = ee_cdiv(rows, p.tco);
+  }
   p.blocks = ee_cdiv(Pc_max, p.tpix) * co_t * a.ncls;
-  // split K until the grid covers the chip twice, keeping >= 8 K-steps per split
+  // split K until the grid covers the chip twice, keeping >= mink K-steps per split
   int taps = a.R * a.S;
   if (a.ncls > 1) taps = ee_cdiv(a.R, a.st) * ee_cdiv(a.S, a.st);
   const int nk = a.Cgp == 8 ? (taps + 3) / 4 : taps * (a.Cgp / BK);
   p.nsplit = 1;
-  while (p.blocks * p.nsplit < 512 && nk / (p.nsplit * 2) >= 8 && p.nsplit < 64) p.nsplit *= 2;
+  while (p.blocks * p.nsplit < target && nk / (p.nsplit * 2) >= mink && p.nsplit < 64) p.nsplit *= 2;
   return p;
 }
 
@@ -1029,6 +1167,17 @@ int eegan_conv_pack_weights(const float* w, const float* scale, int Cout, int Ci
   const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
   pack_weights_kernel<<<blocks, 256, 0, stream>>>(w, scale, Cout, Cin, R, S, transposed, Cgp, rows_pad, Kw, out);
   return ee_check_launch("pack_weights");
+}
+
+long eegan_conv_pack_multi_blocks(int Cout, int Cin, int R, int S, int transposed) {
+  if (!transposed) return ee_round_up(Cout, 128);
+  return (long)(ee_round_up(Cin, 128) / 8) * ee_cdiv(pk_cgp(Cout), pk_bwd_co(R * S));
+}
+
+int eegan_conv_pack_weights_multi(const long* table, int njobs, long total_blocks, hipStream_t stream) {
+  if (njobs <= 0 || total_blocks <= 0) return 0;
+  pack_weights_multi_kernel<<<(unsigned)total_blocks, 256, 0, stream>>>(table, njobs);
+  return ee_check_launch("pack_weights_multi");
 }
 
 long eegan_conv_fwd_workspace(const eegan_conv_desc* d) {

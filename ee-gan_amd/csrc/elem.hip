@@ -405,48 +405,69 @@ __global__ void fc_to_nhwc_kernel(const void* x, int x_f32, int N, int C, int HW
 }
 
 // 3x3 / stride-2 max pool (no padding) with argmax (0..8) and its adjoint
+// 3x3 / stride-2 max pool over 8-channel groups; arg[p][c] = winning tap (first max, NaN wins)
 __global__ void maxpool3s2_kernel(const bf16_t* x, int N, int H, int W, int C, int ld, int Ho, int Wo, bf16_t* y,
                                   int ldy, uint8_t* arg) {
-  GRID_LOOP(e, (long)N * Ho * Wo * C) {
-    const int c = e % C;
-    const long p = e / C;
+  const int C8 = (C + 7) / 8;
+  const bool vec = (ld % 8 == 0) && (ldy % 8 == 0);
+  GRID_LOOP(e, (long)N * Ho * Wo * C8) {
+    const int c0 = (int)(e % C8) * 8;
+    const long p = e / C8;
     const int ox = p % Wo;
     const long t = p / Wo;
     const int oy = t % Ho, n = t / Ho;
-    float best = -INFINITY;
-    int bi = 0;
+    const int nv = min(8, C - c0);
+    V8 best;
+    int bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      best.v[j] = -INFINITY;
+      bi[j] = 0;
+    }
     for (int k = 0; k < 9; ++k) {
       const int iy = 2 * oy + k / 3, ix = 2 * ox + k % 3;
-      const float v = bf2f(x[(((long)n * H + iy) * W + ix) * ld + c]);
-      if (v > best || (v != v)) {
-        best = v;
-        bi = k;
-        if (v != v) break;
-      }
+      const V8 a = load8(x + (((long)n * H + iy) * W + ix) * ld + c0, nv, vec);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if ((a.v[j] > best.v[j] || a.v[j] != a.v[j]) && best.v[j] == best.v[j]) {
+          best.v[j] = a.v[j];
+          bi[j] = k;
+        }
     }
-    y[p * ldy + c] = f2bf(best);
-    arg[e] = (uint8_t)bi;
+    store8(y + p * ldy + c0, best, nv, vec);
+    for (int j = 0; j < nv; ++j) arg[p * C + c0 + j] = (uint8_t)bi[j];
   }
 }
+
 __global__ void maxpool3s2_bwd_kernel(const bf16_t* dy, int lddy, const uint8_t* arg, int N, int H, int W, int C,
                                       int Ho, int Wo, bf16_t* dx, int lddx) {
-  GRID_LOOP(e, (long)N * H * W * C) {
-    const int c = e % C;
-    const long p = e / C;
+  const int C8 = (C + 7) / 8;
+  const bool vec = (lddy % 8 == 0) && (lddx % 8 == 0);
+  GRID_LOOP(e, (long)N * H * W * C8) {
+    const int c0 = (int)(e % C8) * 8;
+    const long p = e / C8;
     const int ix = p % W;
     const long t = p / W;
     const int iy = t % H, n = t / H;
-    float s = 0.f;
+    const int nv = min(8, C - c0);
+    V8 s;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s.v[j] = 0.f;
     const int oy_lo = max(0, (iy - 1) / 2), oy_hi = min(Ho - 1, iy / 2);
     const int ox_lo = max(0, (ix - 1) / 2), ox_hi = min(Wo - 1, ix / 2);
     for (int oy = oy_lo; oy <= oy_hi; ++oy)
       for (int ox = ox_lo; ox <= ox_hi; ++ox) {
-        const int k = (iy - 2 * oy) * 3 + (ix - 2 * ox);
-        if (k < 0 || k > 8 || iy - 2 * oy > 2 || ix - 2 * ox > 2) continue;
+        const int dyy = iy - 2 * oy, dxx = ix - 2 * ox;
+        if (dyy < 0 || dyy > 2 || dxx < 0 || dxx > 2) continue;
+        const int k = dyy * 3 + dxx;
         const long op = ((long)n * Ho + oy) * Wo + ox;
-        if (arg[op * C + c] == k) s += bf2f(dy[op * lddy + c]);
+        const V8 g = load8(dy + op * lddy + c0, nv, vec);
+        const uint8_t* ar = arg + op * C + c0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j < nv && ar[j] == k) s.v[j] += g.v[j];
       }
-    dx[p * lddx + c] = f2bf(s);
+    store8(dx + p * lddx + c0, s, nv, vec);
   }
 }
 
@@ -620,14 +641,14 @@ int eegan_nhwc_to_fc(const uint16_t* y, int ldy, int N, int C, int HW, void* x, 
 int eegan_maxpool3s2(const uint16_t* x, int N, int H, int W, int C, int ld, uint16_t* y, int ldy, uint8_t* arg,
                      hipStream_t s) {
   const int Ho = (H - 3) / 2 + 1, Wo = (W - 3) / 2 + 1;
-  maxpool3s2_kernel<<<grid_for((long)N * Ho * Wo * C), NT, 0, s>>>(x, N, H, W, C, ld, Ho, Wo, y, ldy, arg);
+  maxpool3s2_kernel<<<grid_for((long)N * Ho * Wo * ((C + 7) / 8)), NT, 0, s>>>(x, N, H, W, C, ld, Ho, Wo, y, ldy, arg);
   return ee_check_launch("maxpool3s2");
 }
 
 int eegan_maxpool3s2_bwd(const uint16_t* dy, int lddy, const uint8_t* arg, int N, int H, int W, int C, uint16_t* dx,
                          int lddx, hipStream_t s) {
   const int Ho = (H - 3) / 2 + 1, Wo = (W - 3) / 2 + 1;
-  maxpool3s2_bwd_kernel<<<grid_for((long)N * H * W * C), NT, 0, s>>>(dy, lddy, arg, N, H, W, C, Ho, Wo, dx, lddx);
+  maxpool3s2_bwd_kernel<<<grid_for((long)N * H * W * ((C + 7) / 8)), NT, 0, s>>>(dy, lddy, arg, N, H, W, C, Ho, Wo, dx, lddx);
   return ee_check_launch("maxpool3s2_bwd");
 }
 

@@ -367,48 +367,84 @@ __global__ void bce_kernel(const float* x, const float* y, int n, float* out, co
 
 // ----------------------------------------------------- gradient penalty --
 // per-sample ||[g_img, g_sent]||^2 (g_img NHWC bf16 [B][HW][ld] with C channels)
-__global__ void gp_norm_kernel(const bf16_t* gx, int ld, int HW, int C, const float* gs, int E, float* nrm2) {
+constexpr int GP_CHUNKS = 64;
+
+// per-(chunk, sample) partial sum of squares of the image gradient (16-B pixel rows)
+__global__ __launch_bounds__(256) void gp_norm_kernel(const bf16_t* gx, int ld, int HW, int C, float* ws) {
   __shared__ float red[16];
-  const int b = blockIdx.x;
+  const int b = blockIdx.y;
+  const int per = (HW + GP_CHUNKS - 1) / GP_CHUNKS;
+  const int p0 = blockIdx.x * per, p1 = min(HW, p0 + per);
+  const int C8 = (C + 7) / 8;
   float s = 0.f;
-  for (long e = threadIdx.x; e < (long)HW * C; e += blockDim.x) {
-    const float v = bf2f(gx[((long)b * HW + e / C) * ld + e % C]);
-    s += v * v;
-  }
-  for (int e = threadIdx.x; e < E; e += blockDim.x) {
-    const float v = gs[(long)b * E + e];
-    s += v * v;
+  for (long e = threadIdx.x; e < (long)(p1 - p0) * C8; e += blockDim.x) {
+    const int c0 = (int)(e % C8) * 8;
+    const long p = p0 + e / C8;
+    const uint4 v = *reinterpret_cast<const uint4*>(gx + ((long)b * HW + p) * ld + c0);
+    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float lo = c0 + 2 * j < C ? lo_f(w4[j]) : 0.f, hi = c0 + 2 * j + 1 < C ? hi_f(w4[j]) : 0.f;
+      s += lo * lo + hi * hi;
+    }
   }
   s = block_sum(s, red);
-  if (threadIdx.x == 0) nrm2[b] = s;
+  if (threadIdx.x == 0) ws[b * GP_CHUNKS + blockIdx.x] = s;
 }
 
-// loss = 2 * mean_b(||g_b||^6)
-__global__ void gp_loss_kernel(const float* nrm2, int B, float* out) {
+// nrm2[b] = sum of the chunk partials (fixed order) + ||g_sent_b||^2 ; loss = 2 * mean_b(||g_b||^6)
+__global__ void gp_loss_kernel(const float* ws, const float* gs, int E, int B, float* nrm2, float* out) {
   __shared__ float red[16];
-  float s = 0.f;
-  for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    const float n = sqrtf(nrm2[b]);
-    const float n2 = n * n;
-    s += n2 * n2 * n2;
+  __shared__ float n2s[256];
+  for (int b = 0; b < B; ++b) {
+    float t = 0.f;
+    for (int e = threadIdx.x; e < E; e += blockDim.x) {
+      const float v = gs[(long)b * E + e];
+      t += v * v;
+    }
+    t = block_sum(t, red);
+    if (threadIdx.x == 0) {
+      float sb = 0.f;
+      for (int k = 0; k < GP_CHUNKS; ++k) sb += ws[b * GP_CHUNKS + k];
+      nrm2[b] = sb + t;
+      if (b < 256) n2s[b] = sb + t;
+    }
   }
-  s = block_sum(s, red);
-  if (threadIdx.x == 0) out[0] = 2.f * s / B;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) {
+      const float n2 = b < 256 ? n2s[b] : nrm2[b];
+      s += n2 * n2 * n2;
+    }
+    out[0] = 2.f * s / B;
+  }
 }
 
 // d/dg: 2/B * 6 ||g||^4 g * gout
 __global__ void gp_bwd_kernel(const bf16_t* gx, int ld, int HW, int C, const float* gs, int E, const float* nrm2,
                               int B, const float* gout, bf16_t* dgx, int lddgx, float* dgs) {
-  const long nimg = (long)B * HW * C;
+  const int C8 = (C + 7) / 8;
+  const long nimg = (long)B * HW * C8;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nimg + (long)B * E;
        e += (long)gridDim.x * blockDim.x) {
     if (e < nimg) {
-      const int c = e % C;
-      const long p = e / C;
-      const int b = p / HW;
+      const int c0 = (int)(e % C8) * 8;
+      const long p = e / C8;
+      const int b = (int)(p / HW);
       const float n2 = nrm2[b];
       const float coef = gout[0] * 12.f / B * n2 * n2;
-      dgx[p * lddgx + c] = f2bf(coef * bf2f(gx[p * ld + c]));
+      const uint4 v = *reinterpret_cast<const uint4*>(gx + p * ld + c0);
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = pack2(coef * lo_f(w4[j]), coef * hi_f(w4[j]));
+      bf16_t* dst = dgx + p * lddgx + c0;
+      if (c0 + 8 <= C) {
+        *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+      } else {
+        for (int j = 0; j < 8 && c0 + j < C; ++j) dst[j] = (bf16_t)((o[j >> 1] >> (16 * (j & 1))) & 0xffffu);
+      }
     } else {
       const long q = e - nimg;
       const int b = q / E;
@@ -608,18 +644,28 @@ int eegan_bce_logits_bwd(const float* x, const float* target, int n, const float
   return ee_check_launch("bce_bwd");
 }
 
+long eegan_gp_loss_workspace(int B) { return (long)B * GP_CHUNKS * sizeof(float); }
+
 int eegan_gp_loss(const uint16_t* gx, int ld, int B, int HW, int C, const float* gs, int E, float* nrm2, float* out,
-                  hipStream_t s) {
-  gp_norm_kernel<<<B, 256, 0, s>>>(gx, ld, HW, C, gs, E, nrm2);
+                  float* ws, hipStream_t s) {
+  if ((ld % 8) || ((uintptr_t)gx & 15)) {
+    ee_set_error("gp_loss: image gradient rows must be 16-byte aligned, ld %% 8 == 0 (ld %d)", ld);
+    return -22;
+  }
+  gp_norm_kernel<<<dim3(GP_CHUNKS, B), 256, 0, s>>>(gx, ld, HW, C, ws);
   int rc = ee_check_launch("gp_norm");
   if (rc) return rc;
-  gp_loss_kernel<<<1, 256, 0, s>>>(nrm2, B, out);
+  gp_loss_kernel<<<1, 256, 0, s>>>(ws, gs, E, B, nrm2, out);
   return ee_check_launch("gp_loss");
 }
 
 int eegan_gp_loss_bwd(const uint16_t* gx, int ld, int B, int HW, int C, const float* gs, int E, const float* nrm2,
                       const float* gout, uint16_t* dgx, int lddgx, float* dgs, hipStream_t s) {
-  const long work = (long)B * HW * C + (long)B * E;
+  if ((ld % 8) || (lddgx % 8)) {
+    ee_set_error("gp_loss_bwd: channel strides must be multiples of 8");
+    return -22;
+  }
+  const long work = (long)B * HW * ((C + 7) / 8) + (long)B * E;
   const int blocks = (int)std::min<long>(8192, (work + 255) / 256);
   gp_bwd_kernel<<<blocks, 256, 0, s>>>(gx, ld, HW, C, gs, E, nrm2, B, gout, dgx, lddgx, dgs);
   return ee_check_launch("gp_bwd");

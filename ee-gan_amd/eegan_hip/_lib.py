@@ -41,6 +41,8 @@ _SIGS = {
     'eegan_timing_disarm': ([P], I),
     'eegan_conv_packed_elems': ([I, I, I, I, I], L),
     'eegan_conv_pack_weights': ([P, P, I, I, I, I, I, P, P], I),
+    'eegan_conv_pack_multi_blocks': ([I, I, I, I, I], L),
+    'eegan_conv_pack_weights_multi': ([P, I, L, P], I),
     'eegan_conv_fwd_workspace': ([CD], L),
     'eegan_conv_bwd_data_workspace': ([CD], L),
     'eegan_conv_fwd': ([CD, P, P, P, I, F, P, I, P, P, I, P, P], I),
@@ -91,7 +93,8 @@ _SIGS = {
     'eegan_dout_reduce_bwd': ([P, I, I, P, P, P], I),
     'eegan_bce_logits': ([P, P, I, P, P], I),
     'eegan_bce_logits_bwd': ([P, P, I, P, P, P], I),
-    'eegan_gp_loss': ([P, I, I, I, I, P, I, P, P, P], I),
+    'eegan_gp_loss_workspace': ([I], L),
+    'eegan_gp_loss': ([P, I, I, I, I, P, I, P, P, P, P], I),
     'eegan_gp_loss_bwd': ([P, I, I, I, I, P, I, P, P, P, I, P, P], I),
     'eegan_class_onehot': ([P, I, I, P, P, P], I),
     'eegan_attr_attn': ([P, P, P, I, I, I, F, P, P, P, P], I),

@@ -83,6 +83,7 @@ class PackCache:
         return (W.data_ptr(), W._version, gen[0] if gen is not None else 0)
 
     def get(self, W, transposed):
+        W._eegan_packcache = self   # FlatAdam re-packs registered weights in one launch after its step
         key = self._key(W)
         if transposed:
             if self.bwd_key != key:
@@ -1007,8 +1008,9 @@ class GradPenaltyFn(torch.autograd.Function):
         N, C, H, W = gx.shape
         nrm2 = torch.empty(N, dtype=F32, device=gx.device)
         out = torch.empty((), dtype=F32, device=gx.device)
+        ws = workspace(ops.gp_loss_workspace(N), gx.device)
         ops.gp_loss(gx.data_ptr(), ld_of(gx), N, H * W, C, gs.data_ptr(), gs.shape[1], nrm2.data_ptr(),
-                    out.data_ptr(), stream())
+                    out.data_ptr(), ws.data_ptr(), stream())
         ctx.save_for_backward(gx, gs, nrm2)
         return out
 

@@ -7,7 +7,9 @@ zero_grad is one fill and step is one fused kernel launch.  With a process
 group, step() first averages the flat gradient buffer across ranks with
 bucketed RCCL all-reduces (data parallelism; train.py's DataParallel
 gradient reduction).  After each step a generation counter shared by the
-parameters is bumped so cached bf16 weight packs are rebuilt.
+parameters is bumped and every conv weight's bf16 packs (forward and
+backward-data images, eegan_hip.functional.PackCache) are rebuilt in ONE
+batched launch, so no per-layer pack kernel runs in the next forward/backward.
 """
 import torch
 
@@ -52,6 +54,9 @@ class FlatAdam(torch.optim.Optimizer):
                 p.grad = g
                 p._eegan_gen = self._gen
                 self._views.append((p, o, k, g))
+        self._pack_sig = None
+        self._pack_table = None
+        self._pack_total = 0
         self.step_count = 0   # host mirror (state_dict); the kernels use step_dev
         self.step_dev = torch.zeros(1, dtype=torch.float64, device=dev)
 
@@ -91,4 +96,40 @@ class FlatAdam(torch.optim.Optimizer):
         ops.adam(self.flat.data_ptr(), self.gflat.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.numel, b1, b2,
                  g['lr'], g['eps'], g['weight_decay'], self.step_dev.data_ptr(), stream())
         self._gen[0] += 1
+        self._repack()
         return loss
+
+    def _repack(self):
+        """Refresh the registered bf16 packs of this optimizer's conv weights in
+        one launch; their cache keys then match the new generation."""
+        from .functional import PackCache
+        jobs = []
+        for p, o, k, g in self._views:
+            c = getattr(p, '_eegan_packcache', None)
+            if c is None or p.dim() != 4 or c.scale is not None:
+                continue
+            for tr, buf in ((False, c.fwd), (True, c.bwd)):
+                if buf is not None:
+                    jobs.append((p, c, tr, buf))
+        if not jobs:
+            return
+        sig = tuple((id(c), tr, buf.data_ptr(), buf.numel()) for p, c, tr, buf in jobs)
+        if sig != self._pack_sig:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError('FlatAdam: the set of weight packs changed during graph capture; '
+                                   'run an eager warm-up step first')
+            rows, pre = [], [0]
+            for p, c, tr, buf in jobs:
+                Cout, Cin, R, S = p.shape
+                rows += [p.data_ptr(), 0, buf.data_ptr(), Cout, Cin, R, S, int(tr)]
+                pre.append(pre[-1] + ops.conv_pack_multi_blocks(Cout, Cin, R, S, int(tr)))
+            self._pack_table = torch.tensor(rows + pre, dtype=torch.int64).to(self.flat.device)
+            self._pack_total = pre[-1]
+            self._pack_sig = sig
+        ops.conv_pack_weights_multi(self._pack_table.data_ptr(), len(jobs), self._pack_total, stream())
+        for p, c, tr, buf in jobs:
+            key = PackCache._key(p)
+            if tr:
+                c.bwd_key = key
+            else:
+                c.fwd_key = key

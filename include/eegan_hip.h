@@ -63,6 +63,13 @@ long eegan_conv_packed_elems(int Cout, int Cin, int R, int S, int transposed);
  * transposed=0: forward image [Cout][R][S][Cin_32]; 1: bwd-data image [Cin][R][S][Cout_32] */
 int eegan_conv_pack_weights(const float* w, const float* scale, int Cout, int Cin, int R, int S,
                             int transposed, uint16_t* out, hipStream_t stream);
+/* every conv weight of one optimizer re-packed in ONE launch after its Adam step
+ * (the per-weight packs above, batched).  `table` is device memory, int64:
+ * njobs rows {w, scale, out, Cout, Cin, R, S, transposed} followed by njobs+1
+ * prefix offsets of the blocks each job takes (eegan_conv_pack_multi_blocks);
+ * `total_blocks` = the last offset. */
+long eegan_conv_pack_multi_blocks(int Cout, int Cin, int R, int S, int transposed);
+int eegan_conv_pack_weights_multi(const long* table, int njobs, long total_blocks, hipStream_t s);
 /* split-K partial-slab bytes the call needs (0 when the grid is large enough) */
 long eegan_conv_fwd_workspace(const eegan_conv_desc* d);
 long eegan_conv_bwd_data_workspace(const eegan_conv_desc* d);
@@ -190,8 +197,9 @@ int eegan_dout_reduce_bwd(const float* x, int n, int mode, const float* gout, fl
 int eegan_bce_logits(const float* x, const float* target, int n, float* out, hipStream_t s);
 int eegan_bce_logits_bwd(const float* x, const float* target, int n, const float* gout, float* dx, hipStream_t s);
 /* MA gradient penalty: out = 2 * mean_b ||[g_img_b, g_sent_b]||^6 */
+long eegan_gp_loss_workspace(int B);
 int eegan_gp_loss(const uint16_t* gx, int ld, int B, int HW, int C, const float* gs, int E, float* nrm2, float* out,
-                  hipStream_t s);
+                  float* ws, hipStream_t s);
 int eegan_gp_loss_bwd(const uint16_t* gx, int ld, int B, int HW, int C, const float* gs, int E, const float* nrm2,
                       const float* gout, uint16_t* dgx, int lddgx, float* dgs, hipStream_t s);
 /* labels[i][(id_i - 1) mod ncls] = 1 (bit-exact with train.py:99-103; *err set if an id is out of range) */

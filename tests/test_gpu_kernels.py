@@ -369,3 +369,29 @@ def test_adam_matches_torch(gpu):
         ref.step()
     for p, q in zip(ps, qs):
         assert torch.allclose(p.detach(), q.detach(), rtol=1e-5, atol=1e-7)
+
+
+def test_flat_adam_repacks_conv_weights(gpu):
+    """After FlatAdam.step() every registered conv weight pack (forward and
+    bwd-data image, refreshed by ONE batched launch) equals a fresh per-weight
+    pack of the updated weights, and the caches are marked current."""
+    from eegan_hip.optim import FlatAdam
+    Fn, T, Conv2d = _mods()
+    torch.manual_seed(21)
+    m1 = Conv2d(3, 40, 3, 1, 1).to(gpu)
+    m2 = Conv2d(40, 136, 4, 2, 1).to(gpu)
+    m3 = Conv2d(136, 3, 1, 1, 0).to(gpu)
+    mods = (m1, m2, m3)
+    opt = FlatAdam([p for m in mods for p in m.parameters()], lr=1e-2, betas=(0.0, 0.9))
+    for _ in range(2):
+        opt.zero_grad()
+        x = _nhwc(_bf(torch.randn(2, 3, 8, 8)), gpu).requires_grad_()
+        y = m3(m2(m1(x, act='lrelu')))
+        y.backward(torch.ones_like(y))
+        opt.step()
+    for m in mods:
+        c = m._cache
+        assert c.fwd is not None and c.bwd is not None
+        for tr, buf, key in ((False, c.fwd, c.fwd_key), (True, c.bwd, c.bwd_key)):
+            assert key == Fn.PackCache._key(m.weight)
+            assert torch.equal(buf, Fn.pack_weight(m.weight, tr))
