@@ -332,14 +332,38 @@ constexpr unsigned OOB = 0x80000000u;
 constexpr int CONV_STAGES = 4;
 
 typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((ext_vector_type(4))) int rsrc_t;
 
-EE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* p, long bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)min(bytes, 0x7fffffffL), 0x00020000);
+// Raw buffer resource (V#) for byte range [p, p + bytes): bounds-checked, so an
+// offset >= bytes (OOB) reads zeros.  Built by hand so it can feed inline asm.
+EE_DEV rsrc_t make_rsrc(const void* p, long bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  rsrc_t r;
+  r.x = (int)(uint32_t)a;
+  r.y = (int)((a >> 32) & 0xffffu);  // stride 0
+  r.z = (int)min(bytes, 0x7fffffffL);
+  r.w = 0x00020000;
+  return r;
 }
 
+// One 16-B-per-lane LDS-DMA piece: lane l's 16 bytes from rsrc+voff land at
+// LDS byte (lds_dst + 16 l).  Issued by inline asm on purpose: the compiler's
+// waitcnt pass treats a builtin LDS-DMA as an LDS store that aliases every
+// later ds_read and inserts s_waitcnt vmcnt(0) in front of them, which drains
+// the whole ring every K-step.  Ordering is ours: counted waits + barrier
+// (wait_vmcnt_barrier) before a stage is read.
+EE_DEV void lds_dma16(rsrc_t rsrc, const void* lds_dst, unsigned voff) {
+  const int m0 = __builtin_amdgcn_readfirstlane((int)(uintptr_t)(lds_void_t*)lds_dst);
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(rsrc)
+               : "memory", "m0");
+}
+
+// all but this wave's N youngest LDS-DMA pieces landed, then the workgroup
+// barrier (every wave's pieces of the stage landed); one asm block so no LDS
+// read can be scheduled between the wait and the barrier
 template <int N>
-EE_DEV void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+EE_DEV void wait_vmcnt_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
 template <int MODE, int TCO, int TPIX>
@@ -413,8 +437,8 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a, long src_
     }
   }
   const int PH = a.IH >> a.up2, PW = a.IW >> a.up2;
-  const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, src_bytes);
-  const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(a.wp, w_bytes);
+  const rsrc_t rs_src = make_rsrc(a.src, src_bytes);
+  const rsrc_t rs_w = make_rsrc(a.wp, w_bytes);
 
   auto issue = [&](int kt, int buf) {
     const TapPos tp = tap_pos<MODE>(a, kt, kc, nc, TS, ntaps, r0, s0);
@@ -423,8 +447,7 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a, long src_
 #pragma unroll
       for (int i = 0; i < A_INS; ++i) {
         const unsigned off = (unsigned)(((co0 + i * 64 + rsub) * a.Kw + tp.kw) * 2);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_void_t*)(base + (i * 256 + wave * 64) * 8), 16, off, 0,
-                                                 0, 0);
+        lds_dma16(rs_w, base + (i * 256 + wave * 64) * 8, off);
       }
     }
     const int c = tp.c;
@@ -442,8 +465,7 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a, long src_
             off = (unsigned)((((b_n[i] * a.IH + oy) * a.IW + ox) * a.lds_src + c) * 2);
         }
       }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_src, (lds_void_t*)(base + TCO * BK + (i * 256 + wave * 64) * 8), 16,
-                                               off, 0, 0, 0);
+      lds_dma16(rs_src, base + TCO * BK + (i * 256 + wave * 64) * 8, off);
     }
   };
 
@@ -469,12 +491,11 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a, long src_
     if (st < nk) issue(kt0 + st, st);
   for (int it = 0; it < nk; ++it) {
     if (it + S - 2 < nk) {
-      if (a_wave) wait_vmcnt<(S - 2) * (A_INS + B_INS)>();
-      else wait_vmcnt<(S - 2) * B_INS>();
+      if (a_wave) wait_vmcnt_barrier<(S - 2) * (A_INS + B_INS)>();
+      else wait_vmcnt_barrier<(S - 2) * B_INS>();
     } else {
-      wait_vmcnt<0>();
+      wait_vmcnt_barrier<0>();
     }
-    __builtin_amdgcn_s_barrier();
     if (it + S - 1 < nk) issue(kt0 + it + S - 1, (it + S - 1) % S);
     const bf16_t* base = lds + (it % S) * STAGE;
     bf16x8_t fa[FI], fb[FJ];
@@ -757,8 +778,8 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_glds_kernel(WgradArgs w, lo
   const int hw = w.OH * w.OW;
   // waves that stage no dy chunk (TCO = 32) count fewer loads per K-step
   const bool d_wave = D_TOT >= 256 || tid < D_TOT;
-  const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(w.x, x_bytes);
-  const __amdgpu_buffer_rsrc_t rs_d = make_rsrc(w.dy, dy_bytes);
+  const rsrc_t rs_x = make_rsrc(w.x, x_bytes);
+  const rsrc_t rs_d = make_rsrc(w.dy, dy_bytes);
 
   // dy chunks: fixed pixel row / channel per thread
   int d_row[D_INS], d_co[D_INS];
@@ -796,8 +817,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_glds_kernel(WgradArgs w, lo
       for (int i = 0; i < D_INS; ++i) {
         const int p = pb + d_row[i];
         const unsigned off = (p < p_end && d_co[i] < w.Cout) ? (unsigned)(((long)p * w.lddy + d_co[i]) * 2) : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_d, (lds_void_t*)(base + (i * 256 + wave * 64) * 8), 16, off, 0,
-                                                 0, 0);
+        lds_dma16(rs_d, base + (i * 256 + wave * 64) * 8, off);
       }
     }
 #pragma unroll
@@ -808,8 +828,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_glds_kernel(WgradArgs w, lo
         if ((unsigned)iy < (unsigned)w.IH && (unsigned)ix < (unsigned)w.IW)
           off = (unsigned)(((((long)x_n[i] * PH + (iy >> w.up2)) * PW + (ix >> w.up2)) * w.ldx + x_c[i]) * 2);
       }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_x, (lds_void_t*)(base + BK * TCO + (i * 256 + wave * 64) * 8), 16,
-                                               off, 0, 0, 0);
+      lds_dma16(rs_x, base + BK * TCO + (i * 256 + wave * 64) * 8, off);
       // advance this row's pixel by one K-step
       x_ox[i] += BK;
       while (x_ox[i] >= w.OW) {
@@ -852,12 +871,11 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_glds_kernel(WgradArgs w, lo
     if (st < nk) issue(st, st);
   for (int it = 0; it < nk; ++it) {
     if (it + S - 2 < nk) {
-      if (d_wave) wait_vmcnt<(S - 2) * (D_INS + X_INS)>();
-      else wait_vmcnt<(S - 2) * X_INS>();
+      if (d_wave) wait_vmcnt_barrier<(S - 2) * (D_INS + X_INS)>();
+      else wait_vmcnt_barrier<(S - 2) * X_INS>();
     } else {
-      wait_vmcnt<0>();
+      wait_vmcnt_barrier<0>();
     }
-    __builtin_amdgcn_s_barrier();
     if (it + S - 1 < nk) issue(it + S - 1, (it + S - 1) % S);
     const bf16_t* base = lds + (it % S) * STAGE;
     bf16x8_t fa[FI], fb[FJ];
