@@ -324,7 +324,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 // STAGES-1 K-steps are in flight while one is multiplied, one raw s_barrier per
 // K-step, counted vmcnt waits (never 0 inside the steady state).  The LDS image
 // is lane-linear (64-B rows of 32 bf16), so the bank-conflict swizzle is
-// applied to the SOURCE chunk: LDS slot q of row r holds K-chunk q ^ ((r>>2)&3).
+// applied to the SOURCE chunk: LDS slot q of row r holds K-chunk
+// q ^ swz_b128((r>>2)&3).
 // Out-of-range taps / channels use an out-of-bounds buffer offset, which the
 // hardware bounds check turns into zeros.  Requires C % 8 == 0 (whole 16-B
 // chunks valid or invalid) and TCO >= 64.
@@ -332,6 +333,14 @@ constexpr unsigned OOB = 0x80000000u;
 constexpr int CONV_STAGES = 4;
 
 typedef __attribute__((address_space(3))) void lds_void_t;
+
+// XOR swizzle of the 16-B chunk of 64-B LDS rows read as MFMA fragments by
+// ds_read_b128 (lane l: row l & 15, chunk l >> 4).  gfx950 services a b128 read
+// in four 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, (+32): with the
+// row-block permutation 0,2,3,1 every group covers the 64 banks exactly once
+// (the plain (r>>2)&3 swizzle is 2-way conflicted in every group).
+EE_DEV int swz_b128(int b) { return (0x1320 >> (b * 4)) & 3; }
+
 typedef __attribute__((ext_vector_type(4))) int rsrc_t;
 
 // Raw buffer resource (V#) for byte range [p, p + bytes): bounds-checked, so an
@@ -414,7 +423,7 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a, long src_
 
   // this thread's 16-B chunk of every staged row: rows i*64 + tid/4, K-chunk swizzled
   const int rsub = tid >> 2;
-  const int kc = (tid & 3) ^ ((tid >> 4) & 3);
+  const int kc = (tid & 3) ^ swz_b128((tid >> 4) & 3);
   int b_n[B_INS], b_y[B_INS], b_x[B_INS];
   bool b_ok[B_INS];
 #pragma unroll
@@ -502,17 +511,199 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a, long src_
 #pragma unroll
     for (int i = 0; i < FI; ++i) {
       const int row = wi * WT_CO + i * 16 + fr;
-      fa[i] = as_frag(*reinterpret_cast<const uint4*>(base + row * BK + ((fq ^ ((row >> 2) & 3)) * 8)));
+      fa[i] = as_frag(*reinterpret_cast<const uint4*>(base + row * BK + ((fq ^ swz_b128((row >> 2) & 3)) * 8)));
     }
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
       const int row = wj * WT_PIX + j * 16 + fr;
-      uint4 v = *reinterpret_cast<const uint4*>(base + TCO * BK + row * BK + ((fq ^ ((row >> 2) & 3)) * 8));
+      uint4 v = *reinterpret_cast<const uint4*>(base + TCO * BK + row * BK + ((fq ^ swz_b128((row >> 2) & 3)) * 8));
       v.x &= bmask.x;
       v.y &= bmask.y;
       v.z &= bmask.z;
       v.w &= bmask.w;
       fb[j] = as_frag(v);
+    }
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+  }
+  igemm_epilogue<MODE, FI, FJ, WT_CO, WT_PIX>(a, acc, pix0, co0, wi, wj, lane, split, Pc, CH, CW, qy, qx, stc);
+}
+
+// ------------------------------- FWD / BWDD, pipelined kernel, hoisted gathers --
+// conv_glds_kernel with the per-K-step index arithmetic hoisted out of the loop
+// (the loop was issue-bound on integer address math: ~100 VALU per K-step,
+// several of them quarter-rate multiplies).  Each thread's B rows carry a byte
+// offset of the row's tap-(0,0) source pixel and a bitmask of the taps that land
+// inside the source image; a K-step is (tap, 32-channel slice), walked by
+// uniform counters, so a gather offset is base + uniform tap offset, selected
+// against the mask bit (3-5 VALU per 16-B piece).  Weight pieces use a constant
+// per-thread voffset and the K position as soffset.  Normal-mode operands only
+// (C % 8 == 0, C > 8), no fused upsample, <= 32 taps per parity class.
+EE_DEV void lds_dma16s(rsrc_t rsrc, int lds_addr, unsigned voff, int soff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(lds_addr), "v"(voff), "s"(rsrc),
+               "s"(soff)
+               : "memory", "m0");
+}
+
+template <int MODE, int TCO, int TPIX>
+__global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_bytes, long w_bytes) {
+  constexpr int S = CONV_STAGES;
+  constexpr int WCO = TCO >= 64 ? 2 : 1, WPIX = 4 / WCO;
+  constexpr int WT_CO = TCO / WCO, WT_PIX = TPIX / WPIX;
+  constexpr int FI = WT_CO / 16, FJ = WT_PIX / 16;
+  constexpr int A_TOT = TCO * 4, B_TOT = TPIX * 4;     // 16-B chunks per K-step
+  constexpr int A_INS = (A_TOT + 255) / 256, B_INS = B_TOT / 256;
+  constexpr int STAGE = (TCO + TPIX) * BK;             // bf16 elements per stage
+  static_assert(B_INS >= 1 && FI >= 1 && FJ >= 1, "tile");
+
+  __shared__ __attribute__((aligned(16))) bf16_t lds[S * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wi = wave / WPIX, wj = wave % WPIX;
+  const int cls = blockIdx.z % a.ncls, split = blockIdx.z / a.ncls;
+  const int co0 = blockIdx.y * TCO;
+  const bool a_wave = A_TOT >= 256 || tid < A_TOT;
+
+  int qy = 0, qx = 0, CH = a.OH, CW = a.OW, stc = 1;
+  int r0 = 0, s0 = 0, TR = a.R, TS = a.S, dqy = 0, dqx = 0;
+  if (MODE == MODE_BWDD) {
+    if (a.ncls > 1) {
+      qy = cls / a.st;
+      qx = cls - qy * a.st;
+      CH = (a.OH - qy + a.st - 1) / a.st;
+      CW = (a.OW - qx + a.st - 1) / a.st;
+      stc = a.st;
+    }
+    r0 = (qy + a.ph) % a.st;
+    s0 = (qx + a.pw) % a.st;
+    TR = r0 < a.R ? (a.R - r0 + a.st - 1) / a.st : 0;
+    TS = s0 < a.S ? (a.S - s0 + a.st - 1) / a.st : 0;
+    dqy = (qy + a.ph - r0) / a.st;
+    dqx = (qx + a.pw - s0) / a.st;
+  }
+  const int Pc = a.N * CH * CW;
+  const int pix0 = blockIdx.x * TPIX;
+  if (pix0 >= Pc) return;  // block-uniform
+  const int nc = a.Cgp / BK;
+  const int nk_all = TR * TS * nc;
+  const int kchunk = (nk_all + a.nsplit - 1) / a.nsplit;
+  const int kt0 = min(nk_all, split * kchunk), kt1 = min(nk_all, kt0 + kchunk);
+  const int nk = kt1 - kt0;
+
+  const int rsub = tid >> 2;
+  const int kc8 = ((tid & 3) ^ swz_b128((tid >> 4) & 3)) * 8;  // swizzled 8-channel chunk of this thread
+  const int ld2 = a.lds_src * 2;
+  int pb[B_INS];
+  unsigned vm[B_INS];
+#pragma unroll
+  for (int i = 0; i < B_INS; ++i) {
+    const int p = pix0 + i * 64 + rsub;
+    const bool ok = p < Pc;
+    const int pp = ok ? p : 0;
+    const int hw = CH * CW;
+    const int n = pp / hw;
+    const int rem = pp - n * hw;
+    const int yy = rem / CW;
+    const int xx = rem - yy * CW;
+    int y0, x0;
+    if (MODE == MODE_FWD) {
+      y0 = yy * a.st - a.ph;
+      x0 = xx * a.st - a.pw;
+    } else {
+      y0 = yy + dqy;
+      x0 = xx + dqx;
+    }
+    unsigned m = 0;
+    for (int ta = 0; ta < TR; ++ta) {
+      const int iy = MODE == MODE_FWD ? y0 + ta : y0 - ta;
+      if ((unsigned)iy >= (unsigned)a.IH) continue;
+      for (int tb = 0; tb < TS; ++tb) {
+        const int ix = MODE == MODE_FWD ? x0 + tb : x0 - tb;
+        if ((unsigned)ix < (unsigned)a.IW) m |= 1u << (ta * TS + tb);
+      }
+    }
+    vm[i] = ok ? m : 0u;
+    pb[i] = ((n * a.IH + y0) * a.IW + x0) * ld2 + kc8 * 2;
+  }
+  unsigned aoff[A_INS];
+#pragma unroll
+  for (int i = 0; i < A_INS; ++i) aoff[i] = (unsigned)(((co0 + i * 64 + rsub) * a.Kw + kc8) * 2);
+
+  const rsrc_t rs_src = make_rsrc(a.src, src_bytes);
+  const rsrc_t rs_w = make_rsrc(a.wp, w_bytes);
+  const int lds0 = (int)(uintptr_t)(lds_void_t*)lds;
+
+  // uniform K-step walker: tap (ta, tb), 32-channel slice cs
+  int w_t = nc > 0 ? kt0 / nc : 0;
+  int w_cs = kt0 - w_t * nc;
+  int w_ta = TS > 0 ? w_t / TS : 0;
+  int w_tb = w_t - w_ta * TS;
+  const int IW = a.IW;
+  auto issue = [&](int buf) {
+    const int t = w_ta * TS + w_tb;
+    const int c = w_cs * BK;
+    int toff, kw;
+    if (MODE == MODE_FWD) {
+      toff = (w_ta * IW + w_tb) * ld2 + c * 2;
+      kw = (w_ta * a.S + w_tb) * a.Cgp + c;
+    } else {
+      toff = c * 2 - (w_ta * IW + w_tb) * ld2;
+      kw = ((r0 + a.st * w_ta) * a.S + s0 + a.st * w_tb) * a.Cgp + c;
+    }
+    const int cv = a.Cvalid - c;  // chunk valid iff kc8 < cv
+    const int base = lds0 + buf * (STAGE * 2);
+    if (a_wave) {
+#pragma unroll
+      for (int i = 0; i < A_INS; ++i) lds_dma16s(rs_w, base + (i * 256 + wave * 64) * 16, aoff[i], kw * 2);
+    }
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i) {
+      const bool ok = ((vm[i] >> t) & 1u) && kc8 < cv;
+      const unsigned off = ok ? (unsigned)(pb[i] + toff) : OOB;
+      lds_dma16s(rs_src, base + TCO * BK * 2 + (i * 256 + wave * 64) * 16, off, 0);
+    }
+    if (++w_cs == nc) {
+      w_cs = 0;
+      if (++w_tb == TS) {
+        w_tb = 0;
+        ++w_ta;
+      }
+    }
+  };
+
+  f32x4_t acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int st = 0; st < S - 1; ++st)
+    if (st < nk) issue(st);
+  for (int it = 0; it < nk; ++it) {
+    if (it + S - 2 < nk) {
+      if (a_wave) wait_vmcnt_barrier<(S - 2) * (A_INS + B_INS)>();
+      else wait_vmcnt_barrier<(S - 2) * B_INS>();
+    } else {
+      wait_vmcnt_barrier<0>();
+    }
+    if (it + S - 1 < nk) issue((it + S - 1) % S);
+    const bf16_t* base = lds + (it % S) * STAGE;
+    bf16x8_t fa[FI], fb[FJ];
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const int row = wi * WT_CO + i * 16 + fr;
+      fa[i] = as_frag(*reinterpret_cast<const uint4*>(base + row * BK + ((fq ^ swz_b128((row >> 2) & 3)) * 8)));
+    }
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const int row = wj * WT_PIX + j * 16 + fr;
+      fb[j] = as_frag(*reinterpret_cast<const uint4*>(base + TCO * BK + row * BK + ((fq ^ swz_b128((row >> 2) & 3)) * 8)));
     }
 #pragma unroll
     for (int i = 0; i < FI; ++i)
@@ -553,14 +744,16 @@ struct WgradArgs {
   int accumulate;
 };
 
-// split-slab column (co, (tap, c)) -> torch layout [Cout][Cin][R][S]; padded channels dropped
+// split-slab column (co, (tap, c)) -> channels-last weight layout [Cout][R][S][Cin]
+// (unit stride along c, so a fragment row's 16 lanes store 64 contiguous bytes);
+// padded channels dropped
 struct WgradMap {
   int K, Cg, Cin, RS;
   EE_DEV long operator()(long col) const {  // col < Cout*K < 2^31
     const int ci = (int)col;
     const int co = ci / K, k = ci - co * K;
     const int tap = k / Cg, c = k - tap * Cg;
-    return c < Cin ? ((long)co * Cin + c) * RS + tap : -1;
+    return c < Cin ? ((long)co * RS + tap) * Cin + c : -1;
   }
 };
 
@@ -893,35 +1086,40 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_glds_kernel(WgradArgs w, lo
 }
 
 // ------------------------------------------------------- weight packing --
-// FWD pack:  out[co][(r*S+s)*Cgp + c] = W[co][c][r][s] * scale[co]   (zero padded)
-// BWDD pack: out[ci][(r*S+s)*Cgp + co] = W[co][ci][r][s] * scale[co]
+// fp32 conv weights live channels-last, W[Cout][R][S][Cin] (torch's
+// channels_last memory format of the (Cout, Cin, R, S) parameter), so the
+// forward image is a padded copy of each row and the weight gradient is
+// written with unit stride along Cin.
+// FWD pack:  out[co][(r*S+s)*Cgp + c] = W[co][r][s][c] * scale[co]   (zero padded)
+// BWDD pack: out[ci][(r*S+s)*Cgp + co] = W[co][r][s][ci] * scale[co]
 __global__ void pack_weights_kernel(const float* w, const float* scale, int Cout, int Cin, int R, int S,
                                     int transposed, int Cgp, int rows_pad, int Kw, bf16_t* out) {
   const long total = (long)rows_pad * Kw;
+  const int RS = R * S;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const int row = e / Kw, k = e % Kw;
     const int rs = k / Cgp, c = k - rs * Cgp;
-    const int r = rs / S, s = rs - r * S;
     float v = 0.f;
-    if (rs >= R * S) {
+    if (rs >= RS) {
       // zero columns padding the row to whole 32-deep K steps
     } else if (!transposed) {
-      if (row < Cout && c < Cin) v = w[(((long)row * Cin + c) * R + r) * S + s] * (scale ? scale[row] : 1.f);
+      if (row < Cout && c < Cin) v = w[((long)row * RS + rs) * Cin + c] * (scale ? scale[row] : 1.f);
     } else {
-      if (row < Cin && c < Cout) v = w[(((long)c * Cin + row) * R + r) * S + s] * (scale ? scale[c] : 1.f);
+      if (row < Cin && c < Cout) v = w[((long)c * RS + rs) * Cin + row] * (scale ? scale[c] : 1.f);
     }
     out[e] = f2bf(v);
   }
 }
 
 // Batched re-pack after an optimizer step: one launch for every conv weight of a
-// model (fwd and bwd-data images), staged through LDS so both the fp32 reads
-// and the bf16 writes are contiguous.  `table` (device, int64): njobs rows of
+// model (fwd and bwd-data images).  `table` (device, int64): njobs rows of
 // {w, scale, out, Cout, Cin, R, S, transposed}, then njobs+1 prefix offsets of
 // BLOCKS per job (pack_multi_blocks).  Forward image: one block per output row
-// (w[co] is one contiguous Cin*R*S run); bwd-data image: one block per 8 input
-// channels, streaming the output channels in chunks of 128.
-constexpr int PK_LDS = 9344;   // floats of staging (128 x 73)
+// (w[co] is already the row's (tap, c) order: a padded, coalesced copy);
+// bwd-data image: one block per 8 input channels x a chunk of output channels,
+// transposed through LDS so both the fp32 reads (8-channel runs) and the bf16
+// row writes are contiguous.
+constexpr int PK_LDS = 9344;   // floats of staging
 
 EE_HOST_DEV_INLINE int pk_cgp(int C) { return C <= 8 ? 8 : (C + BK - 1) / BK * BK; }
 // output channels per bwd-image block: 8 input channels x RS taps x CO fit the staging
@@ -944,7 +1142,7 @@ __global__ __launch_bounds__(256) void pack_weights_multi_kernel(const long* __r
   const int Cout = (int)j[3], Cin = (int)j[4], RS = (int)(j[5] * j[6]), tr = (int)j[7];
   const int t = threadIdx.x;
   if (!tr) {
-    // ---- forward image: row co = lb, out[co][tap*Cgp + c] = w[co][c][tap]
+    // ---- forward image: row co = lb, out[co][tap*Cgp + c] = w[co][tap][c]
     const int Cgp = pk_cgp(Cin), Kw = (RS * Cgp + BK - 1) / BK * BK;
     bf16_t* orow = out + (long)lb * Kw;
     if (lb >= Cout) {
@@ -952,43 +1150,14 @@ __global__ __launch_bounds__(256) void pack_weights_multi_kernel(const long* __r
       return;
     }
     const float sc = scale ? scale[lb] : 1.f;
-    const int RSP = RS | 1;  // odd LDS row stride: conflict-free column reads
-    const int cc = max(1, PK_LDS / RSP);
-    for (int c0 = 0; c0 < Cin; c0 += cc) {
-      const int nc = min(cc, Cin - c0);
-      __syncthreads();
-      // 8 independent loads in flight per thread before their LDS stores
-      const float* src = w + ((long)lb * Cin + c0) * RS;
-      for (int e0 = t; e0 < nc * RS; e0 += 256 * 8) {
-        float v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int e = e0 + u * 256;
-          v[u] = e < nc * RS ? src[e] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int e = e0 + u * 256;
-          if (e < nc * RS) {
-            const int c = e / RS, tap = e - c * RS;
-            buf[c * RSP + tap] = v[u];
-          }
-        }
-      }
-      __syncthreads();
-      for (int e = t; e < nc * RS; e += 256) {
-        const int tap = e / nc, c = e - tap * nc;
-        orow[tap * Cgp + c0 + c] = f2bf(buf[c * RSP + tap] * sc);
-      }
+    const float* src = w + (long)lb * RS * Cin;
+    for (int k = t; k < Kw; k += 256) {
+      const int tap = k / Cgp, c = k - tap * Cgp;
+      orow[k] = f2bf(tap < RS && c < Cin ? src[tap * Cin + c] * sc : 0.f);
     }
-    for (int e = t; e < RS * (Cgp - Cin); e += 256) {  // channel padding of every tap
-      const int tap = e / (Cgp - Cin), c = Cin + e - tap * (Cgp - Cin);
-      orow[tap * Cgp + c] = 0;
-    }
-    for (int k = RS * Cgp + t; k < Kw; k += 256) orow[k] = 0;
   } else {
     // ---- bwd-data image: rows ci0..ci0+7 x one chunk of CO output channels,
-    // out[ci][tap*Cgp + co] = w[co][ci][tap]
+    // out[ci][tap*Cgp + co] = w[co][tap][ci]
     constexpr int TI = 8;
     const int Cgp = pk_cgp(Cout), Kw = (RS * Cgp + BK - 1) / BK * BK;
     const int RW = TI * RS + 1;  // odd LDS row stride
@@ -998,7 +1167,7 @@ __global__ __launch_bounds__(256) void pack_weights_multi_kernel(const long* __r
     const int ni = max(0, min(TI, Cin - ci0));
     {
       const int nco = min(CO, Cout - co0);  // may be <= 0 in the channel padding
-      const int nload = max(nco, 0) * ni * RS;
+      const int nload = max(nco, 0) * RS * ni;
       for (int e0 = t; e0 < nload; e0 += 256 * 8) {
         float v[8];
 #pragma unroll
@@ -1006,16 +1175,18 @@ __global__ __launch_bounds__(256) void pack_weights_multi_kernel(const long* __r
           const int e = e0 + u * 256;
           v[u] = 0.f;
           if (e < nload) {
-            const int co = e / (ni * RS), q = e - co * (ni * RS);
-            v[u] = w[((long)(co0 + co) * Cin + ci0) * RS + q] * (scale ? scale[co0 + co] : 1.f);
+            const int co = e / (RS * ni), q = e - co * (RS * ni);
+            const int tap = q / ni, i = q - tap * ni;
+            v[u] = w[((long)(co0 + co) * RS + tap) * Cin + ci0 + i] * (scale ? scale[co0 + co] : 1.f);
           }
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int e = e0 + u * 256;
           if (e < nload) {
-            const int co = e / (ni * RS), q = e - co * (ni * RS);
-            buf[co * RW + q] = v[u];
+            const int co = e / (RS * ni), q = e - co * (RS * ni);
+            const int tap = q / ni, i = q - tap * ni;
+            buf[co * RW + i * RS + tap] = v[u];
           }
         }
       }
@@ -1087,9 +1258,19 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   dim3 grid(ee_cdiv(Pc_max, p.tpix), ee_cdiv(a.Mrows, p.tco), a.ncls * p.nsplit);
   const long w_bytes = (long)ee_round_up(a.Mrows, 128) * a.Kw * 2;
 #define GL(TC, TP) ee_launch(conv_glds_kernel<MODE, TC, TP>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
+#define FA(TC, TP) ee_launch(conv_fast_kernel<MODE, TC, TP>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
 #define IG(TC, TP, WC) ee_launch(conv_igemm_kernel<MODE, TC, TP, WC>, grid, dim3(256), 0, s, a)
   const bool glds = ((a.Cvalid % 8) == 0 || a.Cgp == 8) && src_bytes < 0x7fffffffL && w_bytes < 0x7fffffffL;
-  if (glds) {
+  int tr_ = a.R, ts_ = a.S;
+  if (MODE == MODE_BWDD && a.st > 1) tr_ = ee_cdiv(a.R, a.st), ts_ = ee_cdiv(a.S, a.st);
+  const bool fast = glds && a.Cgp % BK == 0 && !a.up2 && tr_ * ts_ <= 32 && env_int("EEGAN_CONV_FAST", 1);
+  if (fast) {
+    if (p.tco == 128) { if (p.tpix == 128) FA(128, 128); else FA(128, 64); }
+    else if (p.tco == 64) { if (p.tpix == 128) FA(64, 128); else FA(64, 64); }
+    else if (p.tco == 32) { if (p.tpix == 256) FA(32, 256); else FA(32, 64); }
+    else { if (p.tpix == 256) FA(16, 256); else FA(16, 64); }
+  }
+  else if (glds) {
     if (p.tco == 128) { if (p.tpix == 128) GL(128, 128); else GL(128, 64); }
     else if (p.tco == 64) { if (p.tpix == 128) GL(64, 128); else GL(64, 64); }
     else if (p.tco == 32) { if (p.tpix == 256) GL(32, 256); else GL(32, 64); }
@@ -1101,6 +1282,7 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   else { if (p.tpix == 256) IG(16, 256, 1); else IG(16, 64, 1); }
 #undef IG
 #undef GL
+#undef FA
   int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd" : "conv_bwd_data");
   if (rc || p.nsplit == 1) return rc;
   const long total = (long)a.P * a.Mrows;

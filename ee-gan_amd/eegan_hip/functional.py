@@ -16,7 +16,7 @@ import torch
 
 from . import tensor as T
 from ._lib import ops, ConvDesc, BnModDesc, ACT_CODES
-from .tensor import BF16, F32, empty_nhwc, ld_of, ptr, stream, to_nhwc_bf16, workspace
+from .tensor import BF16, F32, CL, empty_nhwc, ld_of, ptr, stream, to_nhwc_bf16, workspace
 
 # In autograd.grad() mode the engine cannot report whether a leaf is needed;
 # parameters are then assumed NOT requested (the gradient penalty asks only
@@ -59,7 +59,7 @@ def _grad_sink(ctx, i):
     if var is None:
         return None
     g = var.grad
-    if g is None or g.dtype != F32 or not g.is_contiguous() or g.shape != var.shape:
+    if g is None or g.dtype != F32 or g.shape != var.shape or g.stride() != var.stride():
         return None
     return g
 
@@ -102,8 +102,8 @@ def pack_weight(W, transposed, scale=None, out=None):
     if out is None or out.numel() != n or out.device != W.device:
         out = torch.empty(n, dtype=BF16, device=W.device)
     Wc = W.detach()
-    if not Wc.is_contiguous() or Wc.dtype != F32:
-        Wc = Wc.float().contiguous()
+    if Wc.dtype != F32 or not Wc.is_contiguous(memory_format=CL):
+        Wc = Wc.float().contiguous(memory_format=CL)
     ops.conv_pack_weights(Wc.data_ptr(), ptr(scale), Cout, Cin, R, S, int(transposed), out.data_ptr(), stream())
     return out
 
@@ -257,11 +257,13 @@ def conv_bwd_data_raw(dz, W, g, x_shape, cache=None):
 
 
 def conv_bwd_weight_raw(x, dz, g, W_shape, out=None):
-    """dW (fresh tensor), or accumulated into `out` when given."""
+    """dW (fresh channels-last fp32 tensor), or accumulated into `out` when given."""
     x = to_nhwc_bf16(x)
     d = _desc_io(g, x.shape, ld_of(x), ld_of(dz))
     ws = workspace(ops.conv_wgrad_workspace(d), x.device)
-    dW = torch.empty(W_shape, dtype=F32, device=x.device) if out is None else out
+    if out is not None and not out.is_contiguous(memory_format=CL):
+        raise ValueError('conv_bwd_weight: dW accumulates into channels-last fp32 storage')
+    dW = torch.empty(W_shape, dtype=F32, device=x.device, memory_format=CL) if out is None else out
     N, C, H, Wd = x.shape
     flops = 2.0 * N * d.Ho * d.Wo * g.K * C * g.R * g.S
     nbytes = 2.0 * (N * H * Wd * C + N * d.Ho * d.Wo * g.K) + 4.0 * g.K * C * g.R * g.S
@@ -322,7 +324,7 @@ class Conv2dFn(torch.autograd.Function):
                 dx = ConvBwdDataFn.apply(dz, W, g, ctx.x_shape, ctx.cache)
         if _needed(ctx, 1):
             sink = _grad_sink(ctx, 1)
-            if sink is not None:
+            if sink is not None and sink.is_contiguous(memory_format=CL):
                 conv_bwd_weight_raw(x, dz, g, W.shape, out=sink)
             else:
                 dW = ConvBwdWeightFn.apply(x, dz, g) if not g.up2 else conv_bwd_weight_raw(x, dz, g, W.shape)

@@ -17,7 +17,7 @@ def _pair(v):
 
 
 class Conv2d(nn.Module):
-    """nn.Conv2d-compatible (weight [Cout,Cin,kh,kw], optional bias).
+    """nn.Conv2d-compatible (weight (Cout,Cin,kh,kw) stored channels-last, optional bias).
     forward(x, act=None, slope=0.2, out_f32=False, up2=False): the activation
     is fused into the epilogue and up2 reads x through a nearest-2x upsample."""
 
@@ -27,7 +27,10 @@ class Conv2d(nn.Module):
         self.kernel_size = _pair(kernel_size)
         self.stride = stride if isinstance(stride, int) else stride[0]
         self.padding = _pair(padding)
-        self.weight = nn.Parameter(torch.empty(out_channels, in_channels, *self.kernel_size))
+        # channels-last storage ([Cout][kh][kw][Cin], torch.channels_last): the layout
+        # the kernels pack from and write weight gradients into with unit stride
+        self.weight = nn.Parameter(torch.empty(out_channels, in_channels, *self.kernel_size).contiguous(
+            memory_format=torch.channels_last))
         self.bias = nn.Parameter(torch.empty(out_channels)) if bias else None
         self.reset_parameters()
         self._cache = Fn.PackCache()

@@ -48,9 +48,11 @@ class FlatAdam(torch.optim.Optimizer):
         with torch.no_grad():
             for p, o in zip(uniq, offs):
                 k = p.numel()
-                self.flat[o:o + k].copy_(p.detach().reshape(-1).float())
-                p.data = self.flat[o:o + k].view_as(p)
-                g = self.gflat[o:o + k].view_as(p)
+                # views keep each parameter's strides (conv weights are channels-last)
+                pv = self.flat[o:o + k].as_strided(p.shape, p.stride())
+                pv.copy_(p.detach())
+                p.data = pv
+                g = self.gflat[o:o + k].as_strided(p.shape, p.stride())
                 p.grad = g
                 p._eegan_gen = self._gen
                 self._views.append((p, o, k, g))
@@ -108,6 +110,8 @@ class FlatAdam(torch.optim.Optimizer):
             c = getattr(p, '_eegan_packcache', None)
             if c is None or p.dim() != 4 or c.scale is not None:
                 continue
+            if not p.is_contiguous(memory_format=torch.channels_last):
+                raise RuntimeError('FlatAdam: conv weight %s is not stored channels-last' % (tuple(p.shape),))
             for tr, buf in ((False, c.fwd), (True, c.bwd)):
                 if buf is not None:
                     jobs.append((p, c, tr, buf))

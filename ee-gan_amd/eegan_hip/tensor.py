@@ -12,6 +12,7 @@ from ._lib import ops
 
 BF16 = torch.bfloat16
 F32 = torch.float32
+CL = torch.channels_last  # fp32 conv weights: (Cout, Cin, R, S) stored [Cout][R][S][Cin]
 
 
 def ld_for(C, dtype=BF16):

@@ -59,7 +59,8 @@ typedef struct eegan_conv_desc {
 
 /* elements of the packed bf16 weight image (rows padded to 128, each tap's channel run to 32) */
 long eegan_conv_packed_elems(int Cout, int Cin, int R, int S, int transposed);
-/* torch layout W[Cout][Cin][R][S] fp32 (x optional per-Cout scale) -> packed bf16.
+/* fp32 conv weights are channels-last: W[Cout][R][S][Cin] (torch.channels_last storage of the
+ * (Cout, Cin, R, S) nn.Conv2d weight).  W (x optional per-Cout scale) -> packed bf16.
  * transposed=0: forward image [Cout][R][S][Cin_32]; 1: bwd-data image [Cin][R][S][Cout_32] */
 int eegan_conv_pack_weights(const float* w, const float* scale, int Cout, int Cin, int R, int S,
                             int transposed, uint16_t* out, hipStream_t stream);
@@ -82,7 +83,7 @@ int eegan_conv_fwd(const eegan_conv_desc* d, const uint16_t* x, const uint16_t* 
  * s*s parity classes that visit only their valid taps */
 int eegan_conv_bwd_data(const eegan_conv_desc* d, const uint16_t* dy, const uint16_t* wpackT, void* dx,
                         int lddx, int dx_f32, float* ws, hipStream_t stream);
-/* dW[Cout][Cin][R][S] (fp32, torch layout) = sum_pixels dy x im2col(x); split-K slabs in ws */
+/* dW[Cout][R][S][Cin] (fp32, channels-last like W) = sum_pixels dy x im2col(x); split-K slabs in ws */
 long eegan_conv_wgrad_workspace(const eegan_conv_desc* d);
 int eegan_conv_bwd_weight(const eegan_conv_desc* d, const uint16_t* x, const uint16_t* dy, float* ws, float* dw,
                           int accumulate, hipStream_t stream);

@@ -54,7 +54,31 @@ CONV_CASES = [
     # many pixel splits of the weight gradient; odd widths (pixel walk wraps rows mid-step)
     (8, 32, 64, 64, 32, 3, 1, 1, True, None, False),
     (2, 32, 37, 23, 64, 4, 2, 1, False, 'lrelu', False),
+    # small grids: split-K forward / backward-data with the hoisted-gather kernel
+    (2, 256, 4, 4, 192, 3, 1, 1, True, 'lrelu', False),
+    (2, 96, 6, 10, 64, 4, 2, 1, False, None, False),
 ]
+
+
+def test_conv_fast_path_matches_generic(gpu, monkeypatch):
+    """The hoisted-gather kernel (EEGAN_CONV_FAST=1, default) sums the same
+    products in the same order as the generic pipelined kernel: bit-identical."""
+    Fn, T, _ = _mods()
+    for N, Cin, H, W, Cout, k, st, pad in [(2, 64, 12, 20, 96, 3, 1, 1), (2, 48, 16, 16, 32, 4, 2, 1),
+                                            (2, 256, 4, 4, 128, 3, 1, 1)]:
+        torch.manual_seed(N * Cin + H)
+        g = Fn.Geom(Cout, k, k, st, pad, pad, 0)
+        x = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        Wt = (torch.randn(Cout, Cin, k, k) * 0.05).to(gpu)
+        Ho, Wo = g.out_hw(H, W)
+        dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
+        outs = []
+        for fast in ('0', '1'):
+            monkeypatch.setenv('EEGAN_CONV_FAST', fast)
+            outs.append((Fn.conv_fwd_raw(x, Wt, None, g).float().cpu(),
+                         Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape)).float().cpu()))
+        assert torch.equal(outs[0][0], outs[1][0])
+        assert torch.equal(outs[0][1], outs[1][1])
 
 
 @pytest.mark.parametrize('case', CONV_CASES, ids=[str(i) for i in range(len(CONV_CASES))])

@@ -1,0 +1,81 @@
+#!/usr/bin/env python
+"""Standalone conv micro-benchmark: time forward / backward-data / weight-
+gradient launches of chosen bench shapes (HIP events, many back-to-back
+launches), so kernel changes can be measured shape by shape.
+
+    python tools/conv_bench.py [--shapes all|NAME,...] [--iters 50] [--dirs fwd,bwdd,wgrad]
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, 'ee-gan_amd'))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+# name: (N, C, H, W, K, R, stride, pad)
+SHAPES = {
+    'c3x3_64_128': (16, 64, 128, 128, 64, 3, 1, 1),
+    'c3x3_128_64': (16, 128, 64, 64, 128, 3, 1, 1),
+    'c3x3_256_32': (16, 256, 32, 32, 256, 3, 1, 1),
+    'c3x3_512_16': (16, 512, 16, 16, 512, 3, 1, 1),
+    'c3x3_32_256': (16, 32, 256, 256, 32, 3, 1, 1),
+    'c4x4s2_32_256': (16, 32, 256, 256, 64, 4, 2, 1),
+    'c4x4s2_128_64': (16, 128, 64, 64, 256, 4, 2, 1),
+    'c3x3_768_4': (16, 768, 4, 4, 1024, 3, 1, 1),
+    'c3x3_512_4': (16, 512, 4, 4, 512, 3, 1, 1),
+    'c4x4s4_1024_4': (16, 1024, 4, 4, 1024, 4, 4, 0),
+    'c3x3_256_8': (16, 256, 8, 8, 256, 3, 1, 1),
+    'c1x1_32_256': (16, 32, 256, 256, 64, 1, 1, 0),
+    'c3x3_3_256': (16, 3, 256, 256, 32, 3, 1, 1),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--shapes', default='all')
+    ap.add_argument('--dirs', default='fwd,bwdd,wgrad')
+    ap.add_argument('--iters', type=int, default=50)
+    args = ap.parse_args()
+    from eegan_hip import functional as Fn
+    from eegan_hip.tensor import empty_nhwc
+    dev = torch.device('cuda', 0)
+    names = list(SHAPES) if args.shapes == 'all' else args.shapes.split(',')
+    dirs = args.dirs.split(',')
+    torch.manual_seed(0)
+    for name in names:
+        N, C, H, W, K, R, st, pd = SHAPES[name]
+        g = Fn.Geom(K, R, R, st, pd, pd, 0)
+        Ho, Wo = g.out_hw(H, W)
+        x = empty_nhwc(N, C, H, W, dev)
+        x.copy_(torch.randn(N, C, H, W, device=dev))
+        dz = empty_nhwc(N, K, Ho, Wo, dev)
+        dz.copy_(torch.randn(N, K, Ho, Wo, device=dev))
+        Wt = (torch.randn(K, C, R, R, device=dev) * 0.05)
+        dW = torch.zeros_like(Wt).contiguous(memory_format=torch.channels_last)
+        cache = Fn.PackCache()
+        flops = 2.0 * N * Ho * Wo * K * C * R * R
+        fns = {
+            'fwd': lambda: Fn.conv_fwd_raw(x, Wt, None, g, cache=cache),
+            'bwdd': lambda: Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), cache=cache),
+            'wgrad': lambda: Fn.conv_bwd_weight_raw(x, dz, g, Wt.shape, out=dW),
+        }
+        for dname in dirs:
+            fn = fns[dname]
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / args.iters
+            print('%-16s %-6s %9.2f us %8.1f TF/s' % (name, dname, us, flops / us / 1e6), flush=True)
+
+
+if __name__ == '__main__':
+    main()
