@@ -1085,6 +1085,148 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_glds_kernel(WgradArgs w, lo
   wgrad_epilogue<FI, FJ, WT_CO, WT_K>(w, acc, co0, kb0, wi, wj, lane);
 }
 
+// Weight gradient with the per-K-step index math hoisted (cf. conv_fast_kernel):
+// power-of-two output grids, no fused upsample.  A K-step is 32 consecutive
+// pixels starting at a multiple of 32, so with OW and OH*OW powers of two each
+// thread's pixel is (n0 + dn, oy0 + dy, ox0 + dx) with (dn, dy, dx) fixed per
+// thread and (n0, oy0, ox0) uniform shifts of the step's first pixel: a gather
+// offset is a per-thread constant plus a uniform term, its bounds test two
+// compares against uniform-shifted constants.  Rows past the split end read dy
+// as zeros (their x rows are finite activations, so the products vanish).
+template <int TCO, int TK>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_fast_kernel(WgradArgs w, long x_bytes, long dy_bytes, int lw,
+                                                                 int lhw) {
+  constexpr int S = CONV_STAGES;
+  constexpr int WCO = TCO >= 64 ? 2 : 1, WKK = 4 / WCO;
+  constexpr int WT_CO = TCO / WCO, WT_K = TK / WKK;
+  constexpr int FI = WT_CO / 16, FJ = WT_K / 16;
+  constexpr int DCH = TCO / 8, XCH = TK / 8;           // 16-B chunks per pixel row
+  constexpr int D_TOT = BK * DCH, X_TOT = BK * XCH;    // chunks per K-step
+  constexpr int D_INS = (D_TOT + 255) / 256, X_INS = X_TOT / 256;
+  constexpr int STAGE = BK * (TCO + TK);
+  static_assert(X_INS >= 1 && FI >= 1 && FJ >= 1, "tile");
+
+  __shared__ __attribute__((aligned(16))) bf16_t lds[S * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wi = wave / WKK, wj = wave % WKK;
+  const int co0 = blockIdx.y * TCO, kb0 = blockIdx.x * TK;
+  const int p_begin = blockIdx.z * w.p_per_split;
+  const int p_end = min(w.P, p_begin + w.p_per_split);
+  const int nk = p_begin < p_end ? (p_end - p_begin + BK - 1) / BK : 0;
+  const bool d_wave = D_TOT >= 256 || tid < D_TOT;
+  const rsrc_t rs_x = make_rsrc(w.x, x_bytes);
+  const rsrc_t rs_d = make_rsrc(w.dy, dy_bytes);
+  const int lds0 = (int)(uintptr_t)(lds_void_t*)lds;
+
+  // dy chunks: pixel row d_row of the step, channel d_co
+  int d_row[D_INS];
+  unsigned d_off[D_INS];
+#pragma unroll
+  for (int i = 0; i < D_INS; ++i) {
+    const int idx = i * 256 + tid;
+    d_row[i] = idx / DCH;
+    const int co = co0 + (((idx % DCH) ^ tr_swz<DCH>(d_row[i])) * 8);
+    d_off[i] = co < w.Cout ? (unsigned)((d_row[i] * w.lddy + co) * 2) : OOB;
+    if (co >= w.Cout) d_row[i] = BK;  // never valid
+  }
+  // x chunks: fixed (tap, channel), pixel = step start + (dn, dy, dx)
+  int x_q[X_INS], x_cy[X_INS], x_cx[X_INS];
+  bool x_kok[X_INS];
+  const int OW = w.OW, HW = w.OH * w.OW;
+#pragma unroll
+  for (int i = 0; i < X_INS; ++i) {
+    const int idx = i * 256 + tid;
+    const int row = idx / XCH;
+    const int k = kb0 + (((idx % XCH) ^ tr_swz<XCH>(row)) * 8);
+    x_kok[i] = k < w.K;
+    const int tap = k / w.Cg, c = k - tap * w.Cg;
+    const int r = tap / w.S, s = tap - r * w.S;
+    x_kok[i] = x_kok[i] && c < w.Cin;
+    // decomposition of `row` relative to a 32-aligned step start
+    const int dn = HW < BK ? row >> lhw : 0;
+    const int rr = HW < BK ? row & (HW - 1) : row;
+    const int dy = OW < BK ? rr >> lw : 0;
+    const int dx = OW < BK ? rr & (OW - 1) : rr;
+    x_cy[i] = dy * w.st - w.ph + r;
+    x_cx[i] = dx * w.st - w.pw + s;
+    x_q[i] = ((dn * w.IH + x_cy[i]) * w.IW + x_cx[i]) * w.ldx + c;
+  }
+
+  auto issue = [&](int step, int buf) {
+    const int p0 = p_begin + step * BK;
+    const int base = lds0 + buf * (STAGE * 2);
+    const int drem = p_end - p0;
+    if (d_wave) {
+#pragma unroll
+      for (int i = 0; i < D_INS; ++i) {
+        const unsigned off = d_row[i] < drem ? d_off[i] : OOB;
+        lds_dma16s(rs_d, base + (i * 256 + wave * 64) * 16, off, p0 * w.lddy * 2);
+      }
+    }
+    const int n0 = p0 >> lhw, rem = p0 & (HW - 1);
+    const int uy = (rem >> lw) * w.st, ux = (rem & (OW - 1)) * w.st;
+    const int ubase = ((n0 * w.IH + uy) * w.IW + ux) * w.ldx;
+#pragma unroll
+    for (int i = 0; i < X_INS; ++i) {
+      const bool ok = x_kok[i] && (unsigned)(uy + x_cy[i]) < (unsigned)w.IH &&
+                      (unsigned)(ux + x_cx[i]) < (unsigned)w.IW;
+      const unsigned off = ok ? (unsigned)((ubase + x_q[i]) * 2) : OOB;
+      lds_dma16s(rs_x, base + BK * TCO * 2 + (i * 256 + wave * 64) * 16, off, 0);
+    }
+  };
+
+  f32x4_t acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pq = li & 3;
+  typedef __attribute__((address_space(3))) s16x4_t lds_s4;
+  auto tr_frag = [&](const bf16_t* img, int nch_shift, int col, auto swz) -> bf16x8_t {
+    const int ch = (col >> 3) + (pq >> 1);
+    const int r0 = 8 * g + q, r1 = r0 + 4;
+    const bf16_t* p0 = img + (r0 << nch_shift) * 8 + ((ch ^ swz(r0)) * 8) + 4 * (pq & 1);
+    const bf16_t* p1 = img + (r1 << nch_shift) * 8 + ((ch ^ swz(r1)) * 8) + 4 * (pq & 1);
+    s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(p0));
+    s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(p1));
+    typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+    s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  };
+  constexpr int DSH = DCH == 16 ? 4 : DCH == 8 ? 3 : 2;
+  constexpr int XSH = XCH == 16 ? 4 : 3;
+  auto dswz = [](int r) { return tr_swz<DCH>(r); };
+  auto xswz = [](int r) { return tr_swz<XCH>(r); };
+
+#pragma unroll
+  for (int st = 0; st < S - 1; ++st)
+    if (st < nk) issue(st, st);
+  for (int it = 0; it < nk; ++it) {
+    if (it + S - 2 < nk) {
+      if (d_wave) wait_vmcnt_barrier<(S - 2) * (D_INS + X_INS)>();
+      else wait_vmcnt_barrier<(S - 2) * X_INS>();
+    } else {
+      wait_vmcnt_barrier<0>();
+    }
+    if (it + S - 1 < nk) issue(it + S - 1, (it + S - 1) % S);
+    const bf16_t* base = lds + (it % S) * STAGE;
+    bf16x8_t fa[FI], fb[FJ];
+#pragma unroll
+    for (int i = 0; i < FI; ++i) fa[i] = tr_frag(base, DSH, wi * WT_CO + i * 16, dswz);
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) fb[j] = tr_frag(base + BK * TCO, XSH, wj * WT_K + j * 16, xswz);
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+  }
+  wgrad_epilogue<FI, FJ, WT_CO, WT_K>(w, acc, co0, kb0, wi, wj, lane);
+}
+
 // ------------------------------------------------------- weight packing --
 // fp32 conv weights live channels-last, W[Cout][R][S][Cin] (torch's
 // channels_last memory format of the (Cout, Cin, R, S) parameter), so the
@@ -1513,7 +1655,17 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
     const long x_bytes = wgrad_x_bytes(d), dy_bytes = wgrad_dy_bytes(d);
 #define WG(TC, TKK, WC) ee_launch(conv_wgrad_kernel<TC, TKK, WC>, grid, dim3(256), 0, stream, w)
 #define WL(TC, TKK) ee_launch(conv_wgrad_glds_kernel<TC, TKK>, grid, dim3(256), 0, stream, w, x_bytes, dy_bytes)
-    if (wgrad_glds_ok(d)) {
+#define WF(TC, TKK) \
+  ee_launch(conv_wgrad_fast_kernel<TC, TKK>, grid, dim3(256), 0, stream, w, x_bytes, dy_bytes, lw, lhw)
+    const int OW = d->Wo, HW = d->Ho * d->Wo;
+    const bool pow2 = OW > 0 && (OW & (OW - 1)) == 0 && (HW & (HW - 1)) == 0;
+    if (wgrad_glds_ok(d) && pow2 && !d->up2 && env_int("EEGAN_CONV_FAST", 1)) {
+      const int lw = __builtin_ctz(OW), lhw = __builtin_ctz(HW);
+      if (TCO == 128) { if (TK == 128) WF(128, 128); else WF(128, 64); }
+      else if (TCO == 64) { if (TK == 128) WF(64, 128); else WF(64, 64); }
+      else { if (TK == 128) WF(32, 128); else WF(32, 64); }
+    }
+    else if (wgrad_glds_ok(d)) {
       if (TCO == 128) { if (TK == 128) WL(128, 128); else WL(128, 64); }
       else if (TCO == 64) { if (TK == 128) WL(64, 128); else WL(64, 64); }
       else { if (TK == 128) WL(32, 128); else WL(32, 64); }
@@ -1523,6 +1675,7 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
     else { if (TK == 128) WG(16, 128, 1); else WG(16, 64, 1); }
 #undef WG
 #undef WL
+#undef WF
     int rc = ee_check_launch("conv_wgrad");
     if (rc || w.dw) return rc;
   } else {

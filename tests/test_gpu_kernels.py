@@ -61,11 +61,13 @@ CONV_CASES = [
 
 
 def test_conv_fast_path_matches_generic(gpu, monkeypatch):
-    """The hoisted-gather kernel (EEGAN_CONV_FAST=1, default) sums the same
-    products in the same order as the generic pipelined kernel: bit-identical."""
+    """The hoisted-gather kernels (EEGAN_CONV_FAST=1, default: forward,
+    backward-data, weight gradient) sum the same products in the same order as
+    the generic pipelined kernels: bit-identical."""
     Fn, T, _ = _mods()
     for N, Cin, H, W, Cout, k, st, pad in [(2, 64, 12, 20, 96, 3, 1, 1), (2, 48, 16, 16, 32, 4, 2, 1),
-                                            (2, 256, 4, 4, 128, 3, 1, 1)]:
+                                            (2, 256, 4, 4, 128, 3, 1, 1), (3, 40, 8, 8, 72, 3, 1, 1),
+                                            (3, 24, 4, 4, 48, 4, 4, 0), (2, 32, 64, 64, 64, 4, 2, 1)]:
         torch.manual_seed(N * Cin + H)
         g = Fn.Geom(Cout, k, k, st, pad, pad, 0)
         x = _nhwc(torch.randn(N, Cin, H, W), gpu)
@@ -76,9 +78,10 @@ def test_conv_fast_path_matches_generic(gpu, monkeypatch):
         for fast in ('0', '1'):
             monkeypatch.setenv('EEGAN_CONV_FAST', fast)
             outs.append((Fn.conv_fwd_raw(x, Wt, None, g).float().cpu(),
-                         Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape)).float().cpu()))
-        assert torch.equal(outs[0][0], outs[1][0])
-        assert torch.equal(outs[0][1], outs[1][1])
+                         Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape)).float().cpu(),
+                         Fn.conv_bwd_weight_raw(x, dz, g, Wt.shape).cpu()))
+        for a, b in zip(*outs):
+            assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize('case', CONV_CASES, ids=[str(i) for i in range(len(CONV_CASES))])
