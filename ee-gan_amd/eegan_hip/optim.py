@@ -32,6 +32,7 @@ class FlatAdam(torch.optim.Optimizer):
                 uniq.append(p)
         super().__init__(uniq, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.process_group = process_group
+        self.params = uniq  # the leaves this optimiser updates (backward(inputs=...))
         self.bucket_elems = max(1, bucket_bytes // 4)
         dev = uniq[0].device
         offs, n = [], 0

@@ -9,6 +9,9 @@ and nothing in the step reads device memory on the host (no .item(), no
 cap_lens.tolist()).  Scalar loss combinations stay torch expressions on
 0-d tensors.
 """
+import contextlib
+import os
+
 import torch
 
 from . import functional as Fn
@@ -32,7 +35,8 @@ def prepare_class_labels(batch_size, class_num, class_ids, device):
 
 class Trainer(object):
     def __init__(self, netG, attr_enhance, netsD, image_encoder, text_encoder, batch_size, disc_class=True,
-                 class_nums=200, class_coe=10.0, sim_coe=0.05, device='cuda', max_attr_nums=3, damsm_global=True):
+                 class_nums=200, class_coe=10.0, sim_coe=0.05, device='cuda', max_attr_nums=3, damsm_global=True,
+                 streams=None):
         self.netG, self.attr_enhance, self.netsD = netG, attr_enhance, netsD
         self.image_encoder, self.text_encoder = image_encoder, text_encoder
         self.batch_size = batch_size
@@ -44,6 +48,37 @@ class Trainer(object):
         self.damsm_global = damsm_global
         self.optimizerG, self.optimizerDs = self.load_optimizers(netG, netsD, attr_enhance)
         self.records = {}
+        # the three discriminators share no parameters, so their d_update
+        # sequences (and, in g_update, their forward/backward on the fake images
+        # beside the DAMSM image encoder) run on separate HIP streams: the small
+        # 64/128-px launches fill the GPU next to the 256-px ones.  Every phase
+        # forks from and joins back into the caller's stream, so a captured step
+        # graph sees the same dependencies.
+        if streams is None:
+            streams = os.environ.get('EEGAN_STREAMS', '1') != '0'
+        self.use_streams = bool(streams) and torch.cuda.is_available() and torch.device(device).type == 'cuda'
+        self._streams = None
+
+    def _side_streams(self, n):
+        if not self.use_streams:
+            return [None] * n
+        if self._streams is None or len(self._streams) < n:
+            self._streams = [torch.cuda.Stream(device=self.device) for _ in range(n)]
+        main = torch.cuda.current_stream()
+        for s in self._streams[:n]:
+            s.wait_stream(main)
+        return self._streams[:n]
+
+    @staticmethod
+    def _on(stream):
+        return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+
+    @staticmethod
+    def _join(streams):
+        main = torch.cuda.current_stream()
+        for s in streams:
+            if s is not None:
+                main.wait_stream(s)
 
     @staticmethod
     def load_optimizers(netG, netDs, attr_enhance):
@@ -133,60 +168,80 @@ class Trainer(object):
 
     # ----------------------------------------------------------- updates --
     def d_update(self, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec=False):
-        """train.py:437-469: per D a hinge(+class) step, then a GP step."""
+        """train.py:437-469: per D a hinge(+class) step, then a GP step (each D on its own stream)."""
+        streams = self._side_streams(len(self.netsD))
         for i in range(len(self.netsD)):
-            real_img, fake_img, netD, optD = imgs[i], fake_imgs[i], self.netsD[i], self.optimizerDs[i]
-            disc_class = self.disc_class and i == 2
+            with self._on(streams[i]):
+                self._d_update_one(i, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec)
+        self._join(streams)
+
+    def _d_update_one(self, i, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec):
+        """One D of d_update (train.py:439-466)."""
+        real_img, fake_img, netD, optD = imgs[i], fake_imgs[i], self.netsD[i], self.optimizerDs[i]
+        disc_class = self.disc_class and i == 2
+        if disc_class:
+            e_real, e_fake, e_unpair, c_real, c_fake, c_unpair = self.d_loss_class(
+                real_img, fake_img, sent_emb, unpair_sent_emb, class_labels, netD)
+            d_loss = e_real + (e_fake + e_unpair) / 2.0 + (c_real + c_fake + c_unpair) / 3.0 * self.d_class_coe
+        else:
+            e_real, e_fake, e_unpair = self.d_loss(real_img, fake_img, sent_emb, unpair_sent_emb, netD)
+            d_loss = e_real + (e_fake + e_unpair) / 2.0
+        optD.zero_grad()
+        d_loss.backward(inputs=optD.params)
+        optD.step()
+        d_loss_gp = self.MA_gradient_penalty(real_img, sent_emb, netD, disc_class)
+        optD.zero_grad()
+        d_loss_gp.backward(inputs=optD.params)
+        optD.step()
+        if iter_rec:
+            self.records['errD_%d/real_sent' % i] = e_real.detach()
+            self.records['errD_%d/fake_sent' % i] = e_fake.detach()
+            self.records['errD_%d/unpair_sent' % i] = e_unpair.detach()
+            self.records['errD_%d/d_loss_gp' % i] = d_loss_gp.detach()
             if disc_class:
-                e_real, e_fake, e_unpair, c_real, c_fake, c_unpair = self.d_loss_class(
-                    real_img, fake_img, sent_emb, unpair_sent_emb, class_labels, netD)
-                d_loss = e_real + (e_fake + e_unpair) / 2.0 + (c_real + c_fake + c_unpair) / 3.0 * self.d_class_coe
-            else:
-                e_real, e_fake, e_unpair = self.d_loss(real_img, fake_img, sent_emb, unpair_sent_emb, netD)
-                d_loss = e_real + (e_fake + e_unpair) / 2.0
-            optD.zero_grad()
-            d_loss.backward()
-            optD.step()
-            d_loss_gp = self.MA_gradient_penalty(real_img, sent_emb, netD, disc_class)
-            optD.zero_grad()
-            d_loss_gp.backward()
-            optD.step()
-            if iter_rec:
-                self.records['errD_%d/real_sent' % i] = e_real.detach()
-                self.records['errD_%d/fake_sent' % i] = e_fake.detach()
-                self.records['errD_%d/unpair_sent' % i] = e_unpair.detach()
-                self.records['errD_%d/d_loss_gp' % i] = d_loss_gp.detach()
-                if disc_class:
-                    self.records['errD_%d/real_class' % i] = c_real.detach()
-                    self.records['errD_%d/fake_class' % i] = c_fake.detach()
-                    self.records['errD_%d/mismatch_class' % i] = c_unpair.detach()
+                self.records['errD_%d/real_class' % i] = c_real.detach()
+                self.records['errD_%d/fake_class' % i] = c_fake.detach()
+                self.records['errD_%d/mismatch_class' % i] = c_unpair.detach()
 
     def g_update(self, fake_imgs, sent_emb, words_emb, attr_emb, class_ids, batch_size, match_labels, cap_lens,
                  class_labels, iter_rec=False):
         """train.py:471-502."""
-        g_loss = None
-        for i in range(len(self.netsD)):
+        nD = len(self.netsD)
+        streams = self._side_streams(nD + 1)
+        terms = []
+        for i in range(nD):
             fake_img, netD = fake_imgs[i], self.netsD[i]
-            if self.disc_class and i == 2:
-                errG, errG_class = self.g_loss_class(fake_img, sent_emb, class_labels, netD)
-                term = errG + errG_class * self.g_class_coe
-            else:
-                errG = self.g_loss(fake_img, sent_emb, netD)
-                term = errG
-            g_loss = term if g_loss is None else g_loss + term
+            with self._on(streams[i]):
+                if self.disc_class and i == 2:
+                    errG, errG_class = self.g_loss_class(fake_img, sent_emb, class_labels, netD)
+                    term = errG + errG_class * self.g_class_coe
+                else:
+                    errG = self.g_loss(fake_img, sent_emb, netD)
+                    term = errG
+            terms.append(term)
             if iter_rec:
                 self.records['errG/G_%d_fake_sent' % i] = errG.detach()
                 if self.disc_class and i == 2:
                     self.records['errG/G_%d_fake_class' % i] = errG_class.detach()
-        w_loss, s_loss, a_loss = self.DAMSM_loss(fake_imgs[-1], sent_emb, words_emb, attr_emb, class_ids, batch_size,
-                                                 match_labels, cap_lens, self.image_encoder)
+        with self._on(streams[nD]):
+            w_loss, s_loss, a_loss = self.DAMSM_loss(fake_imgs[-1], sent_emb, words_emb, attr_emb, class_ids,
+                                                     batch_size, match_labels, cap_lens, self.image_encoder)
+        self._join(streams)
+        g_loss = terms[0]
+        for t in terms[1:]:
+            g_loss = g_loss + t
         g_loss = g_loss + self.DAMSM_coe * (s_loss + w_loss + a_loss)
         if iter_rec:
             self.records['errG/s_loss'] = s_loss.detach()
             self.records['errG/w_loss'] = w_loss.detach()
             self.records['errG/a_loss'] = a_loss.detach()
         self.optimizerG.zero_grad()
-        g_loss.backward()
+        # only the optimised parameters' gradients are formed: train.py's
+        # g_loss.backward() also fills the D parameters' .grad, but d_update
+        # zeroes those before every use (train.py:451,457), and the GP's
+        # interpolated-image gradient is never read -- skipping them changes no
+        # parameter and saves the D weight-gradient passes
+        g_loss.backward(inputs=self.optimizerG.params)
         self.optimizerG.step()
         return g_loss.detach()
 
