@@ -190,8 +190,12 @@ def main():
     if not args.no_timer:
         timer = Fn.LaunchTimer()
         Fn.TIMER = timer
+        # single stream while timing: a dispatch sharing the GPU with another
+        # stream's kernels would read longer than its own work
+        streams, T.use_streams = T.use_streams, False
         for _ in range(per):
             T.train_step(batch)
+        T.use_streams = streams
         Fn.TIMER = None
     kern = timer.summary() if timer is not None else {'conv_fwd': [1, 0.0, 0.0, 1.0]}
     ms = dt / args.steps * 1e3

@@ -20,7 +20,18 @@ n = len(t)
 a, b = n // 4, 3 * n // 4
 seg = t[a:b]
 busy = sum(e - s for s, e, _ in seg)
-span = seg[-1][1] - seg[0][0]
+span = max(e for _, e, _ in seg) - seg[0][0]
+# union of the kernel intervals (concurrent streams overlap)
+cov, cur_s, cur_e = 0, None, None
+for s_, e_, _ in seg:
+    if cur_e is None or s_ > cur_e:
+        if cur_e is not None:
+            cov += cur_e - cur_s
+        cur_s, cur_e = s_, e_
+    else:
+        cur_e = max(cur_e, e_)
+cov += cur_e - cur_s
+print('union busy %.2f ms of span %.2f ms (idle %.2f ms)' % (cov * 1e-6, span * 1e-6, (span - cov) * 1e-6))
 gaps = [seg[i + 1][0] - seg[i][1] for i in range(len(seg) - 1)]
 gaps.sort()
 print('kernels %d  busy %.2f ms  span %.2f ms  busy/span %.3f' % (len(seg), busy * 1e-6, span * 1e-6, busy / span))
