@@ -65,6 +65,7 @@ struct ConvArgs {
   int Mrows, Kw;                // output channels / packed-weight row stride
   int P;                        // N*OH*OW
   int ncls, nsplit;             // parity classes (BWDD stride>1), K splits
+  int noload;                   // diagnostics only (EEGAN_CONV_NOLOAD): skip steady-state loads
 };
 
 // K step kt, 8-channel chunk kc -> kernel tap and channel.  Normal mode: the
@@ -361,6 +362,7 @@ EE_DEV rsrc_t make_rsrc(const void* p, long bytes) {
 // later ds_read and inserts s_waitcnt vmcnt(0) in front of them, which drains
 // the whole ring every K-step.  Ordering is ours: counted waits + barrier
 // (wait_vmcnt_barrier) before a stage is read.
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is ours to clobber in these kernels
 EE_DEV void lds_dma16(rsrc_t rsrc, const void* lds_dst, unsigned voff) {
   const int m0 = __builtin_amdgcn_readfirstlane((int)(uintptr_t)(lds_void_t*)lds_dst);
   asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(rsrc)
@@ -543,14 +545,17 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a, long src_
 // per-thread voffset and the K position as soffset.  Normal-mode operands only
 // (C % 8 == 0, C > 8), no fused upsample, <= 32 taps per parity class.
 EE_DEV void lds_dma16s(rsrc_t rsrc, int lds_addr, unsigned voff, int soff) {
+  // the operands are wave-uniform by construction; readfirstlane makes the
+  // compiler keep them in SGPRs whatever it can prove
+  lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
+  soff = __builtin_amdgcn_readfirstlane(soff);
   asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(lds_addr), "v"(voff), "s"(rsrc),
                "s"(soff)
                : "memory", "m0");
 }
 
-template <int MODE, int TCO, int TPIX>
+template <int MODE, int TCO, int TPIX, int KS = 1, int S = CONV_STAGES>
 __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_bytes, long w_bytes) {
-  constexpr int S = CONV_STAGES;
   constexpr int WCO = TCO >= 64 ? 2 : 1, WPIX = 4 / WCO;
   constexpr int WT_CO = TCO / WCO, WT_PIX = TPIX / WPIX;
   constexpr int FI = WT_CO / 16, FJ = WT_PIX / 16;
@@ -682,34 +687,50 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
     for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
+  // KS K-steps per barrier: stages it .. it+KS-1 are multiplied while stages up
+  // to it+S-1 are in flight; the KS stages issued after the barrier reuse the
+  // slots multiplied in the previous iteration
+  constexpr int YNG = S - 2 * KS;  // stages allowed in flight at the wait
+  static_assert(YNG >= 0, "stages");
 #pragma unroll
-  for (int st = 0; st < S - 1; ++st)
+  for (int st = 0; st < S - KS; ++st)
     if (st < nk) issue(st);
-  for (int it = 0; it < nk; ++it) {
-    if (it + S - 2 < nk) {
-      if (a_wave) wait_vmcnt_barrier<(S - 2) * (A_INS + B_INS)>();
-      else wait_vmcnt_barrier<(S - 2) * B_INS>();
+  for (int it = 0; it < nk; it += KS) {
+    if (it + S - KS <= nk) {
+      if (a_wave) wait_vmcnt_barrier<YNG * (A_INS + B_INS)>();
+      else wait_vmcnt_barrier<YNG * B_INS>();
     } else {
       wait_vmcnt_barrier<0>();
     }
-    if (it + S - 1 < nk) issue((it + S - 1) % S);
-    const bf16_t* base = lds + (it % S) * STAGE;
-    bf16x8_t fa[FI], fb[FJ];
 #pragma unroll
-    for (int i = 0; i < FI; ++i) {
-      const int row = wi * WT_CO + i * 16 + fr;
-      fa[i] = as_frag(*reinterpret_cast<const uint4*>(base + row * BK + ((fq ^ swz_b128((row >> 2) & 3)) * 8)));
+    for (int k = 0; k < KS; ++k)
+      if (it + S - KS + k < nk && !a.noload) issue((it + S - KS + k) % S);
+    bf16x8_t fa[KS][FI], fb[KS][FJ];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      if (it + k >= nk) break;
+      const bf16_t* base = lds + ((it + k) % S) * STAGE;
+#pragma unroll
+      for (int i = 0; i < FI; ++i) {
+        const int row = wi * WT_CO + i * 16 + fr;
+        fa[k][i] = as_frag(*reinterpret_cast<const uint4*>(base + row * BK + ((fq ^ swz_b128((row >> 2) & 3)) * 8)));
+      }
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) {
+        const int row = wj * WT_PIX + j * 16 + fr;
+        fb[k][j] = as_frag(
+            *reinterpret_cast<const uint4*>(base + TCO * BK + row * BK + ((fq ^ swz_b128((row >> 2) & 3)) * 8)));
+      }
     }
 #pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-      const int row = wj * WT_PIX + j * 16 + fr;
-      fb[j] = as_frag(*reinterpret_cast<const uint4*>(base + TCO * BK + row * BK + ((fq ^ swz_b128((row >> 2) & 3)) * 8)));
+    for (int k = 0; k < KS; ++k) {
+      if (it + k >= nk) break;
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[k][i], fb[k][j], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int i = 0; i < FI; ++i)
-#pragma unroll
-      for (int j = 0; j < FJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
   }
   igemm_epilogue<MODE, FI, FJ, WT_CO, WT_PIX>(a, acc, pix0, co0, wi, wj, lane, split, Pc, CH, CW, qy, qx, stc);
 }
@@ -1391,6 +1412,8 @@ Plan plan_igemm(const ConvArgs& a, int Pc_max) {
 template <int MODE>
 int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src_bytes) {
   Plan p = plan_igemm(a, Pc_max);
+  a.noload = env_int("EEGAN_CONV_NOLOAD", 0);
+  const int ksv = env_int("EEGAN_CONV_KS", 2);  // K-steps per barrier (1: sweep baseline)
   a.nsplit = p.nsplit;
   a.part = p.nsplit > 1 ? part_ws : nullptr;
   if (p.nsplit > 1 && !part_ws) {
@@ -1400,7 +1423,11 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   dim3 grid(ee_cdiv(Pc_max, p.tpix), ee_cdiv(a.Mrows, p.tco), a.ncls * p.nsplit);
   const long w_bytes = (long)ee_round_up(a.Mrows, 128) * a.Kw * 2;
 #define GL(TC, TP) ee_launch(conv_glds_kernel<MODE, TC, TP>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
-#define FA(TC, TP) ee_launch(conv_fast_kernel<MODE, TC, TP>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
+#define FA(TC, TP)                                                                                          \
+  do {                                                                                                       \
+    if (ksv == 2) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 4>, grid, dim3(256), 0, s, a, src_bytes, w_bytes);      \
+    else ee_launch(conv_fast_kernel<MODE, TC, TP, 1, 4>, grid, dim3(256), 0, s, a, src_bytes, w_bytes);                     \
+  } while (0)
 #define IG(TC, TP, WC) ee_launch(conv_igemm_kernel<MODE, TC, TP, WC>, grid, dim3(256), 0, s, a)
   const bool glds = ((a.Cvalid % 8) == 0 || a.Cgp == 8) && src_bytes < 0x7fffffffL && w_bytes < 0x7fffffffL;
   int tr_ = a.R, ts_ = a.S;
@@ -1426,7 +1453,7 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
 #undef GL
 #undef FA
   int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd" : "conv_bwd_data");
-  if (rc || p.nsplit == 1) return rc;
+  if (rc || a.nsplit == 1) return rc;
   const long total = (long)a.P * a.Mrows;
   ee_launch(conv_splitk_reduce_kernel<MODE>, dim3((int)std::min<long>((total + 255) / 256, 4096)), dim3(256), 0, s, a);
   return ee_check_launch("conv_splitk_reduce");
