@@ -24,6 +24,9 @@ from collections import defaultdict
 
 # (family, is_primary): the primary kernel counts calls; secondaries add time
 _FAMILIES = [
+    (re.compile(r'conv_fast_kernel<0,'), 'conv_fwd', True),
+    (re.compile(r'conv_fast_kernel<1,'), 'conv_bwd_data', True),
+    (re.compile(r'conv_wgrad_fast_kernel<'), 'conv_bwd_weight', True),
     (re.compile(r'conv_glds_kernel<0,'), 'conv_fwd', True),
     (re.compile(r'conv_glds_kernel<1,'), 'conv_bwd_data', True),
     (re.compile(r'conv_wgrad_glds_kernel<'), 'conv_bwd_weight', True),
