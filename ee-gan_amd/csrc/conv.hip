@@ -1279,14 +1279,15 @@ __global__ void pack_weights_kernel(const float* w, const float* scale, int Cout
 // {w, scale, out, Cout, Cin, R, S, transposed}, then njobs+1 prefix offsets of
 // BLOCKS per job (pack_multi_blocks).  Forward image: one block per output row
 // (w[co] is already the row's (tap, c) order: a padded, coalesced copy);
-// bwd-data image: one block per 8 input channels x a chunk of output channels,
+// bwd-data image: one block per 32 input channels x a chunk of output channels,
 // transposed through LDS so both the fp32 reads (8-channel runs) and the bf16
 // row writes are contiguous.
 constexpr int PK_LDS = 9344;   // floats of staging
 
 EE_HOST_DEV_INLINE int pk_cgp(int C) { return C <= 8 ? 8 : (C + BK - 1) / BK * BK; }
-// output channels per bwd-image block: 8 input channels x RS taps x CO fit the staging
-EE_HOST_DEV_INLINE int pk_bwd_co(int RS) { return min(128, PK_LDS / (8 * RS + 1)); }
+constexpr int PK_TI = 32;      // input channels per bwd-image block (128-B fp32 runs)
+// output channels per bwd-image block: PK_TI input channels x RS taps x CO fit the staging
+EE_HOST_DEV_INLINE int pk_bwd_co(int RS) { return min(128, PK_LDS / (PK_TI * RS + 1)); }
 
 __global__ __launch_bounds__(256) void pack_weights_multi_kernel(const long* __restrict__ table, int njobs) {
   __shared__ float buf[PK_LDS];
@@ -1319,9 +1320,9 @@ __global__ __launch_bounds__(256) void pack_weights_multi_kernel(const long* __r
       orow[k] = f2bf(tap < RS && c < Cin ? src[tap * Cin + c] * sc : 0.f);
     }
   } else {
-    // ---- bwd-data image: rows ci0..ci0+7 x one chunk of CO output channels,
+    // ---- bwd-data image: rows ci0..ci0+TI-1 x one chunk of CO output channels,
     // out[ci][tap*Cgp + co] = w[co][tap][ci]
-    constexpr int TI = 8;
+    constexpr int TI = PK_TI;
     const int Cgp = pk_cgp(Cout), Kw = (RS * Cgp + BK - 1) / BK * BK;
     const int RW = TI * RS + 1;  // odd LDS row stride
     const int CO = pk_bwd_co(RS);
@@ -1387,8 +1388,8 @@ Plan plan_igemm(const ConvArgs& a, int Pc_max) {
   // tuning knobs (benchmark sweeps only): grid target, min K-steps per split,
   // and whether 64-row tiles are tried before splitting K
   const int target = env_int("EEGAN_CONV_TARGET", 512);
-  const int mink = env_int("EEGAN_CONV_MINK", 8);
-  const int small_co = env_int("EEGAN_CONV_SMALLCO", 0);
+  const int mink = env_int("EEGAN_CONV_MINK", 16);
+  const int small_co = env_int("EEGAN_CONV_SMALLCO", 1);
   const int rows = a.Mrows;
   Plan p;
   p.tco = rows > 64 ? 128 : rows > 32 ? 64 : rows > 16 ? 32 : 16;
@@ -1540,7 +1541,7 @@ int eegan_conv_pack_weights(const float* w, const float* scale, int Cout, int Ci
 
 long eegan_conv_pack_multi_blocks(int Cout, int Cin, int R, int S, int transposed) {
   if (!transposed) return ee_round_up(Cout, 128);
-  return (long)(ee_round_up(Cin, 128) / 8) * ee_cdiv(pk_cgp(Cout), pk_bwd_co(R * S));
+  return (long)(ee_round_up(Cin, 128) / PK_TI) * ee_cdiv(pk_cgp(Cout), pk_bwd_co(R * S));
 }
 
 int eegan_conv_pack_weights_multi(const long* table, int njobs, long total_blocks, hipStream_t stream) {

@@ -117,6 +117,33 @@ __global__ __launch_bounds__(NT) void dot_partial_kernel(const bf16_t* x, int ld
   if (threadIdx.x == 0) ws[blockIdx.x] = acc;
 }
 
+// ScaleAdd backward in one pass over g: out = s * g (the residual-branch
+// gradient) and the per-block partials of <g, h> (the gain's gradient)
+__global__ __launch_bounds__(NT) void scale_dot_partial_kernel(const bf16_t* g, int ldg, const bf16_t* h, int ldh,
+                                                               const float* gamma, float alpha, long P, int C,
+                                                               bf16_t* out, int ldo, float* ws) {
+  __shared__ float red[16];
+  const int C8 = (C + 7) / 8;
+  const bool vec = (ldg % 8 == 0) && (ldh % 8 == 0) && (ldo % 8 == 0);
+  const float s = alpha * (gamma ? *gamma : 1.f);
+  float acc = 0.f;
+  GRID_LOOP(e, P * C8) {
+    const long p = e / C8;
+    const int c0 = (int)(e % C8) * 8;
+    const int nv = min(8, C - c0);
+    V8 a = load8(g + p * ldg + c0, nv, vec);
+    V8 b = load8(h + p * ldh + c0, nv, vec);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      acc += a.v[j] * b.v[j];
+      a.v[j] *= s;
+    }
+    store8(out + p * ldo + c0, a, nv, vec);
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) ws[blockIdx.x] = acc;
+}
+
 __global__ void dot_final_kernel(const float* ws, int n, float scale, float* out, int accumulate) {
   __shared__ float red[16];
   float acc = 0.f;
@@ -544,6 +571,16 @@ int eegan_dot(const uint16_t* x, int ldx, const uint16_t* y, int ldy, long P, in
   int rc = ee_check_launch("dot_partial");
   if (rc) return rc;
   dot_final_kernel<<<1, 1024, 0, s>>>(ws, blocks, scale, out, accumulate);
+  return ee_check_launch("dot_final");
+}
+
+int eegan_scale_dot(const uint16_t* g, int ldg, const uint16_t* h, int ldh, const float* gamma, float alpha, long P,
+                    int C, uint16_t* out, int ldo, float* ws, float* dot_out, int accumulate, hipStream_t s) {
+  const int blocks = std::min(1024, grid_for(P * ((C + 7) / 8)));
+  scale_dot_partial_kernel<<<blocks, NT, 0, s>>>(g, ldg, h, ldh, gamma, alpha, P, C, out, ldo, ws);
+  int rc = ee_check_launch("scale_dot_partial");
+  if (rc) return rc;
+  dot_final_kernel<<<1, 1024, 0, s>>>(ws, blocks, 1.f, dot_out, accumulate);
   return ee_check_launch("dot_final");
 }
 

@@ -351,8 +351,13 @@ class ConvBwdDataFn(torch.autograd.Function):
         g_dz = g_W = None
         if ctx.needs_input_grad[0]:
             g_dz = Conv2dFn.apply(gdx, W, None, ctx.g, 0, 0.0, False, ctx.cache)
-        if ctx.needs_input_grad[1]:
-            g_W = ConvBwdWeightFn.apply(gdx, dz, ctx.g)
+        if ctx.needs_input_grad[1] and _needed(ctx, 1):
+            sink = _grad_sink(ctx, 1)
+            if sink is not None and sink.is_contiguous(memory_format=CL):
+                # the gradient penalty's second backward: dW straight into p.grad
+                conv_bwd_weight_raw(gdx, dz, ctx.g, W.shape, out=sink)
+            else:
+                g_W = ConvBwdWeightFn.apply(gdx, dz, ctx.g)
         return g_dz, g_W, None, None, None
 
 
@@ -546,6 +551,20 @@ class ScaleAddFn(torch.autograd.Function):
         h, gamma = ctx.saved_tensors
         g = _as_bf16_grad(g)
         d_res = g if ctx.needs_input_grad[0] else None
+        if not torch.is_grad_enabled() and _needed(ctx, 1) and _needed(ctx, 2):
+            # first-order: gamma * g and <g, h> in one pass, the gain's gradient
+            # accumulated straight into gamma.grad when that is the sink
+            N, C, H, W = g.shape
+            d_h = empty_nhwc(N, C, H, W, g.device)
+            sink = _grad_sink(ctx, 2)
+            d_g = None
+            if sink is None:
+                d_g = torch.empty(1, dtype=F32, device=g.device)
+            ws = workspace(ops.dot_workspace(), g.device)
+            ops.scale_dot(g.data_ptr(), ld_of(g), h.data_ptr(), ld_of(h), gamma.data_ptr(), 1.0, N * H * W, C,
+                          d_h.data_ptr(), ld_of(d_h), ws.data_ptr(), (sink if d_g is None else d_g).data_ptr(),
+                          int(d_g is None), stream())
+            return d_res, d_h, d_g
         d_h = ScaleFn.apply(g, gamma) if ctx.needs_input_grad[1] else None
         d_g = DotFn.apply(g, h) if ctx.needs_input_grad[2] else None
         return d_res, d_h, d_g

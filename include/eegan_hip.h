@@ -138,6 +138,10 @@ int eegan_act_bwd(const uint16_t* dy, int lddy, const uint16_t* y, int ldy, long
                   uint16_t* dx, int lddx, hipStream_t s);
 int eegan_scale_add(const uint16_t* x, int ldx, const uint16_t* y, int ldy, const float* gamma, float alpha, long P,
                     int C, uint16_t* out, int ldo, hipStream_t s);
+/* ScaleAdd backward (models.py:122,142,278 first-order): out = alpha*gamma*g and
+ * dot_out (+)= <g, h>, one pass over g; ws = eegan_dot_workspace() bytes */
+int eegan_scale_dot(const uint16_t* g, int ldg, const uint16_t* h, int ldh, const float* gamma, float alpha, long P,
+                    int C, uint16_t* out, int ldo, float* ws, float* dot_out, int accumulate, hipStream_t stream);
 long eegan_dot_workspace(void);
 int eegan_dot(const uint16_t* x, int ldx, const uint16_t* y, int ldy, long P, int C, float scale, float* ws,
               float* out, int accumulate, hipStream_t s);

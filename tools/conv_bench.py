@@ -30,6 +30,10 @@ SHAPES = {
     'c3x3_256_8': (16, 256, 8, 8, 256, 3, 1, 1),
     'c1x1_32_256': (16, 32, 256, 256, 64, 1, 1, 0),
     'c3x3_3_256': (16, 3, 256, 256, 32, 3, 1, 1),
+    'c3x3_1024_4': (16, 768, 4, 4, 1024, 3, 1, 1),
+    'c4x4s2_512_8': (16, 512, 8, 8, 512, 4, 2, 1),
+    'c3x3_512_8': (16, 512, 8, 8, 512, 3, 1, 1),
+    'c1x1_768_17': (16, 768, 17, 17, 192, 1, 1, 0),
 }
 
 
