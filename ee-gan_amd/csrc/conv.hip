@@ -1114,7 +1114,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_glds_kernel(WgradArgs w, lo
 // offset is a per-thread constant plus a uniform term, its bounds test two
 // compares against uniform-shifted constants.  Rows past the split end read dy
 // as zeros (their x rows are finite activations, so the products vanish).
-template <int TCO, int TK>
+template <int TCO, int TK, int KS = 1>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_fast_kernel(WgradArgs w, long x_bytes, long dy_bytes, int lw,
                                                                  int lhw) {
   constexpr int S = CONV_STAGES;
@@ -1222,28 +1222,41 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fast_kernel(WgradArgs w, lo
   auto dswz = [](int r) { return tr_swz<DCH>(r); };
   auto xswz = [](int r) { return tr_swz<XCH>(r); };
 
+  // KS pixel steps per barrier (as conv_fast_kernel)
+  constexpr int YNG = S - 2 * KS;
+  static_assert(YNG >= 0, "stages");
 #pragma unroll
-  for (int st = 0; st < S - 1; ++st)
+  for (int st = 0; st < S - KS; ++st)
     if (st < nk) issue(st, st);
-  for (int it = 0; it < nk; ++it) {
-    if (it + S - 2 < nk) {
-      if (d_wave) wait_vmcnt_barrier<(S - 2) * (D_INS + X_INS)>();
-      else wait_vmcnt_barrier<(S - 2) * X_INS>();
+  for (int it = 0; it < nk; it += KS) {
+    if (it + S - KS <= nk) {
+      if (d_wave) wait_vmcnt_barrier<YNG * (D_INS + X_INS)>();
+      else wait_vmcnt_barrier<YNG * X_INS>();
     } else {
       wait_vmcnt_barrier<0>();
     }
-    if (it + S - 1 < nk) issue(it + S - 1, (it + S - 1) % S);
-    const bf16_t* base = lds + (it % S) * STAGE;
-    bf16x8_t fa[FI], fb[FJ];
 #pragma unroll
-    for (int i = 0; i < FI; ++i) fa[i] = tr_frag(base, DSH, wi * WT_CO + i * 16, dswz);
+    for (int k = 0; k < KS; ++k)
+      if (it + S - KS + k < nk) issue(it + S - KS + k, (it + S - KS + k) % S);
+    bf16x8_t fa[KS][FI], fb[KS][FJ];
 #pragma unroll
-    for (int j = 0; j < FJ; ++j) fb[j] = tr_frag(base + BK * TCO, XSH, wj * WT_K + j * 16, xswz);
+    for (int k = 0; k < KS; ++k) {
+      if (it + k >= nk) break;
+      const bf16_t* base = lds + ((it + k) % S) * STAGE;
 #pragma unroll
-    for (int i = 0; i < FI; ++i)
+      for (int i = 0; i < FI; ++i) fa[k][i] = tr_frag(base, DSH, wi * WT_CO + i * 16, dswz);
 #pragma unroll
-      for (int j = 0; j < FJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < FJ; ++j) fb[k][j] = tr_frag(base + BK * TCO, XSH, wj * WT_K + j * 16, xswz);
+    }
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      if (it + k >= nk) break;
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[k][i], fb[k][j], acc[i][j], 0, 0, 0);
+    }
   }
   wgrad_epilogue<FI, FJ, WT_CO, WT_K>(w, acc, co0, kb0, wi, wj, lane);
 }
@@ -1630,8 +1643,9 @@ static void wgrad_plan(const eegan_conv_desc* d, int& TCO, int& TK, int& nsplit,
   const int tiles = ee_cdiv(d->K, TCO) * ee_cdiv(K, TK);
   // ~2 blocks per CU, >= 16 K-steps (512 pixels) per split: the fp32 slab
   // (nsplit x Cout x K) is written once and read once by the column reduce
-  int want = std::max(1, 512 / std::max(tiles, 1));
-  const int maxsplit = std::max(1, ee_cdiv(P, 512));
+  // knobs for sweeps: grid target (blocks) and minimum pixels per split
+  int want = std::max(1, env_int("EEGAN_WGRAD_TARGET", 512) / std::max(tiles, 1));
+  const int maxsplit = std::max(1, ee_cdiv(P, env_int("EEGAN_WGRAD_MINP", 512)));
   nsplit = std::min(want, maxsplit);
   pps = ee_round_up(ee_cdiv(P, nsplit), BK);
   nsplit = ee_cdiv(P, pps);
@@ -1683,10 +1697,14 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
     const long x_bytes = wgrad_x_bytes(d), dy_bytes = wgrad_dy_bytes(d);
 #define WG(TC, TKK, WC) ee_launch(conv_wgrad_kernel<TC, TKK, WC>, grid, dim3(256), 0, stream, w)
 #define WL(TC, TKK) ee_launch(conv_wgrad_glds_kernel<TC, TKK>, grid, dim3(256), 0, stream, w, x_bytes, dy_bytes)
-#define WF(TC, TKK) \
-  ee_launch(conv_wgrad_fast_kernel<TC, TKK>, grid, dim3(256), 0, stream, w, x_bytes, dy_bytes, lw, lhw)
+#define WF(TC, TKK)                                                                                      \
+  do {                                                                                                   \
+    if (wks == 2) ee_launch(conv_wgrad_fast_kernel<TC, TKK, 2>, grid, dim3(256), 0, stream, w, x_bytes, dy_bytes, lw, lhw); \
+    else ee_launch(conv_wgrad_fast_kernel<TC, TKK, 1>, grid, dim3(256), 0, stream, w, x_bytes, dy_bytes, lw, lhw);          \
+  } while (0)
     const int OW = d->Wo, HW = d->Ho * d->Wo;
     const bool pow2 = OW > 0 && (OW & (OW - 1)) == 0 && (HW & (HW - 1)) == 0;
+    const int wks = env_int("EEGAN_WGRAD_KS", 2);
     if (wgrad_glds_ok(d) && pow2 && !d->up2 && env_int("EEGAN_CONV_FAST", 1)) {
       const int lw = __builtin_ctz(OW), lhw = __builtin_ctz(HW);
       if (TCO == 128) { if (TK == 128) WF(128, 128); else WF(128, 64); }
