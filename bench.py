@@ -149,16 +149,28 @@ def main():
     T, B, ncls = build(args.config, device)
     batch = make_batch(B, device, seed=3407 + rank, class_num=max(ncls, 1), with_class=True)
 
-    use_graph = args.graph == 'on' or (args.graph == 'auto' and world == 1)
+    # the whole step, collectives included (own per-lane RCCL communicators,
+    # eegan_hip.rccl), is one captured HIP graph on every rank
+    # (EEGAN_GRAPH_DIST=0: eager steps when N > 1)
+    use_graph = args.graph == 'on' or (args.graph == 'auto' and (
+        world == 1 or (bool(D.COMMS) and os.environ.get('EEGAN_GRAPH_DIST', '1') == '1')))
+    graph_error = None
     if use_graph:
         from eegan_hip.trainer import StepGraph
         # the eager timing pass after the capture re-enters AccumulateGrad nodes first seen on the
         # capture stream; torch warns about the stream change, which is harmless here
         torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
-        sg = StepGraph(T, batch, warmup=max(1, args.warmup - 1))   # eager warm-ups, then capture
-        step = sg.replay
-        step()  # last warm-up = first replay
-    else:
+        try:
+            sg = StepGraph(T, batch, warmup=max(1, args.warmup - 1))   # eager warm-ups, then capture
+            step = sg.replay
+            step()  # last warm-up = first replay
+        except Exception as e:  # capture refused (e.g. a runtime without collective capture): run eagerly
+            graph_error = repr(e)[:300]
+            print('bench: step graph capture failed, running eagerly: %s' % graph_error, file=sys.stderr,
+                  flush=True)
+            use_graph = False
+            torch.cuda.synchronize()
+    if not use_graph:
         def step():
             T.train_step(batch)
 
@@ -227,6 +239,8 @@ def main():
            'host_issue_ms_per_step': round(t_issue / args.steps * 1e3, 3),
            'execution': 'hip-graph replay of the captured step' if use_graph else 'eager',
            'roofline': roof}
+    if graph_error:
+        out['graph_capture_error'] = graph_error
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out['cpu_baseline'] = cpu_baseline(args.cpu_seconds)

@@ -20,6 +20,29 @@ import torch.distributed as dist
 from . import functional as Fn
 
 
+# Rehearsal switch (EEGAN_FORCE_DIST=1): initialise a process group and issue
+# every collective of the data-parallel step even with ONE rank, so the RCCL
+# path (incl. its capture into the step's HIP graph) runs on a one-GPU box.
+FORCE = os.environ.get('EEGAN_FORCE_DIST') == '1'
+COMMS = []    # eegan_hip.rccl.Communicator per stream lane when the ranks own GPUs (graph-capturable)
+N_LANES = 6   # lane 0: the caller's (main) stream; 1..: streams bound with bind_stream
+_LANE_OF = {}
+
+
+def bind_stream(stream, lane):
+    """Collectives issued on `stream` use communicator `lane + 1` (lane >= 0)."""
+    if lane + 1 >= N_LANES:
+        raise ValueError('eegan_hip.dist: only %d stream lanes' % (N_LANES - 1))
+    _LANE_OF[stream.cuda_stream] = lane + 1
+
+
+def comm():
+    """The RCCL communicator of the current stream's lane (None without GPU ranks)."""
+    if not COMMS:
+        return None
+    return COMMS[_LANE_OF.get(torch.cuda.current_stream().cuda_stream, 0)]
+
+
 def is_on():
     return dist.is_available() and dist.is_initialized()
 
@@ -32,23 +55,37 @@ def rank():
     return dist.get_rank() if is_on() else 0
 
 
+def collective():
+    """True when the step must issue its collectives (world > 1, or forced)."""
+    return is_on() and (world_size() > 1 or FORCE)
+
+
 def init_from_env(backend=None):
     """Initialise from torchrun's env (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT)."""
     ws = int(os.environ.get('WORLD_SIZE', '1'))
-    if ws <= 1 or is_on():
+    if (ws <= 1 and not FORCE) or is_on():
         install_syncbn_hook()
         return rank(), world_size()
     if backend is None:
         backend = os.environ.get('EEGAN_DIST_BACKEND') or ('nccl' if torch.cuda.is_available() else 'gloo')
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    os.environ.setdefault('MASTER_PORT', '29561')
+    os.environ.setdefault('RANK', '0')
+    os.environ.setdefault('WORLD_SIZE', '1')
     dist.init_process_group(backend=backend)
+    if backend == 'nccl' and os.environ.get('EEGAN_OWN_RCCL', '1') == '1':
+        from .rccl import Communicator
+        COMMS[:] = [Communicator(torch.cuda.current_device()) for _ in range(N_LANES)]
     install_syncbn_hook()
     return rank(), world_size()
 
 
 def install_syncbn_hook(group=None):
-    if is_on() and dist.get_world_size(group) > 1:
-        Fn.SYNC_BN_ALLREDUCE = lambda t: dist.all_reduce(t, group=group)
+    if is_on() and (dist.get_world_size(group) > 1 or FORCE):
+        if COMMS and group is None:
+            Fn.SYNC_BN_ALLREDUCE = all_reduce
+        else:
+            Fn.SYNC_BN_ALLREDUCE = lambda t: dist.all_reduce(t, group=group)
         Fn.SYNC_BN_WORLD = dist.get_world_size(group)
     else:
         Fn.SYNC_BN_ALLREDUCE = None
@@ -63,27 +100,41 @@ class AllGatherFn(torch.autograd.Function):
     def forward(ctx, x):
         ws = world_size()
         x = x.contiguous()
-        out = [torch.empty_like(x) for _ in range(ws)]
-        dist.all_gather(out, x)
         ctx.n = x.shape[0]
         ctx.r = rank()
-        return torch.cat(out, 0)
+        return _gather(x)
 
     @staticmethod
     def backward(ctx, g):
         g = g.contiguous()
-        dist.all_reduce(g)
+        all_reduce(g)
         return g[ctx.r * ctx.n:(ctx.r + 1) * ctx.n]
 
 
+def all_reduce(t):
+    """In-place sum over ranks (own RCCL communicator for device tensors)."""
+    c = comm() if t.is_cuda and t.is_contiguous() else None
+    if c is not None:
+        c.all_reduce(t)
+    else:
+        dist.all_reduce(t)
+
+
+def _gather(x):
+    c = comm() if x.is_cuda else None
+    if c is not None:
+        return c.all_gather(x)
+    out = [torch.empty_like(x) for _ in range(world_size())]
+    dist.all_gather(out, x)
+    return torch.cat(out, 0)
+
+
 def all_gather(x, differentiable=True):
-    if world_size() == 1:
+    if not collective():
         return x
     if differentiable and x.requires_grad:
         return AllGatherFn.apply(x)
-    out = [torch.empty_like(x.contiguous()) for _ in range(world_size())]
-    dist.all_gather(out, x.contiguous())
-    return torch.cat(out, 0)
+    return _gather(x.contiguous())
 
 
 class GradReducer(object):

@@ -726,7 +726,7 @@ class LinearFn(torch.autograd.Function):
 
 # =========================================================== SyncBN path ===
 def _allreduce_f64(t):
-    if SYNC_BN_ALLREDUCE is not None and SYNC_BN_WORLD > 1:
+    if SYNC_BN_ALLREDUCE is not None:  # installed by eegan_hip.dist for world > 1 (or a forced rehearsal)
         SYNC_BN_ALLREDUCE(t)
 
 

@@ -81,11 +81,17 @@ class FlatAdam(torch.optim.Optimizer):
 
     def _allreduce(self):
         import torch.distributed as dist
-        if self.process_group is None or not dist.is_initialized() or dist.get_world_size(self.process_group) == 1:
+        from . import dist as D
+        if self.process_group is None or not dist.is_initialized() or (
+                dist.get_world_size(self.process_group) == 1 and not D.FORCE):
             return
         world = dist.get_world_size(self.process_group)
+        world_pg = self.process_group is dist.group.WORLD
         for s in range(0, self.numel, self.bucket_elems):
-            dist.all_reduce(self.gflat[s:s + self.bucket_elems], group=self.process_group)
+            if world_pg:
+                D.all_reduce(self.gflat[s:s + self.bucket_elems])
+            else:
+                dist.all_reduce(self.gflat[s:s + self.bucket_elems], group=self.process_group)
         self.gflat.mul_(1.0 / world)
 
     @torch.no_grad()

@@ -64,6 +64,8 @@ class Trainer(object):
             return [None] * n
         if self._streams is None or len(self._streams) < n:
             self._streams = [torch.cuda.Stream(device=self.device) for _ in range(n)]
+            for i, st in enumerate(self._streams):
+                D.bind_stream(st, i)   # one RCCL communicator per stream lane
         main = torch.cuda.current_stream()
         for s in self._streams[:n]:
             s.wait_stream(main)
@@ -149,7 +151,7 @@ class Trainer(object):
                    image_encoder):
         """train.py:419-435 over the GLOBAL batch when data-parallel."""
         region_features, cnn_code = image_encoder(fake_imgs)
-        if self.damsm_global and D.world_size() > 1:
+        if self.damsm_global and D.collective():
             region_features = D.all_gather(region_features)
             cnn_code = D.all_gather(cnn_code)
             sent_emb = D.all_gather(sent_emb, differentiable=False)
@@ -304,8 +306,12 @@ class StepGraph(object):
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
         prev, Fn.TIMER = Fn.TIMER, timer
+        # with a process group the RCCL collectives (SyncBN statistics, DAMSM
+        # gathers, gradient buckets) are captured too; thread-local capture
+        # keeps the process group's watchdog thread from invalidating it
+        mode = 'thread_local' if D.collective() else 'global'
         try:
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, capture_error_mode=mode):
                 self.out = trainer.train_step(batch, **step_kw)
         finally:
             Fn.TIMER = prev
