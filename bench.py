@@ -134,7 +134,7 @@ def main():
     ap.add_argument('--no-timer', action='store_true', help='diagnostic: skip the roofline timing pass')
     ap.add_argument('--timing-steps', type=int, default=2, help='eager steps of the roofline timing pass')
     ap.add_argument('--graph', default='auto', choices=['auto', 'on', 'off'],
-                    help='replay the step as one captured HIP graph (auto: on for a single GPU)')
+                    help='replay the step as one captured HIP graph (auto: on; N > 1 needs the own RCCL communicators)')
     args = ap.parse_args()
 
     from eegan_hip import dist as D

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 1
+#define EEGAN_ABI_VERSION 2  /* 2: fp32 conv weights channels-last */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
