@@ -554,7 +554,7 @@ EE_DEV void lds_dma16s(rsrc_t rsrc, int lds_addr, unsigned voff, int soff) {
                : "memory", "m0");
 }
 
-template <int MODE, int TCO, int TPIX, int KS = 1, int S = CONV_STAGES>
+template <int MODE, int TCO, int TPIX, int KS = 1, int S = CONV_STAGES, int VAR = 0>
 __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_bytes, long w_bytes) {
   constexpr int WCO = TCO >= 64 ? 2 : 1, WPIX = 4 / WCO;
   constexpr int WT_CO = TCO / WCO, WT_PIX = TPIX / WPIX;
@@ -695,7 +695,55 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
 #pragma unroll
   for (int st = 0; st < S - KS; ++st)
     if (st < nk) issue(st);
-  for (int it = 0; it < nk; it += KS) {
+  auto rd_frags = [&](int stage, bf16x8_t (&fa_)[FI], bf16x8_t (&fb_)[FJ]) {
+    const bf16_t* base = lds + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const int row = wi * WT_CO + i * 16 + fr;
+      fa_[i] = as_frag(*reinterpret_cast<const uint4*>(base + row * BK + ((fq ^ swz_b128((row >> 2) & 3)) * 8)));
+    }
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const int row = wj * WT_PIX + j * 16 + fr;
+      fb_[j] = as_frag(
+          *reinterpret_cast<const uint4*>(base + TCO * BK + row * BK + ((fq ^ swz_b128((row >> 2) & 3)) * 8)));
+    }
+  };
+  int it0 = 0;
+  if (VAR == 2 && KS == 2) {
+    // straight-line pairs: the second stage's fragment reads interleaved with
+    // the first stage's MFMAs (sched_group_barrier), so their LDS latency hides
+    for (; it0 + 1 < nk; it0 += 2) {
+      if (it0 + S - 2 <= nk) {
+        if (a_wave) wait_vmcnt_barrier<YNG * (A_INS + B_INS)>();
+        else wait_vmcnt_barrier<YNG * B_INS>();
+      } else {
+        wait_vmcnt_barrier<0>();
+      }
+      if (it0 + S - 2 < nk) issue((it0 + S - 2) % S);
+      if (it0 + S - 1 < nk) issue((it0 + S - 1) % S);
+      bf16x8_t fa0[FI], fb0[FJ], fa1[FI], fb1[FJ];
+      rd_frags(it0 % S, fa0, fb0);
+      rd_frags((it0 + 1) % S, fa1, fb1);
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[i], fb0[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < FI + FJ; ++r) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+      for (int r = 0; r < FI + FJ; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * FI * FJ - (FI + FJ), 0);
+    }
+  }
+  for (int it = it0; it < nk; it += KS) {
     if (it + S - KS <= nk) {
       if (a_wave) wait_vmcnt_barrier<YNG * (A_INS + B_INS)>();
       else wait_vmcnt_barrier<YNG * B_INS>();
@@ -1427,7 +1475,7 @@ template <int MODE>
 int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src_bytes) {
   Plan p = plan_igemm(a, Pc_max);
   a.noload = env_int("EEGAN_CONV_NOLOAD", 0);
-  const int ksv = env_int("EEGAN_CONV_KS", 2);  // K-steps per barrier (1: sweep baseline)
+  const int ksv = env_int("EEGAN_CONV_KS", 22);  // 22: pairs, interleaved reads; 2: pairs; 1: single steps
   a.nsplit = p.nsplit;
   a.part = p.nsplit > 1 ? part_ws : nullptr;
   if (p.nsplit > 1 && !part_ws) {
@@ -1439,7 +1487,8 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
 #define GL(TC, TP) ee_launch(conv_glds_kernel<MODE, TC, TP>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
 #define FA(TC, TP)                                                                                          \
   do {                                                                                                       \
-    if (ksv == 2) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 4>, grid, dim3(256), 0, s, a, src_bytes, w_bytes);      \
+    if (ksv == 22) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 4, 2>, grid, dim3(256), 0, s, a, src_bytes, w_bytes); \
+    else if (ksv == 2) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 4>, grid, dim3(256), 0, s, a, src_bytes, w_bytes); \
     else ee_launch(conv_fast_kernel<MODE, TC, TP, 1, 4>, grid, dim3(256), 0, s, a, src_bytes, w_bytes);                     \
   } while (0)
 #define IG(TC, TP, WC) ee_launch(conv_igemm_kernel<MODE, TC, TP, WC>, grid, dim3(256), 0, s, a)
