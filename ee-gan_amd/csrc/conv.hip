@@ -1276,7 +1276,50 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fast_kernel(WgradArgs w, lo
 #pragma unroll
   for (int st = 0; st < S - KS; ++st)
     if (st < nk) issue(st, st);
-  for (int it = 0; it < nk; it += KS) {
+  int it0 = 0;
+  if (KS == 2) {
+    // straight-line pairs, second stage's fragment reads interleaved with the
+    // first stage's MFMAs (as conv_fast_kernel)
+    for (; it0 + 1 < nk; it0 += 2) {
+      if (it0 + S - 2 <= nk) {
+        if (d_wave) wait_vmcnt_barrier<YNG * (D_INS + X_INS)>();
+        else wait_vmcnt_barrier<YNG * X_INS>();
+      } else {
+        wait_vmcnt_barrier<0>();
+      }
+      if (it0 + S - 2 < nk) issue(it0 + S - 2, (it0 + S - 2) % S);
+      if (it0 + S - 1 < nk) issue(it0 + S - 1, (it0 + S - 1) % S);
+      bf16x8_t fa0[FI], fb0[FJ], fa1[FI], fb1[FJ];
+      const bf16_t* b0 = lds + (it0 % S) * STAGE;
+      const bf16_t* b1 = lds + ((it0 + 1) % S) * STAGE;
+#pragma unroll
+      for (int i = 0; i < FI; ++i) fa0[i] = tr_frag(b0, DSH, wi * WT_CO + i * 16, dswz);
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) fb0[j] = tr_frag(b0 + BK * TCO, XSH, wj * WT_K + j * 16, xswz);
+#pragma unroll
+      for (int i = 0; i < FI; ++i) fa1[i] = tr_frag(b1, DSH, wi * WT_CO + i * 16, dswz);
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) fb1[j] = tr_frag(b1 + BK * TCO, XSH, wj * WT_K + j * 16, xswz);
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[i], fb0[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
+      // each transposed fragment is two ds_read_b64_tr_b16
+#pragma unroll
+      for (int r = 0; r < 2 * (FI + FJ); ++r) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+      for (int r = 0; r < FI + FJ; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * FI * FJ - (FI + FJ), 0);
+    }
+  }
+  for (int it = it0; it < nk; it += KS) {
     if (it + S - KS <= nk) {
       if (d_wave) wait_vmcnt_barrier<YNG * (D_INS + X_INS)>();
       else wait_vmcnt_barrier<YNG * X_INS>();
