@@ -604,6 +604,33 @@ class DotFn(torch.autograd.Function):
         return gx, gy
 
 
+class BatchCatFn(torch.autograd.Function):
+    """torch.cat(parts, 0) for NHWC bf16 activations (same C, H, W): one copy
+    per part into a fresh NHWC buffer; the backward returns views of the
+    gradient (differentiable slicing)."""
+
+    @staticmethod
+    def forward(ctx, *parts):
+        parts = [to_nhwc_bf16(p) for p in parts]
+        N0, C, H, W = parts[0].shape
+        ns = [p.shape[0] for p in parts]
+        out = empty_nhwc(sum(ns), C, H, W, parts[0].device)
+        o = 0
+        for p, n in zip(parts, ns):
+            out[o:o + n].copy_(p)
+            o += n
+        ctx.ns = ns
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        outs, o = [], 0
+        for n in ctx.ns:
+            outs.append(g[o:o + n])
+            o += n
+        return tuple(outs)
+
+
 class CatTileFn(torch.autograd.Function):
     """torch.cat((feat, cond.view(-1,E,1,1).repeat(1,1,H,W)), 1) (models.py:302-304, 327-331)."""
 

@@ -93,9 +93,28 @@ class Trainer(object):
         return optG, optDs
 
     # ------------------------------------------------------------ losses --
+    # D has no batch-coupled layer, so the real and fake passes of d_loss (and
+    # the real / mismatch / fake heads) run as ONE batch: the same per-sample
+    # outputs and summed gradients as train.py's separate calls, half the
+    # trunk launches and twice the work per launch (EEGAN_DBATCH=0: separate)
+    DBATCH = os.environ.get('EEGAN_DBATCH', '1') != '0'
+
+    @staticmethod
+    def _d_heads_batched(imgs, fake_imgs, sent_emb, wrong_sent_emb, netD):
+        B = imgs.shape[0]
+        feat = netD(Fn.BatchCatFn.apply(imgs, fake_imgs.detach()))
+        real, fake = feat[:B], feat[B:]
+        heads = Fn.BatchCatFn.apply(real, real, fake)
+        cond = torch.cat([sent_emb.reshape(B, -1), wrong_sent_emb.reshape(B, -1), sent_emb.reshape(B, -1)], 0)
+        return netD.module.COND_DNET(heads, cond), B
+
     @staticmethod
     def d_loss(imgs, fake_imgs, sent_emb, wrong_sent_emb, netD):
         """train.py:336-353."""
+        if Trainer.DBATCH:
+            out, B = Trainer._d_heads_batched(imgs, fake_imgs, sent_emb, wrong_sent_emb, netD)
+            return (Fn.DoutReduceFn.apply(out[:B], 0), Fn.DoutReduceFn.apply(out[2 * B:], 1),
+                    Fn.DoutReduceFn.apply(out[B:2 * B], 1))
         real_features = netD(imgs)
         real_out = netD.module.COND_DNET(real_features, sent_emb)
         errD_real = Fn.DoutReduceFn.apply(real_out, 0)
@@ -109,6 +128,12 @@ class Trainer(object):
     @staticmethod
     def d_loss_class(imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, netD):
         """train.py:355-376."""
+        if Trainer.DBATCH:
+            (sent_out, class_out), B = Trainer._d_heads_batched(imgs, fake_imgs, sent_emb, unpair_sent_emb, netD)
+            return (Fn.DoutReduceFn.apply(sent_out[:B], 0), Fn.DoutReduceFn.apply(sent_out[2 * B:], 1),
+                    Fn.DoutReduceFn.apply(sent_out[B:2 * B], 1), Fn.BceLogitsFn.apply(class_out[:B], class_labels),
+                    Fn.BceLogitsFn.apply(class_out[2 * B:], class_labels),
+                    Fn.BceLogitsFn.apply(class_out[B:2 * B], class_labels))
         real_feature = netD(imgs)
         real_sent_out, real_class_out = netD.module.COND_DNET(real_feature, sent_emb)
         errD_real = Fn.DoutReduceFn.apply(real_sent_out, 0)
