@@ -276,6 +276,19 @@ class Trainer(object):
     def encode_text(self, batch):
         """train.py:169-184: 5 frozen text-encoder calls (captions, 3 attributes, unpaired)."""
         enc = self.text_encoder
+        caps, ucaps = batch['caps'], batch['unpair_caps']
+        if batch.get('max_len') is not None and caps.shape == ucaps.shape:
+            # the frozen encoder is per-caption: captions + unpaired captions as
+            # one batch, the three attribute phrases as another (2 calls, not 5)
+            B = caps.shape[0]
+            with torch.no_grad():
+                w2, s2 = enc(torch.cat([caps, ucaps], 0), torch.cat([batch['cap_lens'].reshape(-1),
+                                                                     batch['unpair_cap_lens'].reshape(-1)], 0),
+                             None, max_len=batch['max_len'])
+                at = batch['attrs'][:, :self.max_attr_nums, :]
+                _, sa = enc(at.reshape(B * at.shape[1], at.shape[2]), batch['attrs_len'][:, :self.max_attr_nums].reshape(-1),
+                            None, max_len=at.shape[2])
+            return w2[:B], s2[:B], sa.reshape(B, at.shape[1], -1), s2[B:]
         with torch.no_grad():
             words, sent = enc(batch['caps'], batch['cap_lens'], None, max_len=batch.get('max_len'))
             attrs = []

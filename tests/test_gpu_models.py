@@ -272,6 +272,12 @@ def test_rnn_encoder(gpu):
     w, s = enc(caps, lens, enc.init_hidden(4))
     _check('rnn/words', w, g['rnn/words'], 1e-5)
     _check('rnn/sent', s, g['rnn/sent'], 1e-5)
+    # the Trainer encodes captions + unpaired captions (and the attribute
+    # phrases) as one batch: per-caption results must not depend on batching
+    T = int(lens.max())
+    w2, s2 = enc(torch.cat([caps, caps.flip(0)]), torch.cat([lens, lens.flip(0)]), None, max_len=T)
+    assert torch.equal(w2[:4], w) and torch.equal(s2[:4], s)
+    assert torch.equal(s2[4:], s.flip(0))
 
 
 def test_cnn_encoder_vs_oracle(gpu):
