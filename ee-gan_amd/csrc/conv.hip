@@ -1475,6 +1475,272 @@ __global__ __launch_bounds__(256) void pack_weights_multi_kernel(const long* __r
   }
 }
 
+// ------------------------------------------------------------ thin convs --
+// 3x3 stride-1 convs with <= 32 output rows: the stem conv_img (3 -> ndf) of
+// models.py:313/330/348, get_image (ngf -> 3) of models.py:25-32, the
+// 32-channel convs of the 256x256 stage, and their data gradients (which are
+// again 3x3 stride-1 convs with <= 32 output rows).  These are all big-image,
+// few-channel shapes on which the tile kernels spend their time in
+// prologue / epilogue / barriers.  Here a wave keeps the whole packed weight
+// slab (NT x NKS A fragments) in VGPRs for its lifetime and streams groups of
+// 16 output pixels: each B fragment (8 channels of one tap of one pixel, 16 B)
+// is loaded straight from global memory into the lane that feeds it to the
+// MFMA -- no LDS, no barriers.  Blocks own contiguous pixel ranges and the
+// blocks of one XCD own adjacent ranges, so the 3x3 halo re-reads hit that
+// XCD's L2.  K layout = the packed weight row: NKS == 3 is the packed mode
+// (Cgp == 8, 4 taps x 8 channels per K step), otherwise tap-major 32-channel
+// slices.
+template <int MODE, int NT, int NKS, int GPI>
+__global__ __launch_bounds__(256) void conv_thin_kernel(ConvArgs a, int iters_per_block, int src_bytes) {
+  constexpr bool PACKED = (NKS == 3);
+  constexpr int NC = PACKED ? 1 : NKS / 9;
+  const int lane = threadIdx.x & 63, kg = lane >> 4, col = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (b & 7) * (nb >> 3) + (b >> 3);  // XCD-contiguous logical block (nb % 8 == 0)
+  // OOB offsets read zeros: padding taps, image borders and tail pixels need no branches
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, src_bytes, 0x00020000);
+  bf16x8_t fa[NT][NKS];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      fa[t][ks] = as_frag(*reinterpret_cast<const uint4*>(a.wp + (long)(16 * t + col) * a.Kw + 32 * ks + 8 * kg));
+  float bia[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = 16 * t + 4 * kg + r;
+      bia[t][r] = (a.bias && co < a.Mrows) ? a.bias[co] : 0.f;
+    }
+  // per-lane tap geometry of every K step (block-invariant)
+  int t_dy[NKS], t_dx[NKS], t_c[NKS];
+  bool t_ok[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int tap = PACKED ? 4 * ks + kg : ks / NC;
+    const int c = PACKED ? 0 : (ks % NC) * 32 + 8 * kg;
+    t_ok[ks] = tap < 9 && c < a.Cvalid;  // chunks past the valid channels are never read
+    const int r = tap / 3, s = tap - 3 * (tap / 3);
+    t_dy[ks] = MODE == MODE_FWD ? r - a.ph : a.ph - r;
+    t_dx[ks] = MODE == MODE_FWD ? s - a.pw : a.pw - s;
+    t_c[ks] = c;
+  }
+  const int PH = a.IH >> a.up2, PW = a.IW >> a.up2, hw = a.OH * a.OW;
+  // packed mode: every chunk starts at channel 0, so one lane mask zeroes the
+  // channels >= Cvalid (other modes require Cvalid % 8 == 0).  Applied with
+  // ANDs after all loads were issued: a branch per load would make the
+  // compiler drain vmcnt after every load.
+  const uint4 cmask = mask_chunk(make_uint4(~0u, ~0u, ~0u, ~0u), 0, PACKED ? a.Cvalid : 8);
+  const bool rows16 = (a.OW & 15) == 0;  // a 16-pixel group never wraps a row: scalar decomposition
+  const int it0 = lb * iters_per_block, it_end = it0 + iters_per_block;
+  // issue the loads of iteration `it` (iterations past the end load zeros)
+  auto load = [&](uint4 (&bv)[GPI][NKS], int (&pp)[GPI], int it) {
+#pragma unroll
+    for (int g = 0; g < GPI; ++g) {
+      const int base = (it * GPI + g) * 16;
+      int n, y, x;
+      if (rows16) {
+        const int n0 = base / hw, rem = base - n0 * hw;
+        const int y0 = rem / a.OW;
+        n = n0;
+        y = y0;
+        x = rem - y0 * a.OW + col;
+      } else {
+        const int p = min(base + col, a.P - 1);
+        n = p / hw;
+        const int rem = p - n * hw;
+        y = rem / a.OW;
+        x = rem - y * a.OW;
+      }
+      pp[g] = (it < it_end && base + col < a.P) ? base + col : -1;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const int iy = y + t_dy[ks], ix = x + t_dx[ks];
+        const bool ok = pp[g] >= 0 && t_ok[ks] && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
+        const int off = (((n * PH + (iy >> a.up2)) * PW + (ix >> a.up2)) * a.lds_src + t_c[ks]) * 2;
+        bv[g][ks] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? off : 0x80000000, 0, 0));
+      }
+    }
+  };
+  auto compute = [&](uint4 (&bv)[GPI][NKS], const int (&pp)[GPI]) {
+#pragma unroll
+    for (int g = 0; g < GPI; ++g) {
+      if (PACKED) {
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          bv[g][ks].x &= cmask.x;
+          bv[g][ks].y &= cmask.y;
+          bv[g][ks].z &= cmask.z;
+          bv[g][ks].w &= cmask.w;
+        }
+      }
+      f32x4_t acc[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t][ks], as_frag(bv[g][ks]), acc[t], 0, 0, 0);
+      if (pp[g] < 0) continue;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int co = 16 * t + 4 * kg;
+        if (co >= a.Mrows) continue;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = act_fwd(acc[t][r] + bia[t][r], a.act, a.slope);
+        bf16_t* op = reinterpret_cast<bf16_t*>(a.out) + (long)pp[g] * a.ldo + co;
+        if (co + 4 <= a.Mrows) {
+          *reinterpret_cast<uint2*>(op) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (co + r < a.Mrows) op[r] = f2bf(v[r]);
+        }
+      }
+    }
+  };
+  // two register stages: the loads of the wave's next iteration are in flight
+  // while this one's MFMAs and stores run (unconditional, zero-filled past the end)
+  uint4 b0[GPI][NKS], b1[GPI][NKS];
+  int p0[GPI], p1[GPI];
+  int it = it0 + wv;
+  load(b0, p0, it);
+  for (; it < it_end; it += 8) {
+    load(b1, p1, it + 4);
+    compute(b0, p0);
+    if (it + 4 >= it_end) break;
+    load(b0, p0, it + 8);
+    compute(b1, p1);
+  }
+}
+
+// LDS-tiled variant of conv_thin_kernel for OW % 64 == 0 (the 64..256-wide
+// images): a block stages an (8 + 2) x (64 + 2)-pixel input halo tile in LDS
+// by LDS-DMA and reads every tap's B fragment from there, instead of gathering
+// each pixel nine times through L2 (which bounds the direct kernel at the L2
+// gather rate, ~28 B/clk per CU).  No staging registers, so 3 blocks fit a CU
+// and overlap one block's halo fill with the others' MFMAs; persistent blocks
+// walk XCD-contiguous tile ranges.  64-B pixel rows use the chunk swizzle
+// c ^ ((pix >> 1) & 2), conflict-free for ds_read_b128 windows of 16 pixels at
+// any start (tap shifts); the DMA lanes fetch in swizzled order.
+template <int MODE, int NT, int NKS>
+__global__ __launch_bounds__(256, 3) void conv_thin_lds_kernel(ConvArgs a, int src_bytes, int tiles_per_block) {
+  constexpr bool PACKED = (NKS == 3);
+  constexpr int NCH = PACKED ? 1 : 4;  // 16-B chunks per staged pixel
+  constexpr int TW = 64, TH = 8, PWT = TW + 2, NPIX = (TH + 2) * PWT, NCHUNK = NPIX * NCH;
+  constexpr int NDMA = (NCHUNK + 255) / 256;  // DMA pieces per thread (tail lanes fill padding)
+  __shared__ uint4 tile[NDMA * 256];
+  const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4, col = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (b & 7) * (nb >> 3) + (b >> 3);
+  const rsrc_t rsv = make_rsrc(a.src, src_bytes);
+  bf16x8_t fa[NT][NKS];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      fa[t][ks] = as_frag(*reinterpret_cast<const uint4*>(a.wp + (long)(16 * t + col) * a.Kw + 32 * ks + 8 * kg));
+  float bia[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = 16 * t + 4 * kg + r;
+      bia[t][r] = (a.bias && co < a.Mrows) ? a.bias[co] : 0.f;
+    }
+  // tile origin relative to the output tile: FWD reads rows y - ph .. y - ph + 2,
+  // BWDD (stride 1) reads dy rows y + ph - 2 .. y + ph
+  const int org_y = MODE == MODE_FWD ? -a.ph : a.ph - 2, org_x = MODE == MODE_FWD ? -a.pw : a.pw - 2;
+  int t_off[NKS], t_ch[NKS];
+  bool t_ok[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int tap = PACKED ? 4 * ks + kg : ks;
+    const int r = tap / 3, s = tap - 3 * (tap / 3);
+    t_ok[ks] = tap < 9;
+    t_off[ks] = (MODE == MODE_FWD ? r : 2 - r) * PWT + (MODE == MODE_FWD ? s : 2 - s);
+    t_ch[ks] = PACKED ? 0 : kg;
+  }
+  // packed mode stages whole 8-channel pixels; channels >= Cvalid are zeroed
+  // when the fragments are read (the DMA cannot mask)
+  const uint4 cmask = mask_chunk(make_uint4(~0u, ~0u, ~0u, ~0u), 0, PACKED ? a.Cvalid : 8);
+  const int PH = a.IH >> a.up2, PWp = a.IW >> a.up2;
+  const int tiles_x = a.OW / TW, tiles_y = (a.OH + TH - 1) / TH, tiles = a.N * tiles_x * tiles_y;
+  const int t0 = lb * tiles_per_block, t1 = min(t0 + tiles_per_block, tiles);
+  for (int tt = t0; tt < t1; ++tt) {
+    const int n = tt / (tiles_x * tiles_y), rem = tt - n * tiles_x * tiles_y;
+    const int y0 = (rem / tiles_x) * TH, x0 = (rem - (rem / tiles_x) * tiles_x) * TW;
+    __syncthreads();  // the previous tile's fragment reads are done
+#pragma unroll
+    for (int i = 0; i < NDMA; ++i) {
+      const int sl = i * 256 + wv * 64 + lane;  // LDS slot this lane's piece lands in
+      const int pix = sl / NCH, phys = sl - pix * NCH;
+      const int ch = NCH == 4 ? (phys ^ ((pix >> 1) & 2)) : 0;
+      const int pr = pix / PWT, pq = pix - pr * PWT;
+      const int iy = y0 + org_y + pr, ix = x0 + org_x + pq;
+      const bool ok = sl < NCHUNK && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
+      const int off = (((n * PH + (iy >> a.up2)) * PWp + (ix >> a.up2)) * a.lds_src + ch * 8) * 2;
+      lds_dma16(rsv, &tile[i * 256 + wv * 64], ok ? (unsigned)off : 0x80000000u);
+    }
+    wait_vmcnt_barrier<0>();
+#pragma unroll 1
+    for (int j = 0; j < TH / 4; ++j) {
+      const int rr = wv * (TH / 4) + j;
+#pragma unroll 2
+      for (int g = 0; g < TW / 16; ++g) {
+        const int q = 16 * g + col;
+        uint4 bv[NKS];
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          const int pix = rr * PWT + q + t_off[ks];
+          bv[ks] = tile[pix * NCH + (NCH == 4 ? (t_ch[ks] ^ ((pix >> 1) & 2)) : 0)];
+        }
+        f32x4_t acc[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          uint4 v = bv[ks];
+          if (PACKED) {
+            v.x &= cmask.x;
+            v.y &= cmask.y;
+            v.z &= cmask.z;
+            v.w &= cmask.w;
+          }
+          if (!t_ok[ks]) v = make_uint4(0, 0, 0, 0);
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t][ks], as_frag(v), acc[t], 0, 0, 0);
+        }
+        const int y = y0 + rr;
+        if (y >= a.OH) continue;
+        const long p = ((long)n * a.OH + y) * a.OW + x0 + q;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int co = 16 * t + 4 * kg;
+          if (co >= a.Mrows) continue;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = act_fwd(acc[t][r] + bia[t][r], a.act, a.slope);
+          bf16_t* op = reinterpret_cast<bf16_t*>(a.out) + p * a.ldo + co;
+          if (co + 4 <= a.Mrows) {
+            *reinterpret_cast<uint2*>(op) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (co + r < a.Mrows) op[r] = f2bf(v[r]);
+          }
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------ dispatch --
 int cgp_of(int C) { return C <= 8 ? 8 : ee_round_up(C, BK); }
 int kw_of(int R, int S, int Cgp) { return ee_round_up(R * S * Cgp, BK); }
@@ -1514,8 +1780,42 @@ Plan plan_igemm(const ConvArgs& a, int Pc_max) {
   return p;
 }
 
+// 3x3 stride-1 convs with <= 32 output rows take conv_thin_kernel.  Returns
+// 0 when the shape is not eligible (the tile kernels run), else the launch rc.
+template <int MODE>
+int try_thin(const ConvArgs& a, hipStream_t s, long src_bytes) {
+  if (!env_int("EEGAN_CONV_THIN", 1) || src_bytes >= 0x7fffffffL) return 0;
+  if (a.R != 3 || a.S != 3 || a.st != 1 || a.ncls != 1 || a.res || a.out_f32 || a.Mrows > 32) return 0;
+  if ((a.ldo & 3) || ((uintptr_t)a.out & 7) || (a.lds_src & 7) || ((uintptr_t)a.src & 15)) return 0;
+  const int nt = a.Mrows > 16 ? 2 : 1;
+  const int nks = a.Cgp == 8 ? 3 : a.Cgp == 32 ? 9 : (a.Cgp == 64 && nt == 1) ? 18 : 0;
+  if (!nks || (nks > 3 && (a.Cvalid & 7))) return 0;
+  const int gpi = nks == 3 ? 2 : 1;
+  const long iters = ((a.P + 15L) / 16 + gpi - 1) / gpi;
+  const int nb = ee_round_up((int)std::min<long>((iters + 3) / 4, 1024), 8);
+  const int ipb = (int)((iters + nb - 1) / nb);
+  if (nks <= 9 && a.OW % 64 == 0 && a.ph <= 1 && a.pw <= 1 && env_int("EEGAN_CONV_THIN_LDS", 1)) {
+    const int tiles = a.N * (a.OW / 64) * ((a.OH + 7) / 8);
+    const int nbl = ee_round_up(std::min(tiles, nks == 3 ? 2048 : 768), 8), tpb = (tiles + nbl - 1) / nbl;
+#define TL(NT, NKS) ee_launch(conv_thin_lds_kernel<MODE, NT, NKS>, dim3(nbl), dim3(256), 0, s, a, (int)src_bytes, tpb)
+    if (nks == 3) { if (nt == 1) TL(1, 3); else TL(2, 3); }
+    else { if (nt == 1) TL(1, 9); else TL(2, 9); }
+#undef TL
+    const int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd(thin-lds)" : "conv_bwd_data(thin-lds)");
+    return rc ? rc : 1;
+  }
+#define TH(NT, NKS, G) ee_launch(conv_thin_kernel<MODE, NT, NKS, G>, dim3(nb), dim3(256), 0, s, a, ipb, (int)src_bytes)
+  if (nks == 3) { if (nt == 1) TH(1, 3, 2); else TH(2, 3, 2); }
+  else if (nks == 9) { if (nt == 1) TH(1, 9, 1); else TH(2, 9, 1); }
+  else TH(1, 18, 1);
+#undef TH
+  const int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd(thin)" : "conv_bwd_data(thin)");
+  return rc ? rc : 1;
+}
+
 template <int MODE>
 int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src_bytes) {
+  if (const int th = try_thin<MODE>(a, s, src_bytes)) return th > 0 ? 0 : th;
   Plan p = plan_igemm(a, Pc_max);
   a.noload = env_int("EEGAN_CONV_NOLOAD", 0);
   const int ksv = env_int("EEGAN_CONV_KS", 22);  // 22: pairs, interleaved reads; 2: pairs; 1: single steps

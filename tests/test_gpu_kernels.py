@@ -84,6 +84,48 @@ def test_conv_fast_path_matches_generic(gpu, monkeypatch):
             assert torch.equal(a, b)
 
 
+def test_conv_thin_path_matches_tile(gpu, monkeypatch):
+    """3x3 stride-1 convs with <= 32 output rows (stem, get_image, 32-channel
+    256x256 convs and their data gradients) take the weight-stationary thin
+    kernel (EEGAN_CONV_THIN=1, default): same K steps in the same order as the
+    tile kernels, so bit-identical; also checked against torch fp32."""
+    Fn, T, _ = _mods()
+    for N, Cin, H, W, Cout, pad, up2, bias, act in [
+            (2, 3, 20, 24, 32, 1, 0, True, 0), (2, 32, 20, 24, 3, 1, 0, False, 3),
+            (2, 32, 17, 15, 32, 1, 0, False, 2), (3, 64, 9, 13, 16, 1, 0, False, 0),
+            (2, 32, 13, 11, 32, 0, 0, False, 0), (2, 32, 16, 20, 24, 1, 1, False, 1),
+            (1, 5, 7, 9, 12, 1, 0, True, 0),
+            # OW % 64 == 0: the LDS halo-tile variant (partial last tile row: H % 8 != 0)
+            (2, 3, 13, 128, 32, 1, 0, True, 0), (2, 32, 10, 64, 3, 1, 0, False, 3),
+            (1, 32, 16, 64, 32, 1, 0, False, 2), (1, 32, 11, 66, 20, 0, 0, False, 0),
+            (1, 32, 16, 128, 32, 1, 1, False, 1), (1, 7, 8, 64, 16, 1, 0, False, 0)]:
+        torch.manual_seed(N * Cin + H + Cout)
+        g = Fn.Geom(Cout, 3, 3, 1, pad, pad, up2)
+        xl = torch.randn(N, Cin, H // 2 if up2 else H, W // 2 if up2 else W)
+        x = _nhwc(xl, gpu)
+        Wt = _bf(torch.randn(Cout, Cin, 3, 3) * 0.1).to(gpu)
+        b = torch.randn(Cout).to(gpu) if bias else None
+        Ho, Wo = g.out_hw(H, W)
+        dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
+        outs = []
+        for thin in ('0', '1'):
+            monkeypatch.setenv('EEGAN_CONV_THIN', thin)
+            o = [Fn.conv_fwd_raw(x, Wt, b, g, act=act).float().cpu()]
+            if not up2:
+                o.append(Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape)).float().cpu())
+            outs.append(o)
+        for a, c in zip(*outs):
+            assert torch.equal(a, c)
+        xin = F.interpolate(_bf(xl), scale_factor=2) if up2 else _bf(xl)
+        yr = F.conv2d(xin, Wt.cpu(), None if b is None else b.cpu(), 1, pad)
+        yr = {0: yr, 1: F.relu(yr), 2: F.leaky_relu(yr, 0.2), 3: torch.tanh(yr)}[act]
+        assert rel_l2(outs[1][0], yr) < 1e-2
+        if not up2:
+            xr = xin.clone().requires_grad_()
+            F.conv2d(xr, Wt.cpu(), None, 1, pad).backward(dz.float().cpu())
+            assert rel_l2(outs[1][1], xr.grad) < 1e-2
+
+
 @pytest.mark.parametrize('case', CONV_CASES, ids=[str(i) for i in range(len(CONV_CASES))])
 def test_conv_fwd_bwd(gpu, case):
     Fn, T, Conv2d = _mods()

@@ -34,6 +34,9 @@ SHAPES = {
     'c4x4s2_512_8': (16, 512, 8, 8, 512, 4, 2, 1),
     'c3x3_512_8': (16, 512, 8, 8, 512, 3, 1, 1),
     'c1x1_768_17': (16, 768, 17, 17, 192, 1, 1, 0),
+    'stem_3_256x32': (32, 3, 256, 256, 32, 3, 1, 1),
+    'img_32_256': (16, 32, 256, 256, 3, 3, 1, 1),
+    'c3x3_32_128': (16, 32, 128, 128, 32, 3, 1, 1),
 }
 
 

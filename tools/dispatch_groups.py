@@ -1,0 +1,44 @@
+"""Group the dispatches of a rocprofv3 kernel trace by (kernel, grid) and
+list the groups that take the most time per step, so the shapes worth
+tuning can be read off a graph-replayed bench run.
+
+    python tools/dispatch_groups.py TRACE_DIR --steps N [--filter conv] [--top 40]
+"""
+import argparse
+import csv
+import glob
+import os
+from collections import defaultdict
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('trace')
+    ap.add_argument('--steps', type=int, required=True)
+    ap.add_argument('--filter', default='')
+    ap.add_argument('--top', type=int, default=40)
+    args = ap.parse_args()
+    groups = defaultdict(lambda: [0, 0])
+    for path in glob.glob(os.path.join(args.trace, '**', '*kernel_trace.csv'), recursive=True):
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                name = r['Kernel_Name']
+                if args.filter and args.filter not in name:
+                    continue
+                short = name.replace('(anonymous namespace)::', '').replace('void ', '')
+                short = short.split('(')[0][:90]
+                grid = (r.get('Grid_Size_X', r.get('Grid_Size', '?')), r.get('Grid_Size_Y', ''),
+                        r.get('Grid_Size_Z', ''))
+                g = groups[(short, grid)]
+                g[0] += 1
+                g[1] += int(r['End_Timestamp']) - int(r['Start_Timestamp'])
+    rows = sorted(groups.items(), key=lambda kv: -kv[1][1])
+    tot = sum(v[1] for v in groups.values())
+    print('total %.3f ms/step over %d groups' % (tot * 1e-6 / args.steps, len(groups)))
+    for (k, grid), (n, ns) in rows[:args.top]:
+        print('%7.3f ms/step %5.1f calls/step %8.2f us  grid %-20s %s' % (
+            ns * 1e-6 / args.steps, n / args.steps, ns * 1e-3 / n, 'x'.join(x for x in grid if x), k))
+
+
+if __name__ == '__main__':
+    main()

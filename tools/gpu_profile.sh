@@ -16,5 +16,7 @@ step 900 prof_write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -
   python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --graph off --no-timer
 python3 tools/rocprof_families.py --trace $O/trace --fetch $O/fetch --write $O/write \
   --steps $((STEPS + 4)) --out $O/families.json > /dev/null
+python3 tools/dispatch_groups.py $O/trace --steps $((STEPS + 4)) --filter conv --top 60 > $O/conv_groups.txt
+python3 tools/dispatch_groups.py $O/trace --steps $((STEPS + 4)) --top 60 > $O/all_groups.txt
 for d in trace fetch write; do find $O/$d -name '*.csv' -size +20M -delete; done
 ls -la $O
