@@ -19,15 +19,14 @@ namespace {
 // coalesced one.
 constexpr int T = 16, KC = 256;
 
-__global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ A, long sai, long sak,
-                                                       const float* __restrict__ B, long sbk, long sbj,
-                                                       float* __restrict__ C, long ldc, int M, int N, int K,
-                                                       const float* __restrict__ bias, int act, float alpha,
-                                                       float beta) {
-  __shared__ float As[T][KC + 1];
-  __shared__ float Bs[KC][T + 1];
+// One 16x16 tile (i0, j0) of C = act(alpha * A B + bias) [* act'(gate)] (+ beta * C).
+// `gate` (optional) multiplies by the derivative of `gate_act` expressed
+// through that activation's output: dh = (dy W2) * relu'(h) in one pass.
+EE_DEV void gemm_tile(float (&As)[T][KC + 1], float (&Bs)[KC][T + 1], const float* __restrict__ A, long sai,
+                      long sak, const float* __restrict__ B, long sbk, long sbj, float* __restrict__ C, long ldc,
+                      int M, int N, int K, const float* __restrict__ bias, int act, float alpha, float beta,
+                      const float* __restrict__ gate, long ldg, int gate_act, int i0, int j0) {
   const int t = threadIdx.x, ti = t / T, tj = t % T;
-  const int i0 = blockIdx.y * T, j0 = blockIdx.x * T;
   const bool a_k_fast = sak == 1, b_j_fast = sbj == 1;
   float acc = 0.f;
   for (int k0 = 0; k0 < K; k0 += KC) {
@@ -60,9 +59,51 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
   if (gi < M && gj < N) {
     float v = alpha * acc + (bias ? bias[gj] : 0.f);
     v = act_fwd(v, act, 0.2f);
+    if (gate) v *= act_dgrad_from_y(gate[gi * ldg + gj], gate_act, 0.2f);
     float* dst = C + gi * ldc + gj;
     *dst = beta != 0.f ? beta * *dst + v : v;
   }
+}
+
+__global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ A, long sai, long sak,
+                                                       const float* __restrict__ B, long sbk, long sbj,
+                                                       float* __restrict__ C, long ldc, int M, int N, int K,
+                                                       const float* __restrict__ bias, int act, float alpha,
+                                                       float beta) {
+  __shared__ float As[T][KC + 1];
+  __shared__ float Bs[KC][T + 1];
+  gemm_tile(As, Bs, A, sai, sak, B, sbk, sbj, C, ldc, M, N, K, bias, act, alpha, beta, nullptr, 0, 0,
+            blockIdx.y * T, blockIdx.x * T);
+}
+
+// Grouped form: up to GMAX independent small GEMMs in one launch (the 28
+// affine_ssa MLPs of the generator run as 2 forward + 6 backward launches
+// instead of ~200).  Descriptors travel by value in the kernel arguments;
+// block b finds its GEMM through the tile prefix sums.
+constexpr int GMAX = 32;
+struct GemmDev {
+  const float *A, *B, *bias, *gate;
+  float* C;
+  int sai, sak, sbk, sbj, ldc, ldg, M, N, K, act, gate_act;
+  float alpha, beta;
+};
+struct GemmGroup {
+  GemmDev d[GMAX];
+  int tile0[GMAX + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const GemmGroup grp) {
+  __shared__ float As[T][KC + 1];
+  __shared__ float Bs[KC][T + 1];
+  const int b = blockIdx.x;
+  int g = 0;
+  while (g + 1 < grp.n && grp.tile0[g + 1] <= b) ++g;
+  const GemmDev& d = grp.d[g];
+  const int tl = b - grp.tile0[g], tn = (d.N + T - 1) / T;
+  const int ti = tl / tn, tj = tl - ti * tn;
+  gemm_tile(As, Bs, d.A, d.sai, d.sak, d.B, d.sbk, d.sbj, d.C, d.ldc, d.M, d.N, d.K, d.bias, d.act, d.alpha,
+            d.beta, d.gate, d.ldg, d.gate_act, ti * T, tj * T);
 }
 
 // column sums: out[j] (+)= sum_i X[i*ld + j]   (Linear bias gradient)
@@ -90,6 +131,34 @@ int eegan_gemm_f32(const float* A, long sai, long sak, const float* B, long sbk,
   dim3 grid(ee_cdiv(N, T), ee_cdiv(M, T));
   ee_launch(gemm_f32_kernel, grid, dim3(256), 0, s, A, sai, sak, B, sbk, sbj, C, ldc, M, N, K, bias, act, alpha, beta);
   return ee_check_launch("gemm_f32");
+}
+
+int eegan_gemm_f32_grouped(const eegan_gemm_desc* descs, int n, hipStream_t s) {
+  for (int g0 = 0; g0 < n; g0 += GMAX) {
+    GemmGroup grp{};
+    grp.n = std::min(GMAX, n - g0);
+    int tiles = 0;
+    for (int i = 0; i < grp.n; ++i) {
+      const eegan_gemm_desc& e = descs[g0 + i];
+      const long strides[6] = {e.sai, e.sak, e.sbk, e.sbj, e.ldc, e.ldg};
+      for (long v : strides)
+        if (v < 0 || v > 0x7fffffffL) {
+          ee_set_error("gemm_f32_grouped: stride %ld out of range", v);
+          return -22;
+        }
+      GemmDev& d = grp.d[i];
+      d = GemmDev{e.A, e.B, e.bias, e.gate, e.C, (int)e.sai, (int)e.sak, (int)e.sbk, (int)e.sbj, (int)e.ldc,
+                  (int)e.ldg, e.M, e.N, e.K, e.act, e.gate_act, e.alpha, e.beta};
+      grp.tile0[i] = tiles;
+      tiles += ee_cdiv(std::max(e.M, 0), T) * ee_cdiv(std::max(e.N, 0), T);
+    }
+    grp.tile0[grp.n] = tiles;
+    if (tiles == 0) continue;
+    ee_launch(gemm_f32_grouped_kernel, dim3(tiles), dim3(256), 0, s, grp);
+    const int rc = ee_check_launch("gemm_f32_grouped");
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 int eegan_colsum_f32(const float* X, long ld, int M, int N, float* out, int accumulate, hipStream_t s) {

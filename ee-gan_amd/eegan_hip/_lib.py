@@ -26,6 +26,12 @@ class BnModDesc(C.Structure):
                 ('mask', C.c_void_p), ('act', C.c_int), ('slope', C.c_float)]
 
 
+class GemmDesc(C.Structure):
+    _fields_ = [('A', C.c_void_p), ('B', C.c_void_p), ('C', C.c_void_p), ('bias', C.c_void_p),
+                ('gate', C.c_void_p)] + [(n, C.c_long) for n in ['sai', 'sak', 'sbk', 'sbj', 'ldc', 'ldg']] + \
+               [(n, C.c_int) for n in ['M', 'N', 'K', 'act', 'gate_act']] + [('alpha', C.c_float), ('beta', C.c_float)]
+
+
 P, I, L, F, D = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_double
 CD, BD = C.POINTER(ConvDesc), C.POINTER(BnModDesc)
 
@@ -83,6 +89,7 @@ _SIGS = {
     'eegan_fill_f32': ([P, L, F, P], I),
     'eegan_gemm_f32': ([P, L, L, P, L, L, P, L, I, I, I, P, I, F, F, P], I),
     'eegan_colsum_f32': ([P, L, I, I, P, I, P], I),
+    'eegan_gemm_f32_grouped': ([C.POINTER(GemmDesc), I, P], I),
     'eegan_act_bwd_f32': ([P, P, L, I, F, P, P], I),
     'eegan_words_sim': ([P, P, P, I, I, P, P, P], I),
     'eegan_words_sim_bwd': ([P, P, P, I, I, P, P, P, P], I),

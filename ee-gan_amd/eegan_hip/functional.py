@@ -10,12 +10,13 @@ Generator-side Functions (BN modulation, upsample-fused convs, linears,
 mask resize) are first-order, as the reference only differentiates G once.
 """
 import ctypes
+import os
 import math
 
 import torch
 
 from . import tensor as T
-from ._lib import ops, ConvDesc, BnModDesc, ACT_CODES
+from ._lib import ops, ConvDesc, BnModDesc, GemmDesc, ACT_CODES
 from .tensor import BF16, F32, CL, empty_nhwc, ld_of, ptr, stream, to_nhwc_bf16, workspace
 
 # In autograd.grad() mode the engine cannot report whether a leaf is needed;
@@ -749,6 +750,143 @@ class LinearFn(torch.autograd.Function):
             ops.colsum_f32(g.data_ptr(), N, M, N, dst.data_ptr(), int(sink is not None), stream())
             db = dst if sink is None else None
         return dx, dW, db, None
+
+
+# ================================================= grouped affine MLPs ===
+# EEGAN_GROUPED_MLP=0 runs every affine_ssa MLP as its own LinearFn pair.
+GROUPED_MLP = os.environ.get('EEGAN_GROUPED_MLP', '1') != '0'
+_ONES = {}
+
+
+def _ones(n, dev):
+    key = (dev, n)
+    if key not in _ONES:
+        _ONES[key] = torch.ones(n, dtype=F32, device=dev)
+    return _ONES[key]
+
+
+def _gemm_grouped(tag, descs):
+    if not descs:
+        return
+    arr = (GemmDesc * len(descs))(*[GemmDesc(*d) for d in descs])
+    flops = sum(2.0 * d[11] * d[12] * d[13] for d in descs)
+    nbytes = sum(4.0 * (d[11] * d[13] + d[13] * d[12] + d[11] * d[12]) for d in descs)
+    _launch('gemm_f32', flops, nbytes, lambda: ops.gemm_f32_grouped(arr, len(descs), stream()),
+            key='%s x%d' % (tag, len(descs)) if TIMER is not None else None)
+
+
+def _gd(A, sai, sak, B, sbk, sbj, C, ldc, M, N, K, bias=0, act=0, beta=0.0, gate=0, ldg=0, gate_act=0):
+    """GemmDesc field order: A, B, C, bias, gate, sai, sak, sbk, sbj, ldc, ldg, M, N, K, act, gate_act, alpha, beta."""
+    return (A, B, C, bias, gate, sai, sak, sbk, sbj, ldc, ldg, M, N, K, act, gate_act, 1.0, beta)
+
+
+class AffineMLPsFn(torch.autograd.Function):
+    """Every affine_ssa fc_gamma / fc_beta MLP of one generator pass
+    (Linear -> ReLU -> Linear, models.py:51-60) as grouped GEMMs: 2 forward
+    launches and 6 backward launches (+ one sum per conditioning input)
+    instead of ~7 small launches per MLP.  Same products in the same order
+    as LinearFn, so the outputs and gradients are bit-identical to it.
+
+    apply(*conds, *params, cidx, nconds): cidx[g] picks MLP g's input among
+    conds; params = (W1, b1, W2, b2) per MLP.  Returns one (B, N_g) output per
+    MLP.  (The non-tensor arguments come last: ctx.next_functions only lists
+    the leading inputs, so tensor positions must match needs_input_grad.)"""
+
+    @staticmethod
+    def forward(ctx, *args):
+        cidx, nconds = args[-2], args[-1]
+        args = args[:-2]
+        conds = [x.reshape(x.shape[0], -1).float().contiguous() for x in args[:nconds]]
+        params = args[nconds:]
+        G = len(params) // 4
+        Bn, K = conds[0].shape
+        Hd = params[0].shape[0]
+        dev = conds[0].device
+        H = torch.empty((G, Bn, Hd), dtype=F32, device=dev)
+        ys = []
+        d1, d2 = [], []
+        for g in range(G):
+            W1, b1, W2, b2 = params[4 * g:4 * g + 4]
+            N = W2.shape[0]
+            y = torch.empty((Bn, N), dtype=F32, device=dev)
+            ys.append(y)
+            d1.append(_gd(conds[cidx[g]].data_ptr(), K, 1, W1.data_ptr(), 1, K, H[g].data_ptr(), Hd, Bn, Hd, K,
+                          bias=ptr(b1), act=ACT_CODES['relu']))
+            d2.append(_gd(H[g].data_ptr(), Hd, 1, W2.data_ptr(), 1, Hd, y.data_ptr(), N, Bn, N, Hd, bias=ptr(b2)))
+        _gemm_grouped('mlp_fwd1', d1)
+        _gemm_grouped('mlp_fwd2', d2)
+        ctx.cidx, ctx.nconds, ctx.G = tuple(cidx), nconds, G
+        ctx.save_for_backward(H, *conds, *params)
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *gys):
+        saved = ctx.saved_tensors
+        H, conds, params = saved[0], saved[1:1 + ctx.nconds], saved[1 + ctx.nconds:]
+        G, Bn, Hd = H.shape
+        K = conds[0].shape[1]
+        dev = H.device
+        ones = _ones(Bn, dev)
+        off = ctx.nconds  # needs_input_grad index of params[0]
+        grads = [None] * len(params)
+        d1, d2 = [], []
+        dH = torch.empty_like(H)
+        need_c = [ctx.needs_input_grad[i] for i in range(ctx.nconds)]
+        DCP = torch.empty((G, Bn, K), dtype=F32, device=dev) if any(need_c) else None
+        live = []
+
+        def sink_or_new(i, shape):
+            s_ = _grad_sink(ctx, off + i) if _needed(ctx, off + i) else None
+            if s_ is not None:
+                return s_, 1.0, None
+            if not _needed(ctx, off + i):
+                return None, 0.0, None
+            t = torch.empty(shape, dtype=F32, device=dev)
+            return t, 0.0, t
+
+        for g in range(G):
+            gy = gys[g]
+            if gy is None:
+                continue
+            live.append(g)
+            gy = gy.reshape(Bn, -1).float().contiguous()
+            W1, b1, W2, b2 = params[4 * g:4 * g + 4]
+            N = W2.shape[0]
+            dst, beta, ret = sink_or_new(4 * g + 2, (N, Hd))
+            if dst is not None:
+                d1.append(_gd(gy.data_ptr(), 1, N, H[g].data_ptr(), Hd, 1, dst.data_ptr(), Hd, N, Hd, Bn, beta=beta))
+                grads[4 * g + 2] = ret
+            dst, beta, ret = sink_or_new(4 * g + 3, (N,))
+            if dst is not None:
+                d1.append(_gd(gy.data_ptr(), 1, N, ones.data_ptr(), 1, 0, dst.data_ptr(), 1, N, 1, Bn, beta=beta))
+                grads[4 * g + 3] = ret
+            d1.append(_gd(gy.data_ptr(), N, 1, W2.data_ptr(), Hd, 1, dH[g].data_ptr(), Hd, Bn, Hd, N,
+                          gate=H[g].data_ptr(), ldg=Hd, gate_act=ACT_CODES['relu']))
+            dst, beta, ret = sink_or_new(4 * g, (Hd, K))
+            if dst is not None:
+                d2.append(_gd(dH[g].data_ptr(), 1, Hd, conds[ctx.cidx[g]].data_ptr(), K, 1, dst.data_ptr(), K,
+                              Hd, K, Bn, beta=beta))
+                grads[4 * g] = ret
+            dst, beta, ret = sink_or_new(4 * g + 1, (Hd,))
+            if dst is not None:
+                d2.append(_gd(dH[g].data_ptr(), 1, Hd, ones.data_ptr(), 1, 0, dst.data_ptr(), 1, Hd, 1, Bn, beta=beta))
+                grads[4 * g + 1] = ret
+            if need_c[ctx.cidx[g]]:
+                d2.append(_gd(dH[g].data_ptr(), Hd, 1, W1.data_ptr(), K, 1, DCP[g].data_ptr(), K, Bn, K, Hd))
+        _gemm_grouped('mlp_bwd1', d1)
+        _gemm_grouped('mlp_bwd2', d2)
+        dconds = [None] * ctx.nconds
+        for ci in range(ctx.nconds):
+            if not need_c[ci]:
+                continue
+            gs = [g for g in live if ctx.cidx[g] == ci]
+            if not gs:
+                continue
+            if gs == list(range(gs[0], gs[-1] + 1)):
+                dconds[ci] = DCP[gs[0]:gs[-1] + 1].sum(0)
+            else:
+                dconds[ci] = DCP[gs].sum(0)
+        return (*dconds, *grads, None, None)
 
 
 # =========================================================== SyncBN path ===

@@ -92,9 +92,20 @@ class affine_ssa(nn.Module):
             nn.init.zeros_(m.weight.data)
             nn.init.zeros_(m.bias.data)
 
-    def forward(self, feat, cond, semi_mask, act=None, up2=False):
-        gam = self.fc_gamma(cond)
-        bet = self.fc_beta(cond)
+    def mlp_params(self):
+        """(W1, b1, W2, b2) of fc_gamma then fc_beta (Fn.AffineMLPsFn order)."""
+        out = []
+        for m in (self.fc_gamma, self.fc_beta):
+            out += [m.linear1.weight, m.linear1.bias, m.linear2.weight, m.linear2.bias]
+        return out
+
+    def forward(self, feat, cond, semi_mask, act=None, up2=False, gb=None):
+        """`gb` = precomputed (gamma, beta) MLP outputs (Gen batches all of them)."""
+        if gb is not None:
+            gam, bet = gb
+        else:
+            gam = self.fc_gamma(cond)
+            bet = self.fc_beta(cond)
         if gam.dim() == 1:
             gam = gam.unsqueeze(0)
         if bet.dim() == 1:
@@ -126,16 +137,18 @@ class SAGB_Block(nn.Module):
             x = self.c_sc(x)          # at low resolution when up2 (commutes with nearest-up)
         return Fn.Upsample2Fn.apply(x) if up2 else x
 
-    def residual(self, feat, conds, semi_mask, up2=False):
-        h = self.affine1(feat, conds[0], semi_mask, act='relu', up2=up2)
+    def residual(self, feat, conds, semi_mask, up2=False, gb=None):
+        gb = gb or (None, None)
+        h = self.affine1(feat, conds[0], semi_mask, act='relu', up2=up2, gb=gb[0])
         h = self.c1(h)
-        h = self.affine2(h, conds[1], semi_mask, act='relu')
+        h = self.affine2(h, conds[1], semi_mask, act='relu', gb=gb[1])
         return self.c2(h)
 
-    def forward(self, feat, conds, semi_mask, up2=False):
+    def forward(self, feat, conds, semi_mask, up2=False, gb=None):
         """`up2=True` consumes the PRE-upsample feature map (fusing the
-        F.interpolate(scale_factor=2) of Gen.SAGB_progress, models.py:219)."""
-        c_feat = Fn.ScaleAddFn.apply(self.shortcut(feat, up2), self.residual(feat, conds, semi_mask, up2),
+        F.interpolate(scale_factor=2) of Gen.SAGB_progress, models.py:219).
+        `gb` = ((gamma1, beta1), (gamma2, beta2)) precomputed by Gen."""
+        c_feat = Fn.ScaleAddFn.apply(self.shortcut(feat, up2), self.residual(feat, conds, semi_mask, up2, gb),
                                      self.gamma)
         c_semi_mask = self.conv_mask(c_feat) if self.pred_mask else None
         return c_feat, c_semi_mask
@@ -207,26 +220,46 @@ class Gen(nn.Module):
         self.stages = 3  # 1: the harness stage-1 slice (img_64 only)
 
     @staticmethod
-    def SAGB_progress(feat, conds, stage_mask, scale, SAGB_block):
+    def SAGB_progress(feat, conds, stage_mask, scale, SAGB_block, gb=None):
         fusion_mask = Fn.MaskResizeSigmoidFn.apply(stage_mask, scale)
-        return SAGB_block(feat, conds, fusion_mask, up2=True)
+        return SAGB_block(feat, conds, fusion_mask, up2=True, gb=gb)
+
+    def affine_mlps(self, sent, attrs):
+        """gamma/beta of every affine_ssa the pass uses, in grouped launches
+        (Fn.AffineMLPsFn); blocks 0-3 condition both affines on sent, blocks
+        4-6 affine1 on sent and affine2 on attrs (models.py:214-236)."""
+        nblk = 5 if self.stages == 1 else 7
+        order = [(b, 0) for b in range(nblk)] + [(b, 1) for b in range(4)] + [(b, 1) for b in range(4, nblk)]
+        cidx, params = [], []
+        for b, k in order:
+            aff = self.blocks[b].affine1 if k == 0 else self.blocks[b].affine2
+            c = 1 if (k == 1 and b >= 4) else 0
+            cidx += [c, c]
+            params += aff.mlp_params()
+        outs = Fn.AffineMLPsFn.apply(sent, attrs, *params, tuple(cidx), 2)
+        gb = [[None, None] for _ in range(nblk)]
+        for i, (b, k) in enumerate(order):
+            gb[b][k] = (outs[2 * i], outs[2 * i + 1])
+        return gb
 
     def forward(self, x, sent, attrs):
+        gb = self.affine_mlps(sent, attrs) if Fn.GROUPED_MLP else [None] * 7
         out = self.fc(x.float())
         out = Fn.FcToNhwcFn.apply(out, 8 * self.ngf)
         stage_mask = self.init_mask(out)
         fusion_mask = Fn.MaskResizeSigmoidFn.apply(stage_mask, 4)
-        out, stage_mask = self.blocks[0](out, [sent, sent], fusion_mask)
+        out, stage_mask = self.blocks[0](out, [sent, sent], fusion_mask, gb=gb[0])
         for ix, scale in enumerate([8, 16, 32]):
-            out, stage_mask = self.SAGB_progress(out, [sent, sent], stage_mask, scale, self.blocks[ix + 1])
+            out, stage_mask = self.SAGB_progress(out, [sent, sent], stage_mask, scale, self.blocks[ix + 1],
+                                                 gb[ix + 1])
         x_32 = out
-        x_64, stage_mask = self.SAGB_progress(x_32, [sent, attrs], stage_mask, 64, self.blocks[4])
+        x_64, stage_mask = self.SAGB_progress(x_32, [sent, attrs], stage_mask, 64, self.blocks[4], gb[4])
         cum_x_64 = self.cum_64(x_32, x_64)
         img_64 = self.get_image_64(cum_x_64)
         if self.stages == 1:
             return [img_64]
-        x_128, stage_mask = self.SAGB_progress(x_64, [sent, attrs], stage_mask, 128, self.blocks[5])
-        x_256, _ = self.SAGB_progress(x_128, [sent, attrs], stage_mask, 256, self.blocks[6])
+        x_128, stage_mask = self.SAGB_progress(x_64, [sent, attrs], stage_mask, 128, self.blocks[5], gb[5])
+        x_256, _ = self.SAGB_progress(x_128, [sent, attrs], stage_mask, 256, self.blocks[6], gb[6])
         cum_x_128 = self.cum_128(cum_x_64, x_128)
         cum_x_256 = self.cum_256(cum_x_128, x_256)
         img_128 = self.get_image_128(cum_x_128)

@@ -178,6 +178,20 @@ int eegan_fill_f32(float* x, long n, float v, hipStream_t s);
 int eegan_gemm_f32(const float* A, long sai, long sak, const float* B, long sbk, long sbj, float* C, long ldc, int M,
                    int N, int K, const float* bias, int act, float alpha, float beta, hipStream_t s);
 int eegan_colsum_f32(const float* X, long ld, int M, int N, float* out, int accumulate, hipStream_t s);
+/* n independent eegan_gemm_f32 problems in ceil(n / 32) launches; `gate` (optional, row stride ldg)
+ * multiplies each result by act'(gate) of activation gate_act (e.g. dh = (dy W2) * relu'(h)).
+ * replaces: the 28 affine_ssa fc_gamma / fc_beta MLPs of models.py:51-60 batched per step */
+typedef struct {
+  const float* A;
+  const float* B;
+  float* C;
+  const float* bias;
+  const float* gate;
+  long sai, sak, sbk, sbj, ldc, ldg;
+  int M, N, K, act, gate_act;
+  float alpha, beta;
+} eegan_gemm_desc;
+int eegan_gemm_f32_grouped(const eegan_gemm_desc* descs, int n, hipStream_t s);
 int eegan_act_bwd_f32(const float* dy, const float* y, long n, int act, float slope, float* dx, hipStream_t s);
 
 /* ------------------------------------------------------------------ losses --

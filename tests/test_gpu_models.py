@@ -203,6 +203,38 @@ def test_generator(gpu):
             _check('gen/' + k, v, g['gen/after/' + k], 2e-2)
 
 
+def test_generator_grouped_mlps_match_per_layer(gpu, monkeypatch):
+    """Fn.AffineMLPsFn (all affine_ssa MLPs in grouped launches) computes the
+    same products in the same order as the per-layer LinearFn path: images
+    and parameter gradients bit-identical; the conditioning gradients sum the
+    per-MLP terms in another order (fp32 rounding only)."""
+    import models
+    from eegan_hip import functional as Fn
+    G = _load(models.Gen(8, 100), 'gen', 21, gpu)
+    z = seeded_tensor('g:z', (2, 100), 1).to(gpu)
+    res = []
+    for grouped in (False, True):
+        monkeypatch.setattr(Fn, 'GROUPED_MLP', grouped)
+        G.zero_grad(set_to_none=True)
+        s = seeded_tensor('g:s', (2, 256), 1).to(gpu).requires_grad_()
+        a = seeded_tensor('g:a', (2, 256), 1).to(gpu).requires_grad_()
+        imgs = G(z, s, a)
+        loss = sum((im.float() * seeded_tensor('g:r%d' % k, im.shape, 2).to(gpu)).sum() for k, im in enumerate(imgs))
+        loss.backward()
+        res.append(([im.float().cpu() for im in imgs], s.grad.cpu(), a.grad.cpu(),
+                     {n: p.grad.cpu().clone() for n, p in G.named_parameters() if p.grad is not None}))
+    (i0, s0, a0, g0), (i1, s1, a1, g1) = res
+    for x, y in zip(i0, i1):
+        assert torch.equal(x, y)
+    assert set(g0) == set(g1)
+    for n in g0:
+        if 'fc_gamma' in n or 'fc_beta' in n:
+            assert torch.equal(g0[n], g1[n]), n
+        else:
+            assert torch.allclose(g0[n], g1[n], rtol=1e-4, atol=1e-6), n
+    assert torch.allclose(s0, s1, rtol=1e-4, atol=1e-6) and torch.allclose(a0, a1, rtol=1e-4, atol=1e-6)
+
+
 @pytest.mark.parametrize('kind', [64, 128, 256])
 def test_discriminator_and_gradient_penalty(gpu, kind):
     import models
