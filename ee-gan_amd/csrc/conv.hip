@@ -1741,6 +1741,125 @@ __global__ __launch_bounds__(256, 3) void conv_thin_lds_kernel(ConvArgs a, int s
   }
 }
 
+// ---------------------------------------------------- thin weight gradient --
+// dW of 3x3 stride-1 pad-1 convs with <= 8 output channels and 25..32 input
+// channels: get_image (ngf -> 3, models.py:25-32) at ngf = 32, whose weight
+// gradient reduces over every pixel of the 256x256 batch into only 3 x 288
+// values -- a shape the tile kernels split into ~170 narrow pieces.  Here
+// M = output channels (one 16-row MFMA tile), N = (tap, 16-channel block) =
+// 18 tiles, K = pixels: each block stages 4 output rows x 64 pixels of dy and
+// the (4 + 2) x (64 + 2) x halo in LDS, and both operands are read K-major with
+// the gfx950 transposing ds_read_b64_tr_b16.  The K order inside a 32-pixel
+// step is permuted (lane group g takes pixels 4g..4g+3 and 16+4g..16+4g+3) so
+// every 32-lane half reads 8 consecutive pixels of a 32-B channel plane:
+// conflict-free.  One partial per block goes to the split slab; the column
+// reduce of the generic path maps it into the channels-last dW.
+constexpr int WTH_H = 4, WTH_W = 64, WTH_PW = WTH_W + 2, WTH_XPIX = (WTH_H + 2) * WTH_PW;
+typedef __attribute__((ext_vector_type(4))) short s16x4_tr;
+
+EE_DEV s16x4_tr lds_tr16(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_tr*)(p));
+}
+EE_DEV bf16x8_t tr_pair(s16x4_tr lo, s16x4_tr hi) {
+  typedef __attribute__((ext_vector_type(8))) short s16x8_tr;
+  const s16x8_tr v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+__global__ __launch_bounds__(256) void conv_wgrad_thin_kernel(WgradArgs w, int x_bytes, int dy_bytes,
+                                                              int tiles_per_block) {
+  constexpr int NT = 18;
+  constexpr int XCH = WTH_XPIX * 4;                 // 16-B chunks of the x halo (32 channels)
+  constexpr int XLD = (XCH + 255) / 256;            // per thread
+  __shared__ __attribute__((aligned(16))) bf16_t xs[2 * WTH_XPIX * 16];  // [cb][pixel][16 ch]
+  __shared__ __attribute__((aligned(16))) bf16_t dys[WTH_H * WTH_W * 8];  // [pixel][8 ch]
+  const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4, li = lane & 15, q = li >> 2, pq = li & 3;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (b & 7) * (nb >> 3) + (b >> 3);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)w.x, (short)0, x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)w.dy, (short)0, dy_bytes, 0x00020000);
+  f32x4_t acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int tiles_x = w.OW / WTH_W, tiles_y = w.OH / WTH_H, tiles = w.N * tiles_x * tiles_y;
+  const int t0 = lb * tiles_per_block, t1 = min(t0 + tiles_per_block, tiles);
+  for (int tt = t0; tt < t1; ++tt) {
+    const int n = tt / (tiles_x * tiles_y), rem = tt - n * tiles_x * tiles_y;
+    const int y0 = (rem / tiles_x) * WTH_H, x0 = (rem - (rem / tiles_x) * tiles_x) * WTH_W;
+    uint4 xv[XLD];
+#pragma unroll
+    for (int i = 0; i < XLD; ++i) {
+      const int e = tid + 256 * i;
+      const int pix = e >> 2, ch = e & 3;
+      const int pr = pix / WTH_PW, pc = pix - pr * WTH_PW;
+      const int iy = y0 + pr - 1, ix = x0 + pc - 1;
+      const bool ok = e < XCH && (unsigned)iy < (unsigned)w.IH && (unsigned)ix < (unsigned)w.IW;
+      const int off = (((n * w.IH + iy) * w.IW + ix) * w.ldx + ch * 8) * 2;
+      xv[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? off : 0x80000000, 0, 0));
+    }
+    const int dr = tid >> 6, dc = tid & 63;
+    const int doff = ((((n * w.OH + y0 + dr) * w.OW) + x0 + dc) * w.lddy) * 2;
+    const uint4 dv = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rd, doff, 0, 0));
+    __syncthreads();  // previous tile's reads done
+#pragma unroll
+    for (int i = 0; i < XLD; ++i) {
+      const int e = tid + 256 * i;
+      if (e < XCH) {
+        const int pix = e >> 2, ch = e & 3;
+        *reinterpret_cast<uint4*>(&xs[((ch >> 1) * WTH_XPIX + pix) * 16 + (ch & 1) * 8]) = xv[i];
+      }
+    }
+    *reinterpret_cast<uint4*>(&dys[tid * 8]) = dv;
+    __syncthreads();
+    const int rr = wv;
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      const int p1 = 32 * kc + 4 * kg + q, p2 = p1 + 16;  // this lane's pixel rows of the two reads
+      // A = dy^T: rows are output channels; lanes with pq >= 2 (channels 8..15,
+      // past the staged 8) re-read channels 0..7, landing in unused rows >= 8
+      const int cA = 4 * (pq & 1);
+      const bf16x8_t fa = tr_pair(lds_tr16(&dys[(rr * WTH_W + p1) * 8 + cA]), lds_tr16(&dys[(rr * WTH_W + p2) * 8 + cA]));
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) {
+            const int xp = cb * WTH_XPIX + (rr + r) * WTH_PW + s;
+            const bf16x8_t fb = tr_pair(lds_tr16(&xs[(xp + p1) * 16 + 4 * pq]), lds_tr16(&xs[(xp + p2) * 16 + 4 * pq]));
+            acc[(r * 3 + s) * 2 + cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[(r * 3 + s) * 2 + cb], 0, 0, 0);
+          }
+    }
+  }
+  // block reduce of the 4 waves' partials through LDS (fixed order: deterministic)
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(xs);  // NT x 64 x 4 floats fit in the x halo
+#pragma unroll
+  for (int ww = 0; ww < 3; ++ww) {
+    if (wv == ww) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float* rp = &red[(t * 64 + lane) * 4 + i];
+          *rp = (ww == 0 ? 0.f : *rp) + acc[t][i];
+        }
+    }
+    __syncthreads();
+  }
+  if (wv == 3) {
+    float* slab = w.ws + (long)b * w.Cout * w.K;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = 4 * kg + i;
+        if (co < w.Cout) slab[co * w.K + (t >> 1) * 32 + (t & 1) * 16 + li] = red[(t * 64 + lane) * 4 + i] + acc[t][i];
+      }
+  }
+}
+
 // ------------------------------------------------------------ dispatch --
 int cgp_of(int C) { return C <= 8 ? 8 : ee_round_up(C, BK); }
 int kw_of(int R, int S, int Cgp) { return ee_round_up(R * S * Cgp, BK); }
@@ -2026,9 +2145,27 @@ static bool wgrad_glds_ok(const eegan_conv_desc* d) {
   return d->K > 16 && wgrad_x_bytes(d) < 0x7fffffffL && wgrad_dy_bytes(d) < 0x7fffffffL;
 }
 
+// blocks of conv_wgrad_thin_kernel for this shape, or 0 when it does not apply
+static int wgrad_thin_blocks(const eegan_conv_desc* d) {
+  if (!env_int("EEGAN_CONV_THIN", 1)) return 0;
+  if (d->R != 3 || d->S != 3 || d->stride != 1 || d->pad_h != 1 || d->pad_w != 1 || d->up2) return 0;
+  if (d->K > 8 || ee_round_up(d->C, 8) != 32 || d->Wo % WTH_W || d->Ho % WTH_H) return 0;
+  if (wgrad_x_bytes(d) >= 0x7fffffffL || wgrad_dy_bytes(d) >= 0x7fffffffL) return 0;
+  const int tiles = d->N * (d->Ho / WTH_H) * (d->Wo / WTH_W);
+  if (tiles < 8) return 0;
+  return ee_round_up(std::min(tiles, 512), 8);
+}
+
 static void wgrad_plan(const eegan_conv_desc* d, int& TCO, int& TK, int& nsplit, int& pps, int& K) {
   const int Cg = ee_round_up(d->C, 8);
   K = d->R * d->S * Cg;
+  if (const int tb = wgrad_thin_blocks(d)) {
+    TCO = 16;
+    TK = 64;
+    nsplit = tb;
+    pps = 0;
+    return;
+  }
   TCO = d->K > 64 ? 128 : d->K > 32 ? 64 : (d->K > 16 && wgrad_glds_ok(d)) ? 32 : d->K > 16 ? 64 : 16;
   TK = K > 64 ? 128 : 64;
   const int P = d->N * d->Ho * d->Wo;
@@ -2084,7 +2221,13 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
     w.dw = dw;
     w.accumulate = accumulate;
   }
-  if (w.P > 0) {
+  if (w.P > 0 && wgrad_thin_blocks(d)) {
+    const int tiles = d->N * (d->Ho / WTH_H) * (d->Wo / WTH_W);
+    ee_launch(conv_wgrad_thin_kernel, dim3(nsplit), dim3(256), 0, stream, w, (int)wgrad_x_bytes(d),
+              (int)wgrad_dy_bytes(d), ee_cdiv(tiles, nsplit));
+    const int rc = ee_check_launch("conv_wgrad(thin)");
+    if (rc) return rc;
+  } else if (w.P > 0) {
     dim3 grid(ee_cdiv(K, TK), ee_cdiv(d->K, TCO), nsplit);
     const long x_bytes = wgrad_x_bytes(d), dy_bytes = wgrad_dy_bytes(d);
 #define WG(TC, TKK, WC) ee_launch(conv_wgrad_kernel<TC, TKK, WC>, grid, dim3(256), 0, stream, w)

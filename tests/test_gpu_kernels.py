@@ -126,6 +126,27 @@ def test_conv_thin_path_matches_tile(gpu, monkeypatch):
             assert rel_l2(outs[1][1], xr.grad) < 1e-2
 
 
+def test_conv_thin_wgrad(gpu, monkeypatch):
+    """Weight gradient of 3x3 convs with <= 8 output and 25..32 input channels
+    (get_image) through the transposed-read thin kernel: against torch fp32
+    and the tile path (different fp32 summation order, so within 1e-5)."""
+    Fn, T, _ = _mods()
+    for N, Cin, H, W, Cout in [(2, 32, 8, 64, 3), (1, 32, 12, 128, 8), (2, 28, 4, 64, 5), (4, 32, 8, 64, 1)]:
+        torch.manual_seed(N + Cin + H + Cout)
+        g = Fn.Geom(Cout, 3, 3, 1, 1, 1, 0)
+        xl = _bf(torch.randn(N, Cin, H, W))
+        dzl = _bf(torch.randn(N, Cout, H, W))
+        x, dz = _nhwc(xl, gpu), _nhwc(dzl, gpu)
+        outs = []
+        for thin in ('0', '1'):
+            monkeypatch.setenv('EEGAN_CONV_THIN', thin)
+            outs.append(Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, 3, 3)).cpu())
+        wr = torch.zeros(Cout, Cin, 3, 3, requires_grad=True)
+        F.conv2d(xl, wr, None, 1, 1).backward(dzl)
+        assert rel_l2(outs[1], wr.grad) < 1e-4
+        assert torch.allclose(outs[0], outs[1], rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.parametrize('case', CONV_CASES, ids=[str(i) for i in range(len(CONV_CASES))])
 def test_conv_fwd_bwd(gpu, case):
     Fn, T, Conv2d = _mods()

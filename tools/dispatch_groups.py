@@ -17,6 +17,7 @@ def main():
     ap.add_argument('--steps', type=int, required=True)
     ap.add_argument('--filter', default='')
     ap.add_argument('--top', type=int, default=40)
+    ap.add_argument('--by-name', action='store_true', help='group by kernel name only, sort by calls')
     args = ap.parse_args()
     groups = defaultdict(lambda: [0, 0])
     for path in glob.glob(os.path.join(args.trace, '**', '*kernel_trace.csv'), recursive=True):
@@ -29,10 +30,10 @@ def main():
                 short = short.split('(')[0][:90]
                 grid = (r.get('Grid_Size_X', r.get('Grid_Size', '?')), r.get('Grid_Size_Y', ''),
                         r.get('Grid_Size_Z', ''))
-                g = groups[(short, grid)]
+                g = groups[(short, ('',) if args.by_name else grid)]
                 g[0] += 1
                 g[1] += int(r['End_Timestamp']) - int(r['Start_Timestamp'])
-    rows = sorted(groups.items(), key=lambda kv: -kv[1][1])
+    rows = sorted(groups.items(), key=lambda kv: -kv[1][0 if args.by_name else 1])
     tot = sum(v[1] for v in groups.values())
     print('total %.3f ms/step over %d groups' % (tot * 1e-6 / args.steps, len(groups)))
     for (k, grid), (n, ns) in rows[:args.top]:
