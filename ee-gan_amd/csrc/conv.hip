@@ -1742,16 +1742,17 @@ __global__ __launch_bounds__(256, 3) void conv_thin_lds_kernel(ConvArgs a, int s
 }
 
 // ---------------------------------------------------- thin weight gradient --
-// dW of 3x3 stride-1 pad-1 convs with <= 8 output channels and 25..32 input
-// channels: get_image (ngf -> 3, models.py:25-32) at ngf = 32, whose weight
-// gradient reduces over every pixel of the 256x256 batch into only 3 x 288
-// values -- a shape the tile kernels split into ~170 narrow pieces.  Here
-// M = output channels (one 16-row MFMA tile), N = (tap, 16-channel block) =
-// 18 tiles, K = pixels: each block stages 4 output rows x 64 pixels of dy and
-// the (4 + 2) x (64 + 2) x halo in LDS, and both operands are read K-major with
-// the gfx950 transposing ds_read_b64_tr_b16.  The K order inside a 32-pixel
-// step is permuted (lane group g takes pixels 4g..4g+3 and 16+4g..16+4g+3) so
-// every 32-lane half reads 8 consecutive pixels of a 32-B channel plane:
+// dW of 3x3 stride-1 pad-1 convs with <= 8 output channels and 32 or 64
+// (padded) input channels: get_image (ngf * {1, 2} -> 3, models.py:25-32),
+// whose weight gradient reduces over every pixel of a 256x256 / 128x128 batch
+// into only 3 x 9 x Cin values -- a shape the tile kernels split into ~100-170
+// narrow pieces.  Here M = output channels (one 16-row MFMA tile), N = (tap,
+// 16-channel block) = 9 * CGB tiles dealt round-robin to the 4 waves, K =
+// pixels: each block stages 4 output rows x 64 pixels of dy and the
+// (4 + 2) x (64 + 2) x halo in LDS, and both operands are read K-major with the
+// gfx950 transposing ds_read_b64_tr_b16.  The K order inside a 32-pixel step
+// is permuted (lane group g takes pixels 4g..4g+3 and 16+4g..16+4g+3) so every
+// 32-lane half reads 8 consecutive pixels of a 32-B channel plane:
 // conflict-free.  One partial per block goes to the split slab; the column
 // reduce of the generic path maps it into the channels-last dW.
 constexpr int WTH_H = 4, WTH_W = 64, WTH_PW = WTH_W + 2, WTH_XPIX = (WTH_H + 2) * WTH_PW;
@@ -1766,22 +1767,23 @@ EE_DEV bf16x8_t tr_pair(s16x4_tr lo, s16x4_tr hi) {
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+template <int CGB>  // 16-channel blocks of the padded Cin (2: 32 channels, 4: 64)
 __global__ __launch_bounds__(256) void conv_wgrad_thin_kernel(WgradArgs w, int x_bytes, int dy_bytes,
                                                               int tiles_per_block) {
-  constexpr int NT = 18;
-  constexpr int XCH = WTH_XPIX * 4;                 // 16-B chunks of the x halo (32 channels)
+  constexpr int NT = 9 * CGB, NTW = (NT + 3) / 4;  // N tiles, per wave
+  constexpr int XCH = WTH_XPIX * CGB * 2;           // 16-B chunks of the x halo
   constexpr int XLD = (XCH + 255) / 256;            // per thread
-  __shared__ __attribute__((aligned(16))) bf16_t xs[2 * WTH_XPIX * 16];  // [cb][pixel][16 ch]
-  __shared__ __attribute__((aligned(16))) bf16_t dys[WTH_H * WTH_W * 8];  // [pixel][8 ch]
+  __shared__ __attribute__((aligned(16))) bf16_t xs[CGB * WTH_XPIX * 16];  // [cb][pixel][16 ch]
+  __shared__ __attribute__((aligned(16))) bf16_t dys[WTH_H * WTH_W * 8];   // [pixel][8 ch]
   const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4, li = lane & 15, q = li >> 2, pq = li & 3;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nb = gridDim.x, b = blockIdx.x;
   const int lb = (b & 7) * (nb >> 3) + (b >> 3);
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)w.x, (short)0, x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)w.dy, (short)0, dy_bytes, 0x00020000);
-  f32x4_t acc[NT];
+  f32x4_t acc[NTW];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < NTW; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int tiles_x = w.OW / WTH_W, tiles_y = w.OH / WTH_H, tiles = w.N * tiles_x * tiles_y;
   const int t0 = lb * tiles_per_block, t1 = min(t0 + tiles_per_block, tiles);
   for (int tt = t0; tt < t1; ++tt) {
@@ -1791,7 +1793,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_thin_kernel(WgradArgs w, int x
 #pragma unroll
     for (int i = 0; i < XLD; ++i) {
       const int e = tid + 256 * i;
-      const int pix = e >> 2, ch = e & 3;
+      const int pix = e / (2 * CGB), ch = e - pix * (2 * CGB);
       const int pr = pix / WTH_PW, pc = pix - pr * WTH_PW;
       const int iy = y0 + pr - 1, ix = x0 + pc - 1;
       const bool ok = e < XCH && (unsigned)iy < (unsigned)w.IH && (unsigned)ix < (unsigned)w.IW;
@@ -1806,57 +1808,48 @@ __global__ __launch_bounds__(256) void conv_wgrad_thin_kernel(WgradArgs w, int x
     for (int i = 0; i < XLD; ++i) {
       const int e = tid + 256 * i;
       if (e < XCH) {
-        const int pix = e >> 2, ch = e & 3;
+        const int pix = e / (2 * CGB), ch = e - pix * (2 * CGB);
         *reinterpret_cast<uint4*>(&xs[((ch >> 1) * WTH_XPIX + pix) * 16 + (ch & 1) * 8]) = xv[i];
       }
     }
     *reinterpret_cast<uint4*>(&dys[tid * 8]) = dv;
     __syncthreads();
-    const int rr = wv;
+#pragma unroll 1
+    for (int rr = 0; rr < WTH_H; ++rr) {
 #pragma unroll
-    for (int kc = 0; kc < 2; ++kc) {
-      const int p1 = 32 * kc + 4 * kg + q, p2 = p1 + 16;  // this lane's pixel rows of the two reads
-      // A = dy^T: rows are output channels; lanes with pq >= 2 (channels 8..15,
-      // past the staged 8) re-read channels 0..7, landing in unused rows >= 8
-      const int cA = 4 * (pq & 1);
-      const bf16x8_t fa = tr_pair(lds_tr16(&dys[(rr * WTH_W + p1) * 8 + cA]), lds_tr16(&dys[(rr * WTH_W + p2) * 8 + cA]));
+      for (int kc = 0; kc < 2; ++kc) {
+        const int p1 = 32 * kc + 4 * kg + q, p2 = p1 + 16;  // this lane's pixel rows of the two reads
+        // A = dy^T: rows are output channels; lanes with pq >= 2 (channels 8..15,
+        // past the staged 8) re-read channels 0..7, landing in unused rows >= 8
+        const int cA = 4 * (pq & 1);
+        const bf16x8_t fa =
+            tr_pair(lds_tr16(&dys[(rr * WTH_W + p1) * 8 + cA]), lds_tr16(&dys[(rr * WTH_W + p2) * 8 + cA]));
 #pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int s = 0; s < 3; ++s)
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb) {
+        for (int j = 0; j < NTW; ++j) {
+          const int t = wv + 4 * j;
+          if (t < NT) {  // wave-uniform
+            const int tap = t / CGB, cb = t - tap * CGB;
+            const int r = tap / 3, s = tap - 3 * r;
             const int xp = cb * WTH_XPIX + (rr + r) * WTH_PW + s;
-            const bf16x8_t fb = tr_pair(lds_tr16(&xs[(xp + p1) * 16 + 4 * pq]), lds_tr16(&xs[(xp + p2) * 16 + 4 * pq]));
-            acc[(r * 3 + s) * 2 + cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[(r * 3 + s) * 2 + cb], 0, 0, 0);
+            const bf16x8_t fb =
+                tr_pair(lds_tr16(&xs[(xp + p1) * 16 + 4 * pq]), lds_tr16(&xs[(xp + p2) * 16 + 4 * pq]));
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[j], 0, 0, 0);
           }
-    }
-  }
-  // block reduce of the 4 waves' partials through LDS (fixed order: deterministic)
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(xs);  // NT x 64 x 4 floats fit in the x halo
-#pragma unroll
-  for (int ww = 0; ww < 3; ++ww) {
-    if (wv == ww) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float* rp = &red[(t * 64 + lane) * 4 + i];
-          *rp = (ww == 0 ? 0.f : *rp) + acc[t][i];
         }
-    }
-    __syncthreads();
-  }
-  if (wv == 3) {
-    float* slab = w.ws + (long)b * w.Cout * w.K;
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int co = 4 * kg + i;
-        if (co < w.Cout) slab[co * w.K + (t >> 1) * 32 + (t & 1) * 16 + li] = red[(t * 64 + lane) * 4 + i] + acc[t][i];
       }
+    }
+  }
+  float* slab = w.ws + (long)b * w.Cout * w.K;
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int t = wv + 4 * j;
+    if (t >= NT) continue;
+    const int tap = t / CGB, cb = t - tap * CGB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = 4 * kg + i;
+      if (co < w.Cout) slab[co * w.K + tap * (16 * CGB) + cb * 16 + li] = acc[j][i];
+    }
   }
 }
 
@@ -2149,7 +2142,8 @@ static bool wgrad_glds_ok(const eegan_conv_desc* d) {
 static int wgrad_thin_blocks(const eegan_conv_desc* d) {
   if (!env_int("EEGAN_CONV_THIN", 1)) return 0;
   if (d->R != 3 || d->S != 3 || d->stride != 1 || d->pad_h != 1 || d->pad_w != 1 || d->up2) return 0;
-  if (d->K > 8 || ee_round_up(d->C, 8) != 32 || d->Wo % WTH_W || d->Ho % WTH_H) return 0;
+  const int cg = ee_round_up(d->C, 8);
+  if (d->K > 8 || (cg != 32 && cg != 64) || d->Wo % WTH_W || d->Ho % WTH_H) return 0;
   if (wgrad_x_bytes(d) >= 0x7fffffffL || wgrad_dy_bytes(d) >= 0x7fffffffL) return 0;
   const int tiles = d->N * (d->Ho / WTH_H) * (d->Wo / WTH_W);
   if (tiles < 8) return 0;
@@ -2223,8 +2217,12 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
   }
   if (w.P > 0 && wgrad_thin_blocks(d)) {
     const int tiles = d->N * (d->Ho / WTH_H) * (d->Wo / WTH_W);
-    ee_launch(conv_wgrad_thin_kernel, dim3(nsplit), dim3(256), 0, stream, w, (int)wgrad_x_bytes(d),
-              (int)wgrad_dy_bytes(d), ee_cdiv(tiles, nsplit));
+    if (w.Cg == 32)
+      ee_launch(conv_wgrad_thin_kernel<2>, dim3(nsplit), dim3(256), 0, stream, w, (int)wgrad_x_bytes(d),
+                (int)wgrad_dy_bytes(d), ee_cdiv(tiles, nsplit));
+    else
+      ee_launch(conv_wgrad_thin_kernel<4>, dim3(nsplit), dim3(256), 0, stream, w, (int)wgrad_x_bytes(d),
+                (int)wgrad_dy_bytes(d), ee_cdiv(tiles, nsplit));
     const int rc = ee_check_launch("conv_wgrad(thin)");
     if (rc) return rc;
   } else if (w.P > 0) {

@@ -127,11 +127,12 @@ def test_conv_thin_path_matches_tile(gpu, monkeypatch):
 
 
 def test_conv_thin_wgrad(gpu, monkeypatch):
-    """Weight gradient of 3x3 convs with <= 8 output and 25..32 input channels
+    """Weight gradient of 3x3 convs with <= 8 output and 25..64 input channels
     (get_image) through the transposed-read thin kernel: against torch fp32
     and the tile path (different fp32 summation order, so within 1e-5)."""
     Fn, T, _ = _mods()
-    for N, Cin, H, W, Cout in [(2, 32, 8, 64, 3), (1, 32, 12, 128, 8), (2, 28, 4, 64, 5), (4, 32, 8, 64, 1)]:
+    for N, Cin, H, W, Cout in [(2, 32, 8, 64, 3), (1, 32, 12, 128, 8), (2, 28, 4, 64, 5), (4, 32, 8, 64, 1),
+                               (2, 64, 8, 64, 3), (1, 56, 4, 128, 6)]:
         torch.manual_seed(N + Cin + H + Cout)
         g = Fn.Geom(Cout, 3, 3, 1, 1, 1, 0)
         xl = _bf(torch.randn(N, Cin, H, W))
