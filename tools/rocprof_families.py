@@ -35,6 +35,9 @@ _FAMILIES = [
     (re.compile(r'conv_igemm_kernel<1,'), 'conv_bwd_data', True),
     (re.compile(r'conv_splitk_reduce_kernel<1>'), 'conv_bwd_data', False),
     (re.compile(r'conv_wgrad_kernel<'), 'conv_bwd_weight', True),
+    (re.compile(r'conv_thin(_lds)?_kernel<0,'), 'conv_fwd', True),
+    (re.compile(r'conv_thin(_lds)?_kernel<1,'), 'conv_bwd_data', True),
+    (re.compile(r'conv_wgrad_thin_kernel<'), 'conv_bwd_weight', True),
     (re.compile(r'colsum_rows_kernel<.*WgradMap'), 'conv_bwd_weight', False),
 ]
 
