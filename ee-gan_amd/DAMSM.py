@@ -126,9 +126,21 @@ class BasicConv2d(nn.Module):
             self._fold_key = key
         return self._shift
 
-    def forward(self, x):
+    def forward(self, x, in_relu=False, defer=False):
+        """in_relu: x is the ReLU output of a BasicConv2d called with defer=True
+        whose consumers all gate (branch chains below): that ReLU's backward
+        runs in this conv's data-gradient epilogue (Fn.Conv2dFn in_act/defer_act)."""
         shift = self._fold()
-        return Fn.Conv2dFn.apply(x, self.conv.weight, shift, self.conv.geom(False), 1, 0.0, False, self._cache)
+        return Fn.Conv2dFn.apply(x, self.conv.weight, shift, self.conv.geom(False), 1, 0.0, False, self._cache,
+                                 1 if in_relu else 0, 0.0, defer)
+
+
+def _chain(x, convs):
+    """x -> convs[0] -> ... -> convs[-1]; every inner ReLU has one consumer, so
+    its backward is fused into the next conv's data gradient."""
+    for i, m in enumerate(convs):
+        x = m(x, in_relu=i > 0, defer=i + 1 < len(convs))
+    return x
 
 
 def _cat(parts):
@@ -148,8 +160,8 @@ class InceptionA(nn.Module):
 
     def forward(self, x):
         b1 = self.branch1x1(x)
-        b5 = self.branch5x5_2(self.branch5x5_1(x))
-        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x)))
+        b5 = _chain(x, (self.branch5x5_1, self.branch5x5_2))
+        b3 = _chain(x, (self.branch3x3dbl_1, self.branch3x3dbl_2, self.branch3x3dbl_3))
         bp = self.branch_pool(Fn.AvgPool3s1Fn.apply(x))
         return _cat([b1, b5, b3, bp])
 
@@ -164,7 +176,7 @@ class InceptionB(nn.Module):
 
     def forward(self, x):
         b3 = self.branch3x3(x)
-        bd = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x)))
+        bd = _chain(x, (self.branch3x3dbl_1, self.branch3x3dbl_2, self.branch3x3dbl_3))
         return _cat([b3, bd, Fn.MaxPool3s2Fn.apply(x)])
 
 
@@ -185,10 +197,9 @@ class InceptionC(nn.Module):
 
     def forward(self, x):
         b1 = self.branch1x1(x)
-        b7 = self.branch7x7_3(self.branch7x7_2(self.branch7x7_1(x)))
-        bd = self.branch7x7dbl_1(x)
-        for m in (self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4, self.branch7x7dbl_5):
-            bd = m(bd)
+        b7 = _chain(x, (self.branch7x7_1, self.branch7x7_2, self.branch7x7_3))
+        bd = _chain(x, (self.branch7x7dbl_1, self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4,
+                        self.branch7x7dbl_5))
         bp = self.branch_pool(Fn.AvgPool3s1Fn.apply(x))
         return _cat([b1, b7, bd, bp])
 
@@ -204,10 +215,8 @@ class InceptionD(nn.Module):
         self.branch7x7x3_4 = BasicConv2d(192, 192, 3, stride=2)
 
     def forward(self, x):
-        b3 = self.branch3x3_2(self.branch3x3_1(x))
-        b7 = self.branch7x7x3_1(x)
-        for m in (self.branch7x7x3_2, self.branch7x7x3_3, self.branch7x7x3_4):
-            b7 = m(b7)
+        b3 = _chain(x, (self.branch3x3_1, self.branch3x3_2))
+        b7 = _chain(x, (self.branch7x7x3_1, self.branch7x7x3_2, self.branch7x7x3_3, self.branch7x7x3_4))
         return _cat([b3, b7, Fn.MaxPool3s2Fn.apply(x)])
 
 
@@ -226,10 +235,10 @@ class InceptionE(nn.Module):
 
     def forward(self, x):
         b1 = self.branch1x1(x)
-        b3 = self.branch3x3_1(x)
-        b3a, b3b = self.branch3x3_2a(b3), self.branch3x3_2b(b3)
-        bd = self.branch3x3dbl_2(self.branch3x3dbl_1(x))
-        bda, bdb = self.branch3x3dbl_3a(bd), self.branch3x3dbl_3b(bd)
+        b3 = self.branch3x3_1(x, defer=True)  # both consumers gate
+        b3a, b3b = self.branch3x3_2a(b3, in_relu=True), self.branch3x3_2b(b3, in_relu=True)
+        bd = self.branch3x3dbl_2(self.branch3x3dbl_1(x, defer=True), in_relu=True, defer=True)  # both consumers gate
+        bda, bdb = self.branch3x3dbl_3a(bd, in_relu=True), self.branch3x3dbl_3b(bd, in_relu=True)
         bp = self.branch_pool(Fn.AvgPool3s1Fn.apply(x))
         return _cat([b1, b3a, b3b, bda, bdb, bp])
 
@@ -268,12 +277,9 @@ class CNN_ENCODER(nn.Module):
 
     def forward(self, x):
         x = Fn.BilinearFn.apply(x if x.dtype == torch.bfloat16 else Fn.ImageToNhwcFn.apply(x), 299, 299)
-        x = self.Conv2d_1a_3x3(x)
-        x = self.Conv2d_2a_3x3(x)
-        x = self.Conv2d_2b_3x3(x)
+        x = _chain(x, (self.Conv2d_1a_3x3, self.Conv2d_2a_3x3, self.Conv2d_2b_3x3))
         x = Fn.MaxPool3s2Fn.apply(x)
-        x = self.Conv2d_3b_1x1(x)
-        x = self.Conv2d_4a_3x3(x)
+        x = _chain(x, (self.Conv2d_3b_1x1, self.Conv2d_4a_3x3))
         x = Fn.MaxPool3s2Fn.apply(x)
         x = self.Mixed_5b(x)
         x = self.Mixed_5c(x)

@@ -66,6 +66,12 @@ struct ConvArgs {
   int P;                        // N*OH*OW
   int ncls, nsplit;             // parity classes (BWDD stride>1), K splits
   int noload;                   // diagnostics only (EEGAN_CONV_NOLOAD): skip steady-state loads
+  // BWDD only: multiply dx by act'(gate) of the activation `gate_act` expressed
+  // through its output (the activated conv input x): the producer's activation
+  // backward fused into this data gradient (x has no other non-gating consumer)
+  const bf16_t* gate;
+  int ldgate, gate_act;
+  float gate_slope;
 };
 
 // K step kt, 8-channel chunk kc -> kernel tap and channel.  Normal mode: the
@@ -136,6 +142,12 @@ EE_DEV void igemm_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], int 
       for (int r = 0; r < 4; ++r) {
         const float bv = (a.bias && co + r < a.Mrows) ? a.bias[co + r] : 0.f;
         v[r] = act_fwd(acc[i][j][r] + bv, a.act, a.slope);
+      }
+      if (MODE == MODE_BWDD && a.gate) {
+        const bf16_t* gp = a.gate + p * a.ldgate + co;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (co + r < a.Mrows) v[r] *= act_dgrad_from_y(bf2f(gp[r]), a.gate_act, a.gate_slope);
       }
       if (a.res) {
         const bf16_t* rp = a.res + p * a.ldres + co;
@@ -794,6 +806,7 @@ __global__ void conv_splitk_reduce_kernel(ConvArgs a) {
     float v = 0.f;
     for (int z = 0; z < a.nsplit; ++z) v += a.part[(long)z * total + e];
     v = act_fwd(v + (a.bias ? a.bias[co] : 0.f), a.act, a.slope);
+    if (a.gate) v *= act_dgrad_from_y(bf2f(a.gate[p * a.ldgate + co]), a.gate_act, a.gate_slope);
     if (a.res) v = bf2f(a.res[p * a.ldres + co]) + gam * v;
     if (a.out_f32) reinterpret_cast<float*>(a.out)[p * a.ldo + co] = v;
     else reinterpret_cast<bf16_t*>(a.out)[p * a.ldo + co] = f2bf(v);
@@ -1897,7 +1910,7 @@ Plan plan_igemm(const ConvArgs& a, int Pc_max) {
 template <int MODE>
 int try_thin(const ConvArgs& a, hipStream_t s, long src_bytes) {
   if (!env_int("EEGAN_CONV_THIN", 1) || src_bytes >= 0x7fffffffL) return 0;
-  if (a.R != 3 || a.S != 3 || a.st != 1 || a.ncls != 1 || a.res || a.out_f32 || a.Mrows > 32) return 0;
+  if (a.R != 3 || a.S != 3 || a.st != 1 || a.ncls != 1 || a.res || a.gate || a.out_f32 || a.Mrows > 32) return 0;
   if ((a.ldo & 3) || ((uintptr_t)a.out & 7) || (a.lds_src & 7) || ((uintptr_t)a.src & 15)) return 0;
   const int nt = a.Mrows > 16 ? 2 : 1;
   const int nks = a.Cgp == 8 ? 3 : a.Cgp == 32 ? 9 : (a.Cgp == 64 && nt == 1) ? 18 : 0;
@@ -2109,6 +2122,12 @@ int eegan_conv_fwd(const eegan_conv_desc* d, const bf16_t* x, const bf16_t* wpac
 
 int eegan_conv_bwd_data(const eegan_conv_desc* d, const bf16_t* dy, const bf16_t* wpackT, void* dx, int lddx,
                         int dx_f32, float* ws, hipStream_t stream) {
+  return eegan_conv_bwd_data_gated(d, dy, wpackT, dx, lddx, dx_f32, nullptr, 0, 0, 0.f, ws, stream);
+}
+
+int eegan_conv_bwd_data_gated(const eegan_conv_desc* d, const bf16_t* dy, const bf16_t* wpackT, void* dx, int lddx,
+                              int dx_f32, const bf16_t* gate, int ldgate, int gate_act, float gate_slope, float* ws,
+                              hipStream_t stream) {
   if (d->up2) {
     ee_set_error("conv_bwd_data: up2 inputs take the hi-res gradient + sum-pool path");
     return -22;
@@ -2121,6 +2140,10 @@ int eegan_conv_bwd_data(const eegan_conv_desc* d, const bf16_t* dy, const bf16_t
   a.ldo = lddx;
   a.out_f32 = dx_f32;
   a.act = ACT_NONE;
+  a.gate = gate;
+  a.ldgate = ldgate;
+  a.gate_act = gate_act;
+  a.gate_slope = gate_slope;
   if (a.P == 0) return 0;
   if (!ld_ok(d->ldy, dy)) {
     ee_set_error("conv_bwd_data: dy channel stride %d must be a multiple of 8", d->ldy);

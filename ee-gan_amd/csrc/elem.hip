@@ -121,7 +121,8 @@ __global__ __launch_bounds__(NT) void dot_partial_kernel(const bf16_t* x, int ld
 // gradient) and the per-block partials of <g, h> (the gain's gradient)
 __global__ __launch_bounds__(NT) void scale_dot_partial_kernel(const bf16_t* g, int ldg, const bf16_t* h, int ldh,
                                                                const float* gamma, float alpha, long P, int C,
-                                                               bf16_t* out, int ldo, float* ws) {
+                                                               bf16_t* out, int ldo, float* ws, int act,
+                                                               float slope) {
   __shared__ float red[16];
   const int C8 = (C + 7) / 8;
   const bool vec = (ldg % 8 == 0) && (ldh % 8 == 0) && (ldo % 8 == 0);
@@ -136,7 +137,7 @@ __global__ __launch_bounds__(NT) void scale_dot_partial_kernel(const bf16_t* g, 
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       acc += a.v[j] * b.v[j];
-      a.v[j] *= s;
+      a.v[j] *= act ? s * act_dgrad_from_y(b.v[j], act, slope) : s;
     }
     store8(out + p * ldo + c0, a, nv, vec);
   }
@@ -575,9 +576,10 @@ int eegan_dot(const uint16_t* x, int ldx, const uint16_t* y, int ldy, long P, in
 }
 
 int eegan_scale_dot(const uint16_t* g, int ldg, const uint16_t* h, int ldh, const float* gamma, float alpha, long P,
-                    int C, uint16_t* out, int ldo, float* ws, float* dot_out, int accumulate, hipStream_t s) {
+                    int C, uint16_t* out, int ldo, float* ws, float* dot_out, int accumulate, int act, float slope,
+                    hipStream_t s) {
   const int blocks = std::min(1024, grid_for(P * ((C + 7) / 8)));
-  scale_dot_partial_kernel<<<blocks, NT, 0, s>>>(g, ldg, h, ldh, gamma, alpha, P, C, out, ldo, ws);
+  scale_dot_partial_kernel<<<blocks, NT, 0, s>>>(g, ldg, h, ldh, gamma, alpha, P, C, out, ldo, ws, act, slope);
   int rc = ee_check_launch("scale_dot_partial");
   if (rc) return rc;
   dot_final_kernel<<<1, 1024, 0, s>>>(ws, blocks, 1.f, dot_out, accumulate);

@@ -53,6 +53,7 @@ _SIGS = {
     'eegan_conv_bwd_data_workspace': ([CD], L),
     'eegan_conv_fwd': ([CD, P, P, P, I, F, P, I, P, P, I, P, P], I),
     'eegan_conv_bwd_data': ([CD, P, P, P, I, I, P, P], I),
+    'eegan_conv_bwd_data_gated': ([CD, P, P, P, I, I, P, I, I, F, P, P], I),
     'eegan_conv_wgrad_workspace': ([CD], L),
     'eegan_conv_bwd_weight': ([CD, P, P, P, P, I, P], I),
     'eegan_bn_stats_workspace': ([L, I], L),
@@ -64,7 +65,7 @@ _SIGS = {
     'eegan_bnmod_bwd_dx': ([BD, P, I, P, D, P, I, P], I),
     'eegan_act_bwd': ([P, I, P, I, L, I, I, F, P, I, P], I),
     'eegan_scale_add': ([P, I, P, I, P, F, L, I, P, I, P], I),
-    'eegan_scale_dot': ([P, I, P, I, P, F, L, I, P, I, P, P, I, P], I),
+    'eegan_scale_dot': ([P, I, P, I, P, F, L, I, P, I, P, P, I, I, F, P], I),
     'eegan_dot_workspace': ([], L),
     'eegan_dot': ([P, I, P, I, L, I, F, P, P, I, P], I),
     'eegan_chansum_workspace': ([L, I], L),
@@ -127,6 +128,10 @@ def _load():
 
 LIB = _load()
 ABI_VERSION = LIB.eegan_abi_version()
+EXPECTED_ABI = 3
+if ABI_VERSION != EXPECTED_ABI:
+    raise ImportError('%s has ABI %d, these bindings need %d: rebuild (make -C ee-gan_amd/csrc)'
+                      % (LIB_PATH, ABI_VERSION, EXPECTED_ABI))
 
 
 class HipError(RuntimeError):

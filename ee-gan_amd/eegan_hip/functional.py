@@ -232,8 +232,12 @@ def conv_fwd_raw(x, W, b, g, act=0, slope=0.2, out_f32=False, cache=None, res=No
     return y
 
 
-def conv_bwd_data_raw(dz, W, g, x_shape, cache=None):
-    """dx for the LOGICAL input grid (hi-res when g.up2), NHWC bf16."""
+def conv_bwd_data_raw(dz, W, g, x_shape, cache=None, gate=None, gate_act=0, gate_slope=0.2):
+    """dx for the LOGICAL input grid (hi-res when g.up2), NHWC bf16.  `gate`
+    (the activated conv input, act code gate_act): dx *= act'(gate) in the
+    epilogue -- the producing layer's activation backward, fused."""
+    if gate is not None and g.up2:
+        raise ValueError('conv_bwd_data_raw: gated data gradients of up2 convs are not supported')
     N, C, H, Wd = x_shape
     Hl, Wl = (H * 2, Wd * 2) if g.up2 else (H, Wd)
     dx = empty_nhwc(N, C, Hl, Wl, dz.device)
@@ -247,9 +251,14 @@ def conv_bwd_data_raw(dz, W, g, x_shape, cache=None):
     Ho, Wo = d.Ho, d.Wo
     flops = 2.0 * N * Ho * Wo * g.K * C * g.R * g.S
     nbytes = 2.0 * (N * Hl * Wl * C + N * Ho * Wo * g.K + g.K * C * g.R * g.S)
-    _launch('conv_bwd_data', flops, nbytes, lambda: ops.conv_bwd_data(
-        d, dz.data_ptr(), wp.data_ptr(), dx.data_ptr(), ld_of(dx), 0, ptr(ws), stream()),
-        key=_shape_key(d) if TIMER is not None else None)
+    if gate is None:
+        _launch('conv_bwd_data', flops, nbytes, lambda: ops.conv_bwd_data(
+            d, dz.data_ptr(), wp.data_ptr(), dx.data_ptr(), ld_of(dx), 0, ptr(ws), stream()),
+            key=_shape_key(d) if TIMER is not None else None)
+    else:
+        _launch('conv_bwd_data', flops, nbytes, lambda: ops.conv_bwd_data_gated(
+            d, dz.data_ptr(), wp.data_ptr(), dx.data_ptr(), ld_of(dx), 0, gate.data_ptr(), ld_of(gate), gate_act,
+            gate_slope, ptr(ws), stream()), key=_shape_key(d) if TIMER is not None else None)
     if g.up2:
         lo = empty_nhwc(N, C, H, Wd, dz.device)
         ops.sumpool2(dx.data_ptr(), N, Hl, Wl, C, ld_of(dx), lo.data_ptr(), ld_of(lo), stream())
@@ -299,14 +308,30 @@ def _as_bf16_grad(g):
     return to_nhwc_bf16(g)
 
 
+# EEGAN_FUSE_ACT_BWD=0: every activation backward runs as its own pass (A/B switch).
+FUSE_ACT_BWD = os.environ.get('EEGAN_FUSE_ACT_BWD', '1') != '0'
+
+
 class Conv2dFn(torch.autograd.Function):
-    """y = act(conv(x, W) + b); NHWC bf16 in, bf16 (or fp32) out."""
+    """y = act(conv(x, W) + b); NHWC bf16 in, bf16 (or fp32) out.
+
+    Activation backward fused across a single-consumer link (first-order
+    backward only; under create_graph both sides fall back to ActBwdFn):
+    `in_act` = activation that produced x (x = act(z) of a layer called with
+    `defer_act=True`): dx is multiplied by act'(x) in the data-gradient
+    epilogue, and the producer passes its incoming gradient on unmasked.  The
+    factor distributes over a sum of gradients, so x may have several
+    consumers as long as every one of them gates (models decide: resD,
+    DiscSent/DiscCond heads, Inception branch chains)."""
 
     @staticmethod
-    def forward(ctx, x, W, b, g, act, slope, out_f32, cache):
+    def forward(ctx, x, W, b, g, act, slope, out_f32, cache, in_act=0, in_slope=0.2, defer_act=False):
         x = to_nhwc_bf16(x)
+        if in_act and g.up2:
+            raise ValueError('Conv2dFn: in_act with up2 is not supported')
         y = conv_fwd_raw(x, W, b, g, act, slope, out_f32, cache)
         ctx.g, ctx.act, ctx.slope, ctx.cache = g, act, slope, cache
+        ctx.in_act, ctx.in_slope, ctx.defer_act = in_act, in_slope, defer_act
         ctx.x_shape = tuple(x.shape)
         ctx.save_for_backward(x, W, y if act else None)
         return y
@@ -316,11 +341,15 @@ class Conv2dFn(torch.autograd.Function):
         x, W, y = ctx.saved_tensors
         g = ctx.g
         gy = _as_bf16_grad(gy)
-        dz = ActBwdFn.apply(gy, y, ctx.act, ctx.slope) if ctx.act else gy
+        fused = FUSE_ACT_BWD and not torch.is_grad_enabled()
+        dz = ActBwdFn.apply(gy, y, ctx.act, ctx.slope) if ctx.act and not (fused and ctx.defer_act) else gy
         dx = dW = db = None
         if _needed(ctx, 0):
             if g.up2:
                 dx = conv_bwd_data_raw(dz, W, g, ctx.x_shape, ctx.cache)
+            elif fused and ctx.in_act:
+                dx = conv_bwd_data_raw(dz, W, g, ctx.x_shape, ctx.cache, gate=x, gate_act=ctx.in_act,
+                                       gate_slope=ctx.in_slope)
             else:
                 dx = ConvBwdDataFn.apply(dz, W, g, ctx.x_shape, ctx.cache)
         if _needed(ctx, 1):
@@ -335,7 +364,7 @@ class Conv2dFn(torch.autograd.Function):
                 chansum_raw(dz, out=sink)
             else:
                 db = ChanSumFn.apply(dz)
-        return dx, dW, db, None, None, None, None, None
+        return dx, dW, db, None, None, None, None, None, None, None, None
 
 
 class ConvBwdDataFn(torch.autograd.Function):
@@ -537,7 +566,9 @@ class ScaleAddFn(torch.autograd.Function):
     """out = res + gamma * h   (gamma: fp32 (1,) parameter; models.py:122,142,278)."""
 
     @staticmethod
-    def forward(ctx, res, h, gamma):
+    def forward(ctx, res, h, gamma, h_act=0, h_slope=0.2):
+        """h_act: activation that produced h in a layer called with defer_act=True
+        (first-order backward folds its derivative into gamma * g; see Conv2dFn)."""
         res = to_nhwc_bf16(res)
         h = to_nhwc_bf16(h)
         N, C, H, W = h.shape
@@ -545,6 +576,7 @@ class ScaleAddFn(torch.autograd.Function):
         ops.scale_add(res.data_ptr(), ld_of(res), h.data_ptr(), ld_of(h), gamma.data_ptr(), 1.0, N * H * W, C,
                       out.data_ptr(), ld_of(out), stream())
         ctx.save_for_backward(h, gamma)
+        ctx.h_act, ctx.h_slope = h_act, h_slope
         return out
 
     @staticmethod
@@ -552,23 +584,26 @@ class ScaleAddFn(torch.autograd.Function):
         h, gamma = ctx.saved_tensors
         g = _as_bf16_grad(g)
         d_res = g if ctx.needs_input_grad[0] else None
-        if not torch.is_grad_enabled() and _needed(ctx, 1) and _needed(ctx, 2):
-            # first-order: gamma * g and <g, h> in one pass, the gain's gradient
-            # accumulated straight into gamma.grad when that is the sink
+        h_act = ctx.h_act if FUSE_ACT_BWD else 0
+        if not torch.is_grad_enabled() and _needed(ctx, 1) and (_needed(ctx, 2) or h_act):
+            # first-order: gamma * g [* act'(h)] and <g, h> in one pass, the gain's
+            # gradient accumulated straight into gamma.grad when that is the sink
             N, C, H, W = g.shape
             d_h = empty_nhwc(N, C, H, W, g.device)
-            sink = _grad_sink(ctx, 2)
+            sink = _grad_sink(ctx, 2) if _needed(ctx, 2) else None
             d_g = None
             if sink is None:
                 d_g = torch.empty(1, dtype=F32, device=g.device)
             ws = workspace(ops.dot_workspace(), g.device)
             ops.scale_dot(g.data_ptr(), ld_of(g), h.data_ptr(), ld_of(h), gamma.data_ptr(), 1.0, N * H * W, C,
                           d_h.data_ptr(), ld_of(d_h), ws.data_ptr(), (sink if d_g is None else d_g).data_ptr(),
-                          int(d_g is None), stream())
-            return d_res, d_h, d_g
+                          int(d_g is None), h_act, ctx.h_slope, stream())
+            if not _needed(ctx, 2):
+                d_g = None
+            return d_res, d_h, d_g, None, None
         d_h = ScaleFn.apply(g, gamma) if ctx.needs_input_grad[1] else None
         d_g = DotFn.apply(g, h) if ctx.needs_input_grad[2] else None
-        return d_res, d_h, d_g
+        return d_res, d_h, d_g, None, None
 
 
 class ScaleFn(torch.autograd.Function):

@@ -18,8 +18,10 @@ def _pair(v):
 
 class Conv2d(nn.Module):
     """nn.Conv2d-compatible (weight (Cout,Cin,kh,kw) stored channels-last, optional bias).
-    forward(x, act=None, slope=0.2, out_f32=False, up2=False): the activation
-    is fused into the epilogue and up2 reads x through a nearest-2x upsample."""
+    forward(x, act=None, slope=0.2, out_f32=False, up2=False, in_act=None, defer_act=False):
+    the activation is fused into the epilogue and up2 reads x through a
+    nearest-2x upsample; in_act / defer_act fuse an activation's backward
+    into the consuming conv's data gradient (Fn.Conv2dFn)."""
 
     def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, bias=True):
         super().__init__()
@@ -51,9 +53,12 @@ class Conv2d(nn.Module):
             self._geo[up2] = g
         return g
 
-    def forward(self, x, act=None, slope=0.2, out_f32=False, up2=False):
+    def forward(self, x, act=None, slope=0.2, out_f32=False, up2=False, in_act=None, in_slope=0.2,
+                defer_act=False):
+        """in_act / defer_act: fused activation backward across a single-consumer
+        link (see Fn.Conv2dFn)."""
         return Fn.Conv2dFn.apply(x, self.weight, self.bias, self.geom(up2), ACT_CODES[act], slope, out_f32,
-                                 self._cache)
+                                 self._cache, ACT_CODES[in_act], in_slope, defer_act)
 
     def extra_repr(self):
         return '%d, %d, kernel_size=%s, stride=%d, padding=%s, bias=%s' % (

@@ -281,7 +281,8 @@ class resD(nn.Module):
         self.gamma = nn.Parameter(torch.zeros(1))
 
     def forward(self, x):
-        return Fn.ScaleAddFn.apply(self.shortcut(x), self.residual(x), self.gamma)
+        # residual()'s last LeakyReLU is deferred to ScaleAddFn's backward
+        return Fn.ScaleAddFn.apply(self.shortcut(x), self.residual(x), self.gamma, Fn.ACT_CODES['lrelu'], 0.2)
 
     def shortcut(self, x):
         if self.downsample:
@@ -291,8 +292,10 @@ class resD(nn.Module):
         return x
 
     def residual(self, x):
-        h = self.conv_r[0](x, act='lrelu', slope=0.2)
-        return self.conv_r[2](h, act='lrelu', slope=0.2)
+        # each LeakyReLU's backward runs inside its only consumer's backward
+        # (the next conv's data gradient, ScaleAddFn): Conv2dFn in_act / defer_act
+        h = self.conv_r[0](x, act='lrelu', slope=0.2, defer_act=True)
+        return self.conv_r[2](h, act='lrelu', slope=0.2, in_act='lrelu', defer_act=True)
 
 
 class DiscSent(nn.Module):
@@ -307,8 +310,8 @@ class DiscSent(nn.Module):
 
     def forward(self, feat, cond):
         h = Fn.CatTileFn.apply(feat, cond.reshape(-1, self.ef_dim))
-        h = self.joint_conv[0](h, act='lrelu', slope=0.2)
-        return self.joint_conv[2](h, out_f32=True)
+        h = self.joint_conv[0](h, act='lrelu', slope=0.2, defer_act=True)
+        return self.joint_conv[2](h, out_f32=True, in_act='lrelu')
 
 
 class DiscCond(nn.Module):
@@ -326,9 +329,9 @@ class DiscCond(nn.Module):
 
     def forward(self, img_code, c_code):
         h = Fn.CatTileFn.apply(img_code, c_code.reshape(-1, self.nef))
-        h = self.joinConv[0](h, act='lrelu', slope=0.2)
-        pair = self.pair_node(h, out_f32=True).reshape(-1)
-        cls = self.class_node(h, out_f32=True).reshape(-1, self.ndf * 2)
+        h = self.joinConv[0](h, act='lrelu', slope=0.2, defer_act=True)  # both consumers gate
+        pair = self.pair_node(h, out_f32=True, in_act='lrelu').reshape(-1)
+        cls = self.class_node(h, out_f32=True, in_act='lrelu').reshape(-1, self.ndf * 2)
         return pair, self.class_linear(cls)
 
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 2  /* 2: fp32 conv weights channels-last */
+#define EEGAN_ABI_VERSION 3  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
@@ -83,6 +83,12 @@ int eegan_conv_fwd(const eegan_conv_desc* d, const uint16_t* x, const uint16_t* 
  * s*s parity classes that visit only their valid taps */
 int eegan_conv_bwd_data(const eegan_conv_desc* d, const uint16_t* dy, const uint16_t* wpackT, void* dx,
                         int lddx, int dx_f32, float* ws, hipStream_t stream);
+/* the same, times act'(gate) of activation gate_act expressed through its output `gate` (the activated
+ * conv input, channel stride ldgate): the producing layer's activation backward (models.py:262-288
+ * LeakyReLU, Inception BasicConv2d ReLU) fused into this data gradient */
+int eegan_conv_bwd_data_gated(const eegan_conv_desc* d, const uint16_t* dy, const uint16_t* wpackT, void* dx,
+                              int lddx, int dx_f32, const uint16_t* gate, int ldgate, int gate_act,
+                              float gate_slope, float* ws, hipStream_t stream);
 /* dW[Cout][R][S][Cin] (fp32, channels-last like W) = sum_pixels dy x im2col(x); split-K slabs in ws */
 long eegan_conv_wgrad_workspace(const eegan_conv_desc* d);
 int eegan_conv_bwd_weight(const eegan_conv_desc* d, const uint16_t* x, const uint16_t* dy, float* ws, float* dw,
@@ -138,10 +144,12 @@ int eegan_act_bwd(const uint16_t* dy, int lddy, const uint16_t* y, int ldy, long
                   uint16_t* dx, int lddx, hipStream_t s);
 int eegan_scale_add(const uint16_t* x, int ldx, const uint16_t* y, int ldy, const float* gamma, float alpha, long P,
                     int C, uint16_t* out, int ldo, hipStream_t s);
-/* ScaleAdd backward (models.py:122,142,278 first-order): out = alpha*gamma*g and
- * dot_out (+)= <g, h>, one pass over g; ws = eegan_dot_workspace() bytes */
+/* ScaleAdd backward (models.py:122,142,278 first-order): out = alpha*gamma*g [* act'(h)] and
+ * dot_out (+)= <g, h>, one pass over g; act != 0 folds the backward of the activation that produced h
+ * (resD's second LeakyReLU); ws = eegan_dot_workspace() bytes */
 int eegan_scale_dot(const uint16_t* g, int ldg, const uint16_t* h, int ldh, const float* gamma, float alpha, long P,
-                    int C, uint16_t* out, int ldo, float* ws, float* dot_out, int accumulate, hipStream_t stream);
+                    int C, uint16_t* out, int ldo, float* ws, float* dot_out, int accumulate, int act, float slope,
+                    hipStream_t stream);
 long eegan_dot_workspace(void);
 int eegan_dot(const uint16_t* x, int ldx, const uint16_t* y, int ldy, long P, int C, float scale, float* ws,
               float* out, int accumulate, hipStream_t s);

@@ -235,6 +235,40 @@ def test_generator_grouped_mlps_match_per_layer(gpu, monkeypatch):
     assert torch.allclose(s0, s1, rtol=1e-4, atol=1e-6) and torch.allclose(a0, a1, rtol=1e-4, atol=1e-6)
 
 
+def test_fused_activation_backward_matches_separate(gpu, monkeypatch):
+    """Activation backward fused into the consuming conv's data gradient /
+    ScaleAddFn (resD, D heads, Inception branch chains) against the separate
+    act_bwd passes (EEGAN_FUSE_ACT_BWD=0).  The fused product is taken on the
+    fp32 accumulator before the one bf16 rounding (the separate pass rounds
+    twice), so values agree to bf16 rounding, not bit for bit."""
+    import models
+    from DAMSM import CNN_ENCODER
+    from eegan_hip import functional as Fn
+    from eegan_hip.tensor import to_nhwc_bf16
+    from _util import rel_l2
+    D = _load(models.Dis256(8, True, 10), 'dis256', 30 + 256, gpu)
+    E = CNN_ENCODER(256).to(gpu)
+    x = seeded_tensor('fa:x', (2, 3, 256, 256), 1, 'uniform').to(gpu)
+    s = seeded_tensor('fa:s', (2, 256), 1).to(gpu)
+    res = []
+    for fuse in (False, True):
+        monkeypatch.setattr(Fn, 'FUSE_ACT_BWD', fuse)
+        D.zero_grad(set_to_none=True)
+        xi = to_nhwc_bf16(x).detach().requires_grad_()
+        pair, cls = D.COND_DNET(D(xi), s)
+        (pair.sum() + cls.square().sum()).backward()
+        xe = x.detach().clone().requires_grad_()
+        feats, code = E(xe)
+        (feats.square().sum() + code.sum()).backward()
+        res.append((xi.grad.float().cpu(), xe.grad.cpu(),
+                    {n: p.grad.cpu() for n, p in D.named_parameters() if p.grad is not None}))
+    (gx0, ge0, gp0), (gx1, ge1, gp1) = res
+    assert rel_l2(gx1, gx0) < 2e-2 and rel_l2(ge1, ge0) < 2e-2
+    assert set(gp0) == set(gp1)
+    for n in gp0:
+        assert rel_l2(gp1[n], gp0[n]) < 2e-2, n
+
+
 @pytest.mark.parametrize('kind', [64, 128, 256])
 def test_discriminator_and_gradient_penalty(gpu, kind):
     import models
