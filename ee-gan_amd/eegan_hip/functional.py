@@ -1197,6 +1197,89 @@ class DoutReduceFn(torch.autograd.Function):
         return dx.reshape(ctx.shape), None
 
 
+class DoutReduce3Fn(torch.autograd.Function):
+    """The three D-loss reductions of a batched head output x = [real; mismatch;
+    fake] (Trainer._d_heads_batched): DoutReduceFn on x[0:B] (mode m0),
+    x[2B:3B] (m1), x[B:2B] (m2) -- one gradient buffer for x instead of a
+    zero-filled buffer, a copy and an add per slice."""
+
+    @staticmethod
+    def forward(ctx, x, B, modes):
+        xc = x.float().contiguous()
+        per = xc.numel() // 3
+        outs = [torch.empty((), dtype=F32, device=x.device) for _ in range(3)]
+        for o, sl, m in zip(outs, (0, 2, 1), modes):
+            ops.dout_reduce(xc.data_ptr() + 4 * sl * per, per, m, o.data_ptr(), stream())
+        ctx.modes, ctx.shape = modes, x.shape
+        ctx.save_for_backward(xc)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        (xc,) = ctx.saved_tensors
+        per = xc.numel() // 3
+        dx = torch.empty_like(xc)
+        for g, sl, m in zip(gs, (0, 2, 1), ctx.modes):
+            g = torch.zeros(1, dtype=F32, device=xc.device) if g is None else g.float().reshape(1).contiguous()
+            ops.dout_reduce_bwd(xc.data_ptr() + 4 * sl * per, per, m, g.data_ptr(), dx.data_ptr() + 4 * sl * per,
+                                stream())
+        return dx.reshape(ctx.shape), None, None
+
+
+class BceLogits3Fn(torch.autograd.Function):
+    """BceLogitsFn(x[0:B], t), (x[2B:3B], t), (x[B:2B], t) of a batched class
+    head output, with one gradient buffer (see DoutReduce3Fn)."""
+
+    @staticmethod
+    def forward(ctx, x, target):
+        xc = x.float().contiguous()
+        tc = target.float().contiguous()
+        per = xc.numel() // 3
+        outs = [torch.empty((), dtype=F32, device=x.device) for _ in range(3)]
+        for o, sl in zip(outs, (0, 2, 1)):
+            ops.bce_logits(xc.data_ptr() + 4 * sl * per, tc.data_ptr(), per, o.data_ptr(), stream())
+        ctx.shape = x.shape
+        ctx.save_for_backward(xc, tc)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        xc, tc = ctx.saved_tensors
+        per = xc.numel() // 3
+        dx = torch.empty_like(xc)
+        for g, sl in zip(gs, (0, 2, 1)):
+            g = torch.zeros(1, dtype=F32, device=xc.device) if g is None else g.float().reshape(1).contiguous()
+            ops.bce_logits_bwd(xc.data_ptr() + 4 * sl * per, tc.data_ptr(), per, g.data_ptr(),
+                               dx.data_ptr() + 4 * sl * per, stream())
+        return dx.reshape(ctx.shape), None
+
+
+class HeadsGatherFn(torch.autograd.Function):
+    """[f[:B]; f[:B]; f[B:]] of a batched [real; fake] D feature map (the
+    real / mismatch / fake head inputs) in 2 copies; backward in one add and
+    one copy instead of slice-backward zero fills, copies and adds."""
+
+    @staticmethod
+    def forward(ctx, feat, B):
+        feat = to_nhwc_bf16(feat)
+        N, C, H, W = feat.shape
+        out = empty_nhwc(N + B, C, H, W, feat.device)
+        out[:2 * B].unflatten(0, (2, B)).copy_(feat[:B].unsqueeze(0).expand(2, B, C, H, W))
+        out[2 * B:].copy_(feat[B:])
+        ctx.B, ctx.N = B, N
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        B, N = ctx.B, ctx.N
+        g = _as_bf16_grad(g)
+        _, C, H, W = g.shape
+        gf = empty_nhwc(N, C, H, W, g.device)
+        torch.add(g[:B], g[B:2 * B], out=gf[:B])
+        gf[B:].copy_(g[2 * B:])
+        return gf, None
+
+
 class BceLogitsFn(torch.autograd.Function):
     """F.binary_cross_entropy_with_logits(x, target) (mean)."""
 

@@ -103,8 +103,7 @@ class Trainer(object):
     def _d_heads_batched(imgs, fake_imgs, sent_emb, wrong_sent_emb, netD):
         B = imgs.shape[0]
         feat = netD(Fn.BatchCatFn.apply(imgs, fake_imgs.detach()))
-        real, fake = feat[:B], feat[B:]
-        heads = Fn.BatchCatFn.apply(real, real, fake)
+        heads = Fn.HeadsGatherFn.apply(feat, B)  # [real; real; fake]
         cond = torch.cat([sent_emb.reshape(B, -1), wrong_sent_emb.reshape(B, -1), sent_emb.reshape(B, -1)], 0)
         return netD.module.COND_DNET(heads, cond), B
 
@@ -113,8 +112,7 @@ class Trainer(object):
         """train.py:336-353."""
         if Trainer.DBATCH:
             out, B = Trainer._d_heads_batched(imgs, fake_imgs, sent_emb, wrong_sent_emb, netD)
-            return (Fn.DoutReduceFn.apply(out[:B], 0), Fn.DoutReduceFn.apply(out[2 * B:], 1),
-                    Fn.DoutReduceFn.apply(out[B:2 * B], 1))
+            return Fn.DoutReduce3Fn.apply(out, B, (0, 1, 1))  # real, fake, mismatch
         real_features = netD(imgs)
         real_out = netD.module.COND_DNET(real_features, sent_emb)
         errD_real = Fn.DoutReduceFn.apply(real_out, 0)
@@ -130,10 +128,8 @@ class Trainer(object):
         """train.py:355-376."""
         if Trainer.DBATCH:
             (sent_out, class_out), B = Trainer._d_heads_batched(imgs, fake_imgs, sent_emb, unpair_sent_emb, netD)
-            return (Fn.DoutReduceFn.apply(sent_out[:B], 0), Fn.DoutReduceFn.apply(sent_out[2 * B:], 1),
-                    Fn.DoutReduceFn.apply(sent_out[B:2 * B], 1), Fn.BceLogitsFn.apply(class_out[:B], class_labels),
-                    Fn.BceLogitsFn.apply(class_out[2 * B:], class_labels),
-                    Fn.BceLogitsFn.apply(class_out[B:2 * B], class_labels))
+            return (*Fn.DoutReduce3Fn.apply(sent_out, B, (0, 1, 1)),  # real, fake, mismatch
+                    *Fn.BceLogits3Fn.apply(class_out, class_labels))
         real_feature = netD(imgs)
         real_sent_out, real_class_out = netD.module.COND_DNET(real_feature, sent_emb)
         errD_real = Fn.DoutReduceFn.apply(real_sent_out, 0)
