@@ -93,6 +93,28 @@ __global__ void scale_add_kernel(const bf16_t* x, int ldx, const bf16_t* y, int 
   }
 }
 
+// torch.cat(parts, 1) of NHWC bf16 activations in one launch (every part's
+// channel count a multiple of 8, so each 16-B output chunk has one source)
+constexpr int CAT_MAX = 8;
+struct CatParts {
+  const bf16_t* p[CAT_MAX];
+  int ld[CAT_MAX];
+  int c0[CAT_MAX + 1];
+  int n;
+};
+
+__global__ void cat_channels_kernel(const CatParts parts, long P, bf16_t* out, int ldo) {
+  const int C8 = parts.c0[parts.n] / 8;
+  GRID_LOOP(e, P * C8) {
+    const long p = e / C8;
+    const int c = (int)(e % C8) * 8;
+    int j = 0;
+    while (j + 1 < parts.n && parts.c0[j + 1] <= c) ++j;
+    const uint4 v = *reinterpret_cast<const uint4*>(parts.p[j] + p * parts.ld[j] + (c - parts.c0[j]));
+    *reinterpret_cast<uint4*>(out + p * ldo + c) = v;
+  }
+}
+
 // partial sums of x*y (or x when y == null) per block -> ws[block]
 __global__ __launch_bounds__(NT) void dot_partial_kernel(const bf16_t* x, int ldx, const bf16_t* y, int ldy, long P,
                                                          int C, float* ws) {
@@ -561,6 +583,27 @@ int eegan_scale_add(const uint16_t* x, int ldx, const uint16_t* y, int ldy, cons
                     int C, uint16_t* out, int ldo, hipStream_t s) {
   scale_add_kernel<<<grid_for(P * ((C + 7) / 8)), NT, 0, s>>>(x, ldx, y, ldy, gamma, alpha, P, C, out, ldo);
   return ee_check_launch("scale_add");
+}
+
+int eegan_cat_channels(const uint16_t* const* parts, const int* lds, const int* Cs, int n, long P, uint16_t* out,
+                       int ldo, hipStream_t s) {
+  if (n < 1 || n > CAT_MAX || (ldo % 8) || ((uintptr_t)out & 15)) {
+    ee_set_error("cat_channels: %d parts (1..%d), ldo %d", n, CAT_MAX, ldo);
+    return -22;
+  }
+  CatParts cp{};
+  cp.n = n;
+  for (int i = 0; i < n; ++i) {
+    if ((Cs[i] % 8) || (lds[i] % 8) || ((uintptr_t)parts[i] & 15)) {
+      ee_set_error("cat_channels: part %d needs C, ld multiples of 8 and 16-B alignment", i);
+      return -22;
+    }
+    cp.p[i] = parts[i];
+    cp.ld[i] = lds[i];
+    cp.c0[i + 1] = cp.c0[i] + Cs[i];
+  }
+  cat_channels_kernel<<<grid_for(P * (cp.c0[n] / 8)), NT, 0, s>>>(cp, P, out, ldo);
+  return ee_check_launch("cat_channels");
 }
 
 long eegan_dot_workspace(void) { return 1024 * sizeof(float); }

@@ -65,6 +65,7 @@ _SIGS = {
     'eegan_bnmod_bwd_dx': ([BD, P, I, P, D, P, I, P], I),
     'eegan_act_bwd': ([P, I, P, I, L, I, I, F, P, I, P], I),
     'eegan_scale_add': ([P, I, P, I, P, F, L, I, P, I, P], I),
+    'eegan_cat_channels': ([P, P, P, I, L, P, I, P], I),
     'eegan_scale_dot': ([P, I, P, I, P, F, L, I, P, I, P, P, I, I, F, P], I),
     'eegan_dot_workspace': ([], L),
     'eegan_dot': ([P, I, P, I, L, I, F, P, P, I, P], I),

@@ -144,6 +144,10 @@ int eegan_act_bwd(const uint16_t* dy, int lddy, const uint16_t* y, int ldy, long
                   uint16_t* dx, int lddx, hipStream_t s);
 int eegan_scale_add(const uint16_t* x, int ldx, const uint16_t* y, int ldy, const float* gamma, float alpha, long P,
                     int C, uint16_t* out, int ldo, hipStream_t s);
+/* out[:, c0_i : c0_i + Cs[i]] = parts[i] for n <= 8 NHWC parts of P pixels (channel counts, strides multiples
+ * of 8): the Inception branch concat (torchvision Inception3 torch.cat(outputs, 1)) in one launch */
+int eegan_cat_channels(const uint16_t* const* parts, const int* lds, const int* Cs, int n, long P, uint16_t* out,
+                       int ldo, hipStream_t s);
 /* ScaleAdd backward (models.py:122,142,278 first-order): out = alpha*gamma*g [* act'(h)] and
  * dot_out (+)= <g, h>, one pass over g; act != 0 folds the backward of the activation that produced h
  * (resD's second LeakyReLU); ws = eegan_dot_workspace() bytes */

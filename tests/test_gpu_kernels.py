@@ -148,6 +148,26 @@ def test_conv_thin_wgrad(gpu, monkeypatch):
         assert torch.allclose(outs[0], outs[1], rtol=1e-5, atol=1e-4)
 
 
+def test_cat_channels(gpu):
+    """Inception branch concat (one launch when every part has C % 8 == 0,
+    else the per-part path) against torch.cat, with strided (sliced) parts."""
+    Fn, T, _ = _mods()
+    torch.manual_seed(5)
+    for Cs in [(64, 64, 96, 32), (320, 384, 384, 384, 384, 192), (8, 12, 16)]:
+        src = [torch.randn(3, c, 5, 7) for c in Cs]
+        parts = []
+        for i, t in enumerate(src):
+            if i == 1:  # a channel slice of a wider NHWC buffer (ld > C)
+                big = _nhwc(torch.randn(3, t.shape[1] + 16, 5, 7), gpu)
+                big[:, 8:8 + t.shape[1]].copy_(t.to(gpu).to(torch.bfloat16))
+                parts.append(big[:, 8:8 + t.shape[1]])
+            else:
+                parts.append(_nhwc(t, gpu))
+        out = Fn.CatChannelsFn.apply(*parts)
+        ref = torch.cat([_bf(t) for t in src], 1)
+        assert torch.equal(out.float().cpu(), ref)
+
+
 @pytest.mark.parametrize('case', CONV_CASES, ids=[str(i) for i in range(len(CONV_CASES))])
 def test_conv_fwd_bwd(gpu, case):
     Fn, T, Conv2d = _mods()
