@@ -11,6 +11,8 @@ training step (train.py:241-248), so every BasicConv2d's BatchNorm is folded
 into the conv weights/bias and the ReLU into the conv epilogue; the encoder
 runs forward + input-gradient backward on the bf16 MFMA conv kernels.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -147,6 +149,50 @@ def _cat(parts):
     return Fn.CatChannelsFn.apply(*parts)
 
 
+# EEGAN_FUSE_1X1=0: the branch 1x1 convs that share a block input run separately.
+FUSE_1X1 = os.environ.get('EEGAN_FUSE_1X1', '1') != '0'
+
+
+class _Stacked1x1:
+    """The 1x1 BasicConv2d branches of an Inception block that read the same
+    input, run as ONE conv with their (BN-folded) weights stacked along the
+    output channels; the branches take channel-slice views of its output
+    (Fn.SplitChannelsFn).  Forward: 1 launch instead of k; backward: one data
+    gradient over the assembled slice gradients instead of k of them and k-1
+    gradient adds.  Frozen encoder: the stacked weights are rebuilt only when
+    a member's parameters or BN statistics change."""
+
+    def __init__(self, mods):
+        self.mods = list(mods)
+        self.key = None
+
+    def _build(self):
+        key = tuple((m.bn.weight._version, m.bn.bias._version, m.bn.running_mean._version,
+                     m.bn.running_var._version, m.conv.weight._version, m.conv.weight.data_ptr()) for m in self.mods)
+        if key != self.key:
+            with torch.no_grad():
+                ws, scales, shifts = [], [], []
+                for m in self.mods:
+                    bn = m.bn
+                    sc = (bn.weight / torch.sqrt(bn.running_var + bn.eps)).float()
+                    ws.append(m.conv.weight.detach().float())
+                    scales.append(sc)
+                    shifts.append((bn.bias - bn.running_mean * sc).float())
+                self.W = torch.cat(ws, 0).contiguous(memory_format=torch.channels_last)
+                self.shift = torch.cat(shifts).contiguous()
+                self.cache = Fn.PackCache(torch.cat(scales).contiguous())
+                self.sizes = tuple(m.conv.out_channels for m in self.mods)
+                self.geom = Fn.Geom(sum(self.sizes), 1, 1, 1, 0, 0, 0)
+            self.key = key
+
+    def __call__(self, x):
+        if not FUSE_1X1:
+            return tuple(m(x) for m in self.mods)
+        self._build()
+        y = Fn.Conv2dFn.apply(x, self.W, self.shift, self.geom, 1, 0.0, False, self.cache)
+        return Fn.SplitChannelsFn.apply(y, self.sizes)
+
+
 class InceptionA(nn.Module):
     def __init__(self, in_channels, pool_features):
         super().__init__()
@@ -157,11 +203,12 @@ class InceptionA(nn.Module):
         self.branch3x3dbl_2 = BasicConv2d(64, 96, 3, padding=1)
         self.branch3x3dbl_3 = BasicConv2d(96, 96, 3, padding=1)
         self.branch_pool = BasicConv2d(in_channels, pool_features, 1)
+        self._stem = _Stacked1x1([self.branch1x1, self.branch5x5_1, self.branch3x3dbl_1])
 
     def forward(self, x):
-        b1 = self.branch1x1(x)
-        b5 = _chain(x, (self.branch5x5_1, self.branch5x5_2))
-        b3 = _chain(x, (self.branch3x3dbl_1, self.branch3x3dbl_2, self.branch3x3dbl_3))
+        b1, t5, t3 = self._stem(x)
+        b5 = _chain(t5, (self.branch5x5_2,))
+        b3 = _chain(t3, (self.branch3x3dbl_2, self.branch3x3dbl_3))
         bp = self.branch_pool(Fn.AvgPool3s1Fn.apply(x))
         return _cat([b1, b5, b3, bp])
 
@@ -194,12 +241,12 @@ class InceptionC(nn.Module):
         self.branch7x7dbl_4 = BasicConv2d(c7, c7, (7, 1), padding=(3, 0))
         self.branch7x7dbl_5 = BasicConv2d(c7, 192, (1, 7), padding=(0, 3))
         self.branch_pool = BasicConv2d(in_channels, 192, 1)
+        self._stem = _Stacked1x1([self.branch1x1, self.branch7x7_1, self.branch7x7dbl_1])
 
     def forward(self, x):
-        b1 = self.branch1x1(x)
-        b7 = _chain(x, (self.branch7x7_1, self.branch7x7_2, self.branch7x7_3))
-        bd = _chain(x, (self.branch7x7dbl_1, self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4,
-                        self.branch7x7dbl_5))
+        b1, t7, td = self._stem(x)
+        b7 = _chain(t7, (self.branch7x7_2, self.branch7x7_3))
+        bd = _chain(td, (self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4, self.branch7x7dbl_5))
         bp = self.branch_pool(Fn.AvgPool3s1Fn.apply(x))
         return _cat([b1, b7, bd, bp])
 
@@ -213,10 +260,12 @@ class InceptionD(nn.Module):
         self.branch7x7x3_2 = BasicConv2d(192, 192, (1, 7), padding=(0, 3))
         self.branch7x7x3_3 = BasicConv2d(192, 192, (7, 1), padding=(3, 0))
         self.branch7x7x3_4 = BasicConv2d(192, 192, 3, stride=2)
+        self._stem = _Stacked1x1([self.branch3x3_1, self.branch7x7x3_1])
 
     def forward(self, x):
-        b3 = _chain(x, (self.branch3x3_1, self.branch3x3_2))
-        b7 = _chain(x, (self.branch7x7x3_1, self.branch7x7x3_2, self.branch7x7x3_3, self.branch7x7x3_4))
+        t3, t7 = self._stem(x)
+        b3 = _chain(t3, (self.branch3x3_2,))
+        b7 = _chain(t7, (self.branch7x7x3_2, self.branch7x7x3_3, self.branch7x7x3_4))
         return _cat([b3, b7, Fn.MaxPool3s2Fn.apply(x)])
 
 
@@ -232,12 +281,12 @@ class InceptionE(nn.Module):
         self.branch3x3dbl_3a = BasicConv2d(384, 384, (1, 3), padding=(0, 1))
         self.branch3x3dbl_3b = BasicConv2d(384, 384, (3, 1), padding=(1, 0))
         self.branch_pool = BasicConv2d(in_channels, 192, 1)
+        self._stem = _Stacked1x1([self.branch1x1, self.branch3x3_1, self.branch3x3dbl_1])
 
     def forward(self, x):
-        b1 = self.branch1x1(x)
-        b3 = self.branch3x3_1(x, defer=True)  # both consumers gate
-        b3a, b3b = self.branch3x3_2a(b3, in_relu=True), self.branch3x3_2b(b3, in_relu=True)
-        bd = self.branch3x3dbl_2(self.branch3x3dbl_1(x, defer=True), in_relu=True, defer=True)  # both consumers gate
+        b1, b3, td = self._stem(x)
+        b3a, b3b = self.branch3x3_2a(b3), self.branch3x3_2b(b3)
+        bd = self.branch3x3dbl_2(td, defer=True)  # both consumers gate
         bda, bdb = self.branch3x3dbl_3a(bd, in_relu=True), self.branch3x3dbl_3b(bd, in_relu=True)
         bp = self.branch_pool(Fn.AvgPool3s1Fn.apply(x))
         return _cat([b1, b3a, b3b, bda, bdb, bp])

@@ -743,6 +743,34 @@ class CatChannelsFn(torch.autograd.Function):
         return tuple(outs)
 
 
+class SplitChannelsFn(torch.autograd.Function):
+    """Channel-slice views y[:, o_i : o_i + C_i] of one NHWC activation (the
+    outputs of stacked 1x1 convs); backward assembles the slices' gradients
+    into one buffer in one launch (eegan_cat_channels) instead of autograd's
+    zero-filled slice gradients and adds."""
+
+    @staticmethod
+    def forward(ctx, y, sizes):
+        outs, o = [], 0
+        for c in sizes:
+            outs.append(y[:, o:o + c])
+            o += c
+        ctx.sizes = tuple(sizes)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        parts = []
+        for g, c in zip(gs, ctx.sizes):
+            if g is None:
+                ref = next(x for x in gs if x is not None)
+                N, _, H, W = ref.shape
+                g = empty_nhwc(N, c, H, W, ref.device)
+                g.zero_()
+            parts.append(_as_bf16_grad(g))
+        return CatChannelsFn.apply(*parts), None
+
+
 # ================================================================ linear ===
 def _gemm(tag, A, sai, sak, B, sbk, sbj, C, ldc, M, N, K, bias, act, alpha, beta):
     _launch('gemm_f32', 2.0 * M * N * K, 4.0 * (M * K + K * N + M * N), lambda: ops.gemm_f32(

@@ -269,6 +269,25 @@ def test_fused_activation_backward_matches_separate(gpu, monkeypatch):
         assert rel_l2(gp1[n], gp0[n]) < 2e-2, n
 
 
+def test_inception_stacked_1x1_matches_separate(gpu, monkeypatch):
+    """Inception blocks' shared-input 1x1 branches as one stacked conv
+    (DAMSM._Stacked1x1) vs separate convs: identical forward (same K order per
+    output channel), input gradient equal up to the summation order."""
+    import DAMSM
+    from _util import rel_l2
+    E = DAMSM.CNN_ENCODER(256).to(gpu)
+    x = seeded_tensor('s1:x', (2, 3, 128, 128), 1, 'uniform').to(gpu)
+    res = []
+    for fuse in (False, True):
+        monkeypatch.setattr(DAMSM, 'FUSE_1X1', fuse)
+        xe = x.detach().clone().requires_grad_()
+        feats, code = E(xe)
+        (feats.square().sum() + code.sum()).backward()
+        res.append((feats.cpu(), code.cpu(), xe.grad.cpu()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert rel_l2(res[1][2], res[0][2]) < 2e-2
+
+
 @pytest.mark.parametrize('kind', [64, 128, 256])
 def test_discriminator_and_gradient_penalty(gpu, kind):
     import models
