@@ -72,6 +72,11 @@ struct ConvArgs {
   const bf16_t* gate;
   int ldgate, gate_act;
   float gate_slope;
+  // residual read at half resolution (nearest-2x: pixel (y>>1, x>>1)) and
+  // scaled: out = res_scale * res + gamma * act(acc).  BWDD: a 2x2
+  // average-pool's adjoint fused into the data gradient (resD's shortcut)
+  int res_up2;
+  float res_scale;
 };
 
 // K step kt, 8-channel chunk kc -> kernel tap and channel.  Normal mode: the
@@ -114,7 +119,7 @@ template <int MODE, int FI, int FJ, int WT_CO, int WT_PIX>
 EE_DEV void igemm_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], int pix0, int co0, int wi, int wj,
                            int lane, int split, int Pc, int CH, int CW, int qy, int qx, int stc) {
   const int fr = lane & 15;
-  const float gam = a.res ? *a.gamma : 1.f;
+  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
 #pragma unroll
   for (int j = 0; j < FJ; ++j) {
     const int pc = pix0 + wj * WT_PIX + j * 16 + fr;
@@ -150,10 +155,17 @@ EE_DEV void igemm_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], int 
           if (co + r < a.Mrows) v[r] *= act_dgrad_from_y(bf2f(gp[r]), a.gate_act, a.gate_slope);
       }
       if (a.res) {
-        const bf16_t* rp = a.res + p * a.ldres + co;
+        long rpix = p;
+        if (a.res_up2) {
+          const long hw = (long)a.OH * a.OW;
+          const long n = p / hw, rem = p - n * hw;
+          const int y = (int)(rem / a.OW), x = (int)(rem - (long)y * a.OW);
+          rpix = (n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
+        }
+        const bf16_t* rp = a.res + rpix * a.ldres + co;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (co + r < a.Mrows) v[r] = bf2f(rp[r]) + gam * v[r];
+          if (co + r < a.Mrows) v[r] = a.res_scale * bf2f(rp[r]) + gam * v[r];
       }
       if (a.out_f32) {
         float* op = reinterpret_cast<float*>(a.out) + p * a.ldo + co;
@@ -799,7 +811,7 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
 template <int MODE>  // MODE only tags the kernel name (profiles tell fwd / bwd-data apart)
 __global__ void conv_splitk_reduce_kernel(ConvArgs a) {
   const long total = (long)a.P * a.Mrows;
-  const float gam = a.res ? *a.gamma : 1.f;
+  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const long p = e / a.Mrows;
     const int co = e - p * a.Mrows;
@@ -807,7 +819,16 @@ __global__ void conv_splitk_reduce_kernel(ConvArgs a) {
     for (int z = 0; z < a.nsplit; ++z) v += a.part[(long)z * total + e];
     v = act_fwd(v + (a.bias ? a.bias[co] : 0.f), a.act, a.slope);
     if (a.gate) v *= act_dgrad_from_y(bf2f(a.gate[p * a.ldgate + co]), a.gate_act, a.gate_slope);
-    if (a.res) v = bf2f(a.res[p * a.ldres + co]) + gam * v;
+    if (a.res) {
+      long rpix = p;
+      if (a.res_up2) {
+        const long hw = (long)a.OH * a.OW;
+        const long n = p / hw, rem = p - n * hw;
+        const int y = (int)(rem / a.OW), x = (int)(rem - (long)y * a.OW);
+        rpix = (n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
+      }
+      v = a.res_scale * bf2f(a.res[rpix * a.ldres + co]) + gam * v;
+    }
     if (a.out_f32) reinterpret_cast<float*>(a.out)[p * a.ldo + co] = v;
     else reinterpret_cast<bf16_t*>(a.out)[p * a.ldo + co] = f2bf(v);
   }
@@ -2016,6 +2037,7 @@ void fill_fwd(ConvArgs& a, const eegan_conv_desc* d) {
   a.P = d->N * d->Ho * d->Wo;
   a.ncls = 1;
   a.nsplit = 1;
+  a.res_scale = 1.f;
 }
 
 void fill_bwdd(ConvArgs& a, const eegan_conv_desc* d) {
@@ -2039,6 +2061,7 @@ void fill_bwdd(ConvArgs& a, const eegan_conv_desc* d) {
   a.P = d->N * d->H * d->W;
   a.ncls = d->stride > 1 ? d->stride * d->stride : 1;
   a.nsplit = 1;
+  a.res_scale = 1.f;
 }
 
 int bwdd_pc_max(const eegan_conv_desc* d) {
@@ -2128,6 +2151,14 @@ int eegan_conv_bwd_data(const eegan_conv_desc* d, const bf16_t* dy, const bf16_t
 int eegan_conv_bwd_data_gated(const eegan_conv_desc* d, const bf16_t* dy, const bf16_t* wpackT, void* dx, int lddx,
                               int dx_f32, const bf16_t* gate, int ldgate, int gate_act, float gate_slope, float* ws,
                               hipStream_t stream) {
+  return eegan_conv_bwd_data_ex(d, dy, wpackT, dx, lddx, dx_f32, gate, ldgate, gate_act, gate_slope, nullptr, 0, 0,
+                                1.f, ws, stream);
+}
+
+int eegan_conv_bwd_data_ex(const eegan_conv_desc* d, const bf16_t* dy, const bf16_t* wpackT, void* dx, int lddx,
+                           int dx_f32, const bf16_t* gate, int ldgate, int gate_act, float gate_slope,
+                           const bf16_t* res, int ldres, int res_up2, float res_scale, float* ws,
+                           hipStream_t stream) {
   if (d->up2) {
     ee_set_error("conv_bwd_data: up2 inputs take the hi-res gradient + sum-pool path");
     return -22;
@@ -2144,6 +2175,14 @@ int eegan_conv_bwd_data_gated(const eegan_conv_desc* d, const bf16_t* dy, const 
   a.ldgate = ldgate;
   a.gate_act = gate_act;
   a.gate_slope = gate_slope;
+  a.res = res;
+  a.ldres = ldres;
+  a.res_up2 = res_up2;
+  a.res_scale = res_scale;
+  if (res_up2 && ((d->H & 1) || (d->W & 1))) {
+    ee_set_error("conv_bwd_data: half-resolution residual needs an even input grid");
+    return -22;
+  }
   if (a.P == 0) return 0;
   if (!ld_ok(d->ldy, dy)) {
     ee_set_error("conv_bwd_data: dy channel stride %d must be a multiple of 8", d->ldy);

@@ -54,6 +54,7 @@ _SIGS = {
     'eegan_conv_fwd': ([CD, P, P, P, I, F, P, I, P, P, I, P, P], I),
     'eegan_conv_bwd_data': ([CD, P, P, P, I, I, P, P], I),
     'eegan_conv_bwd_data_gated': ([CD, P, P, P, I, I, P, I, I, F, P, P], I),
+    'eegan_conv_bwd_data_ex': ([CD, P, P, P, I, I, P, I, I, F, P, I, I, F, P, P], I),
     'eegan_conv_wgrad_workspace': ([CD], L),
     'eegan_conv_bwd_weight': ([CD, P, P, P, P, I, P], I),
     'eegan_bn_stats_workspace': ([L, I], L),

@@ -232,12 +232,13 @@ def conv_fwd_raw(x, W, b, g, act=0, slope=0.2, out_f32=False, cache=None, res=No
     return y
 
 
-def conv_bwd_data_raw(dz, W, g, x_shape, cache=None, gate=None, gate_act=0, gate_slope=0.2):
+def conv_bwd_data_raw(dz, W, g, x_shape, cache=None, gate=None, gate_act=0, gate_slope=0.2, res=None, res_up2=0,
+                      res_scale=1.0):
     """dx for the LOGICAL input grid (hi-res when g.up2), NHWC bf16.  `gate`
     (the activated conv input, act code gate_act): dx *= act'(gate) in the
     epilogue -- the producing layer's activation backward, fused."""
-    if gate is not None and g.up2:
-        raise ValueError('conv_bwd_data_raw: gated data gradients of up2 convs are not supported')
+    if (gate is not None or res is not None) and g.up2:
+        raise ValueError('conv_bwd_data_raw: gated / residual data gradients of up2 convs are not supported')
     N, C, H, Wd = x_shape
     Hl, Wl = (H * 2, Wd * 2) if g.up2 else (H, Wd)
     dx = empty_nhwc(N, C, Hl, Wl, dz.device)
@@ -251,7 +252,12 @@ def conv_bwd_data_raw(dz, W, g, x_shape, cache=None, gate=None, gate_act=0, gate
     Ho, Wo = d.Ho, d.Wo
     flops = 2.0 * N * Ho * Wo * g.K * C * g.R * g.S
     nbytes = 2.0 * (N * Hl * Wl * C + N * Ho * Wo * g.K + g.K * C * g.R * g.S)
-    if gate is None:
+    if res is not None:
+        _launch('conv_bwd_data', flops, nbytes, lambda: ops.conv_bwd_data_ex(
+            d, dz.data_ptr(), wp.data_ptr(), dx.data_ptr(), ld_of(dx), 0, ptr(gate),
+            ld_of(gate) if gate is not None else 0, gate_act, gate_slope, res.data_ptr(), ld_of(res), int(res_up2),
+            res_scale, ptr(ws), stream()), key=_shape_key(d) if TIMER is not None else None)
+    elif gate is None:
         _launch('conv_bwd_data', flops, nbytes, lambda: ops.conv_bwd_data(
             d, dz.data_ptr(), wp.data_ptr(), dx.data_ptr(), ld_of(dx), 0, ptr(ws), stream()),
             key=_shape_key(d) if TIMER is not None else None)
@@ -365,6 +371,63 @@ class Conv2dFn(torch.autograd.Function):
             else:
                 db = ChanSumFn.apply(dz)
         return dx, dW, db, None, None, None, None, None, None, None, None
+
+
+class PoolConvFn(torch.autograd.Function):
+    """(avg_pool2d(x, 2), act(conv(x, W) + b)) of one resD input
+    (models.py:267-285: the shortcut pools x, the residual's first conv reads
+    x).  The first-order backward returns ONE dx: the conv's data gradient
+    with the pooled branch's gradient (x 1/4 at (y/2, x/2)) added in its
+    epilogue -- no average-pool adjoint pass, no gradient add.  Under
+    create_graph it is composed of the differentiable Functions instead.
+    defer_act as in Conv2dFn."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, g, act, slope, cache, defer_act=False):
+        x = to_nhwc_bf16(x)
+        N, C, H, Wd = x.shape
+        p = empty_nhwc(N, C, H // 2, Wd // 2, x.device)
+        ops.avgpool2(x.data_ptr(), N, H, Wd, C, ld_of(x), p.data_ptr(), ld_of(p), stream())
+        y = conv_fwd_raw(x, W, b, g, act, slope, False, cache)
+        ctx.g, ctx.act, ctx.slope, ctx.cache, ctx.defer_act = g, act, slope, cache, defer_act
+        ctx.x_shape = tuple(x.shape)
+        ctx.save_for_backward(x, W, y if act else None)
+        return p, y
+
+    @staticmethod
+    def backward(ctx, gp, gy):
+        x, W, y = ctx.saved_tensors
+        g = ctx.g
+        fused = FUSE_ACT_BWD and not torch.is_grad_enabled()
+        dx = dW = db = None
+        dz = None
+        if gy is not None:
+            gy = _as_bf16_grad(gy)
+            dz = ActBwdFn.apply(gy, y, ctx.act, ctx.slope) if ctx.act and not (fused and ctx.defer_act) else gy
+        if _needed(ctx, 0):
+            if fused and gp is not None and dz is not None:
+                dx = conv_bwd_data_raw(dz, W, g, ctx.x_shape, ctx.cache, res=_as_bf16_grad(gp), res_up2=1,
+                                       res_scale=0.25)
+            else:
+                parts = []
+                if dz is not None:
+                    parts.append(ConvBwdDataFn.apply(dz, W, g, ctx.x_shape, ctx.cache))
+                if gp is not None:
+                    parts.append(AvgPool2AdjFn.apply(_as_bf16_grad(gp)))
+                dx = parts[0] if len(parts) == 1 else parts[0] + parts[1]
+        if dz is not None and _needed(ctx, 1):
+            sink = _grad_sink(ctx, 1)
+            if sink is not None and sink.is_contiguous(memory_format=CL):
+                conv_bwd_weight_raw(x, dz, g, W.shape, out=sink)
+            else:
+                dW = ConvBwdWeightFn.apply(x, dz, g)
+        if dz is not None and ctx.needs_input_grad[2] and _needed(ctx, 2):
+            sink = _grad_sink(ctx, 2)
+            if sink is not None:
+                chansum_raw(dz, out=sink)
+            else:
+                db = ChanSumFn.apply(dz)
+        return dx, dW, db, None, None, None, None, None
 
 
 class ConvBwdDataFn(torch.autograd.Function):

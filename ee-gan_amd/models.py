@@ -282,7 +282,15 @@ class resD(nn.Module):
 
     def forward(self, x):
         # residual()'s last LeakyReLU is deferred to ScaleAddFn's backward
-        return Fn.ScaleAddFn.apply(self.shortcut(x), self.residual(x), self.gamma, Fn.ACT_CODES['lrelu'], 0.2)
+        lrelu = Fn.ACT_CODES['lrelu']
+        if self.downsample and Fn.FUSE_ACT_BWD:
+            # the shortcut's pooling and conv_r[0] read x together (Fn.PoolConvFn: one dx)
+            c0 = self.conv_r[0]
+            xp, h = Fn.PoolConvFn.apply(x, c0.weight, c0.bias, c0.geom(False), lrelu, 0.2, c0._cache, True)
+            sc = self.conv_s(xp) if self.learned_shortcut else xp
+            r = self.conv_r[2](h, act='lrelu', slope=0.2, in_act='lrelu', defer_act=True)
+            return Fn.ScaleAddFn.apply(sc, r, self.gamma, lrelu, 0.2)
+        return Fn.ScaleAddFn.apply(self.shortcut(x), self.residual(x), self.gamma, lrelu, 0.2)
 
     def shortcut(self, x):
         if self.downsample:

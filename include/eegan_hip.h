@@ -89,6 +89,13 @@ int eegan_conv_bwd_data(const eegan_conv_desc* d, const uint16_t* dy, const uint
 int eegan_conv_bwd_data_gated(const eegan_conv_desc* d, const uint16_t* dy, const uint16_t* wpackT, void* dx,
                               int lddx, int dx_f32, const uint16_t* gate, int ldgate, int gate_act,
                               float gate_slope, float* ws, hipStream_t stream);
+/* gated (gate may be NULL) plus a residual: dx = res_scale * res + [gated] conv_transpose(dy, W); res_up2
+ * reads res at half resolution (pixel (y/2, x/2)): with res_scale 1/4 the 2x2 average pool's adjoint, so
+ * resD's shortcut (avg_pool2d, models.py:280-285) and first residual conv (267) share one input gradient */
+int eegan_conv_bwd_data_ex(const eegan_conv_desc* d, const uint16_t* dy, const uint16_t* wpackT, void* dx,
+                           int lddx, int dx_f32, const uint16_t* gate, int ldgate, int gate_act, float gate_slope,
+                           const uint16_t* res, int ldres, int res_up2, float res_scale, float* ws,
+                           hipStream_t stream);
 /* dW[Cout][R][S][Cin] (fp32, channels-last like W) = sum_pixels dy x im2col(x); split-K slabs in ws */
 long eegan_conv_wgrad_workspace(const eegan_conv_desc* d);
 int eegan_conv_bwd_weight(const eegan_conv_desc* d, const uint16_t* x, const uint16_t* dy, float* ws, float* dw,
