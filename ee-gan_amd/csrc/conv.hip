@@ -77,6 +77,8 @@ struct ConvArgs {
   // average-pool's adjoint fused into the data gradient (resD's shortcut)
   int res_up2;
   float res_scale;
+  int gate_vec;  // same for the activation gate
+  int res_vec;  // res rows 8-byte aligned (ldres % 4 == 0, aligned base): vector residual loads
 };
 
 // K step kt, 8-channel chunk kc -> kernel tap and channel.  Normal mode: the
@@ -125,11 +127,20 @@ EE_DEV void igemm_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], int 
     const int pc = pix0 + wj * WT_PIX + j * 16 + fr;
     if (pc >= Pc) continue;
     long p = pc;
+    long rpix = pc;  // residual pixel (half resolution when res_up2)
     if (MODE == MODE_BWDD && a.ncls > 1) {
       const int hw = CH * CW;
       const int n = pc / hw, rem = pc - n * hw;
       const int yy = rem / CW, xx = rem - yy * CW;
-      p = ((long)n * a.OH + qy + stc * yy) * a.OW + qx + stc * xx;
+      const int y = qy + stc * yy, x = qx + stc * xx;
+      p = ((long)n * a.OH + y) * a.OW + x;
+      if (a.res_up2) rpix = ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
+    } else if (a.res_up2) {
+      // 32-bit index math, once per pixel (P < 2^31 is checked on the host)
+      const unsigned hw = (unsigned)a.OH * (unsigned)a.OW;
+      const unsigned n = (unsigned)pc / hw, rem = (unsigned)pc - n * hw;
+      const unsigned y = rem / (unsigned)a.OW, x = rem - y * (unsigned)a.OW;
+      rpix = ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
     }
 #pragma unroll
     for (int i = 0; i < FI; ++i) {
@@ -150,22 +161,29 @@ EE_DEV void igemm_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], int 
       }
       if (MODE == MODE_BWDD && a.gate) {
         const bf16_t* gp = a.gate + p * a.ldgate + co;
+        if (a.gate_vec && co + 4 <= a.Mrows) {
+          const uint2 gv = *reinterpret_cast<const uint2*>(gp);
+          const float gg[4] = {lo_f(gv.x), hi_f(gv.x), lo_f(gv.y), hi_f(gv.y)};
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (co + r < a.Mrows) v[r] *= act_dgrad_from_y(bf2f(gp[r]), a.gate_act, a.gate_slope);
+          for (int r = 0; r < 4; ++r) v[r] *= act_dgrad_from_y(gg[r], a.gate_act, a.gate_slope);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (co + r < a.Mrows) v[r] *= act_dgrad_from_y(bf2f(gp[r]), a.gate_act, a.gate_slope);
+        }
       }
       if (a.res) {
-        long rpix = p;
-        if (a.res_up2) {
-          const long hw = (long)a.OH * a.OW;
-          const long n = p / hw, rem = p - n * hw;
-          const int y = (int)(rem / a.OW), x = (int)(rem - (long)y * a.OW);
-          rpix = (n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
-        }
-        const bf16_t* rp = a.res + rpix * a.ldres + co;
+        const bf16_t* rp = a.res + (a.res_up2 ? rpix : p) * a.ldres + co;
+        if (a.res_vec && co + 4 <= a.Mrows) {  // 8-byte aligned rows (host-checked): one load
+          const uint2 rv = *reinterpret_cast<const uint2*>(rp);
+          const float rr[4] = {lo_f(rv.x), hi_f(rv.x), lo_f(rv.y), hi_f(rv.y)};
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (co + r < a.Mrows) v[r] = a.res_scale * bf2f(rp[r]) + gam * v[r];
+          for (int r = 0; r < 4; ++r) v[r] = a.res_scale * rr[r] + gam * v[r];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (co + r < a.Mrows) v[r] = a.res_scale * bf2f(rp[r]) + gam * v[r];
+        }
       }
       if (a.out_f32) {
         float* op = reinterpret_cast<float*>(a.out) + p * a.ldo + co;
@@ -822,10 +840,10 @@ __global__ void conv_splitk_reduce_kernel(ConvArgs a) {
     if (a.res) {
       long rpix = p;
       if (a.res_up2) {
-        const long hw = (long)a.OH * a.OW;
-        const long n = p / hw, rem = p - n * hw;
-        const int y = (int)(rem / a.OW), x = (int)(rem - (long)y * a.OW);
-        rpix = (n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
+        const unsigned hw = (unsigned)a.OH * (unsigned)a.OW;
+        const unsigned n = (unsigned)p / hw, rem = (unsigned)p - n * hw;
+        const unsigned y = rem / (unsigned)a.OW, x = rem - y * (unsigned)a.OW;
+        rpix = ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
       }
       v = a.res_scale * bf2f(a.res[rpix * a.ldres + co]) + gam * v;
     }
@@ -2125,6 +2143,7 @@ int eegan_conv_fwd(const eegan_conv_desc* d, const bf16_t* x, const bf16_t* wpac
   a.bias = bias;
   a.res = res;
   a.ldres = ldres;
+  a.res_vec = res && (ldres % 4) == 0 && ((uintptr_t)res & 7) == 0;
   a.gamma = gamma;
   a.out = y;
   a.ldo = d->ldy;
@@ -2175,8 +2194,10 @@ int eegan_conv_bwd_data_ex(const eegan_conv_desc* d, const bf16_t* dy, const bf1
   a.ldgate = ldgate;
   a.gate_act = gate_act;
   a.gate_slope = gate_slope;
+  a.gate_vec = gate && (ldgate % 4) == 0 && ((uintptr_t)gate & 7) == 0;
   a.res = res;
   a.ldres = ldres;
+  a.res_vec = res && (ldres % 4) == 0 && ((uintptr_t)res & 7) == 0;
   a.res_up2 = res_up2;
   a.res_scale = res_scale;
   if (res_up2 && ((d->H & 1) || (d->W & 1))) {
