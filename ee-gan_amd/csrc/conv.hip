@@ -1434,19 +1434,16 @@ __global__ void pack_weights_kernel(const float* w, const float* scale, int Cout
 // model (fwd and bwd-data images).  `table` (device, int64): njobs rows of
 // {w, scale, out, Cout, Cin, R, S, transposed}, then njobs+1 prefix offsets of
 // BLOCKS per job (pack_multi_blocks).  Forward image: one block per output row
-// (w[co] is already the row's (tap, c) order: a padded, coalesced copy);
-// bwd-data image: one block per 32 input channels x a chunk of output channels,
-// transposed through LDS so both the fp32 reads (8-channel runs) and the bf16
-// row writes are contiguous.
-constexpr int PK_LDS = 9344;   // floats of staging
+// (w[co] is already the row's (tap, c) order: a padded copy, 8 columns = one
+// 16-byte store per thread); bwd-data image: per tap, a 64x64 (ci, co) tile
+// transposed through LDS, so the fp32 reads are 256-byte runs along ci and the
+// bf16 writes 128-byte runs along co.
+constexpr int PK_T = 64;  // bwd-image tile: input channels (rows) x output channels (columns)
 
 EE_HOST_DEV_INLINE int pk_cgp(int C) { return C <= 8 ? 8 : (C + BK - 1) / BK * BK; }
-constexpr int PK_TI = 32;      // input channels per bwd-image block (128-B fp32 runs)
-// output channels per bwd-image block: PK_TI input channels x RS taps x CO fit the staging
-EE_HOST_DEV_INLINE int pk_bwd_co(int RS) { return min(128, PK_LDS / (PK_TI * RS + 1)); }
 
 __global__ __launch_bounds__(256) void pack_weights_multi_kernel(const long* __restrict__ table, int njobs) {
-  __shared__ float buf[PK_LDS];
+  __shared__ float buf[PK_T * (PK_T + 1)];
   const long* pre = table + 8L * njobs;
   int lo = 0, hi = njobs - 1;
   while (lo < hi) {
@@ -1464,64 +1461,47 @@ __global__ __launch_bounds__(256) void pack_weights_multi_kernel(const long* __r
   if (!tr) {
     // ---- forward image: row co = lb, out[co][tap*Cgp + c] = w[co][tap][c]
     const int Cgp = pk_cgp(Cin), Kw = (RS * Cgp + BK - 1) / BK * BK;
-    bf16_t* orow = out + (long)lb * Kw;
-    if (lb >= Cout) {
-      for (int k = t; k < Kw; k += 256) orow[k] = 0;
-      return;
-    }
-    const float sc = scale ? scale[lb] : 1.f;
+    bf16_t* orow = out + (long)lb * Kw;  // Kw % 32 == 0: 16-byte aligned 8-column groups
+    const bool live = lb < Cout;
+    const float sc = (live && scale) ? scale[lb] : 1.f;
     const float* src = w + (long)lb * RS * Cin;
-    for (int k = t; k < Kw; k += 256) {
-      const int tap = k / Cgp, c = k - tap * Cgp;
-      orow[k] = f2bf(tap < RS && c < Cin ? src[tap * Cin + c] * sc : 0.f);
+    for (int k = t * 8; k < Kw; k += 256 * 8) {
+      const int tap = k / Cgp, c = k - tap * Cgp;  // Cgp % 8 == 0: the group stays in one tap
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = (live && tap < RS && c + u < Cin) ? src[tap * Cin + c + u] * sc : 0.f;
+      *reinterpret_cast<uint4*>(orow + k) =
+          make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
     }
   } else {
-    // ---- bwd-data image: rows ci0..ci0+TI-1 x one chunk of CO output channels,
-    // out[ci][tap*Cgp + co] = w[co][tap][ci]
-    constexpr int TI = PK_TI;
+    // ---- bwd-data image: out[ci][tap*Cgp + co] = w[co][tap][ci] * scale[co];
+    // block lb -> (ci tile, tap, co tile)
     const int Cgp = pk_cgp(Cout), Kw = (RS * Cgp + BK - 1) / BK * BK;
-    const int RW = TI * RS + 1;  // odd LDS row stride
-    const int CO = pk_bwd_co(RS);
-    const int nchunk = (Cgp + CO - 1) / CO;
-    const int ci0 = (lb / nchunk) * TI, co0 = (lb % nchunk) * CO;
-    const int ni = max(0, min(TI, Cin - ci0));
-    {
-      const int nco = min(CO, Cout - co0);  // may be <= 0 in the channel padding
-      const int nload = max(nco, 0) * RS * ni;
-      for (int e0 = t; e0 < nload; e0 += 256 * 8) {
-        float v[8];
+    const int nco = (Cgp + PK_T - 1) / PK_T;
+    const int cot = lb % nco, tap = (lb / nco) % RS, cit = lb / (nco * RS);
+    const int ci0 = cit * PK_T, co0 = cot * PK_T;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int e = e0 + u * 256;
-          v[u] = 0.f;
-          if (e < nload) {
-            const int co = e / (RS * ni), q = e - co * (RS * ni);
-            const int tap = q / ni, i = q - tap * ni;
-            v[u] = w[((long)(co0 + co) * RS + tap) * Cin + ci0 + i] * (scale ? scale[co0 + co] : 1.f);
-          }
-        }
+    for (int r = 0; r < PK_T * PK_T / 256; ++r) {
+      const int e = r * 256 + t, co = e / PK_T, i = e % PK_T;  // lanes run along ci
+      float v = 0.f;
+      if (co0 + co < Cout && ci0 + i < Cin)
+        v = w[((long)(co0 + co) * RS + tap) * Cin + ci0 + i] * (scale ? scale[co0 + co] : 1.f);
+      buf[co * (PK_T + 1) + i] = v;
+    }
+    __syncthreads();
+    const int ncol = min(PK_T, Cgp - co0);  // never past this tap's Cgp columns
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int e = e0 + u * 256;
-          if (e < nload) {
-            const int co = e / (RS * ni), q = e - co * (RS * ni);
-            const int tap = q / ni, i = q - tap * ni;
-            buf[co * RW + i * RS + tap] = v[u];
-          }
-        }
-      }
-      __syncthreads();
-      const int ncol = min(CO, Cgp - co0);
-      for (int e = t; e < TI * RS * ncol; e += 256) {
-        const int row = e / (RS * ncol), rem = e - row * (RS * ncol);
-        const int tap = rem / ncol, co = rem - tap * ncol;
-        const float v = (row < ni && co < nco) ? buf[co * RW + row * RS + tap] : 0.f;
-        out[(long)(ci0 + row) * Kw + tap * Cgp + co0 + co] = f2bf(v);
+    for (int r = 0; r < PK_T * PK_T / 2 / 256; ++r) {
+      const int e = r * 256 + t, row = e / (PK_T / 2), cp = 2 * (e % (PK_T / 2));  // lanes run along co
+      if (cp < ncol) {
+        bf16_t* op = out + (long)(ci0 + row) * Kw + tap * Cgp + co0 + cp;
+        *reinterpret_cast<uint32_t*>(op) = pack2(buf[cp * (PK_T + 1) + row], buf[(cp + 1) * (PK_T + 1) + row]);
       }
     }
-    if (co0 + CO < Cgp) return;  // the last channel chunk also zeroes the row tail
-    for (int e = t; e < TI * (Kw - RS * Cgp); e += 256) {
-      const int row = e / (Kw - RS * Cgp), k = RS * Cgp + e - row * (Kw - RS * Cgp);
+    if (tap != RS - 1 || cot != nco - 1) return;  // one block per row tile zeroes the K tail
+    const int tail = Kw - RS * Cgp;
+    for (int e = t; e < PK_T * tail; e += 256) {
+      const int row = e / tail, k = RS * Cgp + e - row * tail;
       out[(long)(ci0 + row) * Kw + k] = 0;
     }
   }
@@ -2112,7 +2092,7 @@ int eegan_conv_pack_weights(const float* w, const float* scale, int Cout, int Ci
 
 long eegan_conv_pack_multi_blocks(int Cout, int Cin, int R, int S, int transposed) {
   if (!transposed) return ee_round_up(Cout, 128);
-  return (long)(ee_round_up(Cin, 128) / PK_TI) * ee_cdiv(pk_cgp(Cout), pk_bwd_co(R * S));
+  return (long)(ee_round_up(Cin, 128) / PK_T) * R * S * ee_cdiv(pk_cgp(Cout), PK_T);
 }
 
 int eegan_conv_pack_weights_multi(const long* table, int njobs, long total_blocks, hipStream_t stream) {
