@@ -181,30 +181,48 @@ EE_DEV void store8(bf16_t* dst, const float (&o)[8], int nvalid) {
   }
 }
 
-// grid (chunks, N): output pixels [chunk*ppc, ...) of sample n
+// grid (chunks, N): output pixels [chunk*ppc, ...) of sample n.  FUNR pixels
+// per thread per iteration: their loads are all issued before any arithmetic
+// (a single 16-byte load per iteration left these kernels latency-bound).
+constexpr int FUNR = 4;
+
 __global__ __launch_bounds__(NT) void bnmod_fwd_kernel(ModArgs a, bf16_t* __restrict__ y, int ldy, int ppc) {
   const int C8 = (a.C + 7) / 8, rows = NT / C8;
   const int row = threadIdx.x / C8, cg = threadIdx.x - row * C8;
   if (row >= rows) return;
   const int n = blockIdx.y, c0 = cg * 8, nv = a.C - c0;
   const int Ho = a.H << a.up2, Wo = a.W << a.up2;
-  const long HWo = (long)Ho * Wo;
-  const long q1 = min(HWo, (long)(blockIdx.x + 1) * ppc);
+  const int HWo = Ho * Wo;  // per-sample pixel counts fit 32 bits
+  const int q1 = min(HWo, ((int)blockIdx.x + 1) * ppc);
   ChanParams P;
   load_params(a, n, c0, P);
-  for (long q = (long)blockIdx.x * ppc + row; q < q1; q += rows) {
-    const int oy = q / Wo, ox = q - (long)oy * Wo;
-    const long ip = ((long)n * a.H + (oy >> a.up2)) * a.W + (ox >> a.up2);
-    const float m = a.mode == 1 ? a.mask[(long)n * HWo + q] : 0.f;
-    float xv[8], o[8];
-    unpack8(*reinterpret_cast<const uint4*>(a.x + ip * a.ldx + c0), xv);
+  for (int qb = (int)blockIdx.x * ppc + row; qb < q1; qb += FUNR * rows) {
+    uint4 xr[FUNR];
+    float mr[FUNR];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float mul, add;
-      coeffs(a, P, j, m, mul, add);
-      o[j] = act_fwd((xv[j] - P.mean[j]) * P.istd[j] * mul + add, a.act, a.slope);
+    for (int u = 0; u < FUNR; ++u) {
+      const int q = qb + u * rows;
+      if (q < q1) {
+        const int oy = (unsigned)q / (unsigned)Wo, ox = q - oy * Wo;
+        const long ip = ((long)n * a.H + (oy >> a.up2)) * a.W + (ox >> a.up2);
+        xr[u] = *reinterpret_cast<const uint4*>(a.x + ip * a.ldx + c0);
+        mr[u] = a.mode == 1 ? a.mask[(long)n * HWo + q] : 0.f;
+      }
     }
-    store8(y + ((long)n * HWo + q) * ldy + c0, o, nv);
+#pragma unroll
+    for (int u = 0; u < FUNR; ++u) {
+      const int q = qb + u * rows;
+      if (q >= q1) break;
+      float xv[8], o[8];
+      unpack8(xr[u], xv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float mul, add;
+        coeffs(a, P, j, mr[u], mul, add);
+        o[j] = act_fwd((xv[j] - P.mean[j]) * P.istd[j] * mul + add, a.act, a.slope);
+      }
+      store8(y + ((long)n * HWo + q) * ldy + c0, o, nv);
+    }
   }
 }
 
@@ -224,9 +242,9 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_reduce_kernel(ModArgs a, const b
   const int row = t / C8, cg = t - row * C8;
   const int n = blockIdx.y;
   const int Ho = a.H << a.up2, Wo = a.W << a.up2;
-  const long HWo = (long)Ho * Wo;
-  const long q0 = (long)blockIdx.x * pix_per_chunk;
-  const long q1 = min(HWo, q0 + pix_per_chunk);
+  const int HWo = Ho * Wo;  // per-sample pixel counts fit 32 bits
+  const int q0 = (int)blockIdx.x * pix_per_chunk;
+  const int q1 = min(HWo, q0 + pix_per_chunk);
   float acc[4][8];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -236,56 +254,95 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_reduce_kernel(ModArgs a, const b
   float* red = sh;                 // [rows][C8] for dmask
   ChanParams P;
   if (row < rows) load_params(a, n, c0, P);
+  // a pixel's C8 channel groups are C8 consecutive lanes of one wave when C8 is a
+  // power of two <= 64: its dmask is then a shuffle reduction (no LDS, no barriers)
+  const bool wave_red = (C8 & (C8 - 1)) == 0 && C8 <= 64;
   // base of the pixel loop must be block-uniform for the dmask reduction
-  for (long qb = q0; qb < q1; qb += rows) {
-    const long q = qb + row;
-    float dm = 0.f;
-    if (row < rows && q < q1) {
-      const int oy = q / Wo, ox = q - (long)oy * Wo;
-      const long ip = ((long)n * a.H + (oy >> a.up2)) * a.W + (ox >> a.up2);
-      const long op = (long)n * HWo + q;
-      const float m = a.mode == 1 ? a.mask[op] : 0.f;
-      float xv[8], gv[8];
-      unpack8(*reinterpret_cast<const uint4*>(a.x + ip * a.ldx + c0), xv);
-      unpack8(*reinterpret_cast<const uint4*>(dt + op * lddt + c0), gv);
+  for (int qb = q0; qb < q1; qb += 2 * rows) {
+    uint4 xr[2], gr[2];
+    float mr[2];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const bool ok = c0 + j < C;  // channel padding may hold anything
-        const float xh = ok ? (xv[j] - P.mean[j]) * P.istd[j] : 0.f;
-        float mul, add;
-        coeffs(a, P, j, m, mul, add);
-        const float tv = xh * mul + add;
-        float g = ok ? gv[j] : 0.f;
-        if (a.act == ACT_RELU) g = tv > 0.f ? g : 0.f;
-        else if (a.act == ACT_LRELU) g = tv > 0.f ? g : g * a.slope;
-        const float dxh = g * mul;
-        if (a.mode == 1) {
-          acc[0][j] += g * m * xh;
-          acc[1][j] += g * m;
-          dm += g * (P.pm[j] * xh + P.pa[j]);
-        } else {
-          acc[0][j] += g * xh;
-          acc[1][j] += g;
-        }
-        acc[2][j] += dxh;
-        acc[3][j] += dxh * xh;
+    for (int u = 0; u < 2; ++u) {
+      const int q = qb + u * rows + row;
+      if (row < rows && q < q1) {
+        const int oy = (unsigned)q / (unsigned)Wo, ox = q - oy * Wo;
+        const long ip = ((long)n * a.H + (oy >> a.up2)) * a.W + (ox >> a.up2);
+        const long op = (long)n * HWo + q;
+        xr[u] = *reinterpret_cast<const uint4*>(a.x + ip * a.ldx + c0);
+        gr[u] = *reinterpret_cast<const uint4*>(dt + op * lddt + c0);
+        mr[u] = a.mode == 1 ? a.mask[op] : 0.f;
       }
     }
-    if (a.mode == 1 && dmask) {
-      if (row < rows) red[row * C8 + cg] = dm;
-      __syncthreads();
-      if (t < rows && qb + t < q1) {
-        float s = 0.f;
-        for (int i = 0; i < C8; ++i) s += red[t * C8 + i];
-        dmask[(long)n * HWo + qb + t] = s;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = qb + u * rows + row;
+      float dm = 0.f;
+      if (row < rows && q < q1) {
+        const float m = mr[u];
+        float xv[8], gv[8];
+        unpack8(xr[u], xv);
+        unpack8(gr[u], gv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const bool ok = c0 + j < C;  // channel padding may hold anything
+          const float xh = ok ? (xv[j] - P.mean[j]) * P.istd[j] : 0.f;
+          float mul, add;
+          coeffs(a, P, j, m, mul, add);
+          const float tv = xh * mul + add;
+          float g = ok ? gv[j] : 0.f;
+          if (a.act == ACT_RELU) g = tv > 0.f ? g : 0.f;
+          else if (a.act == ACT_LRELU) g = tv > 0.f ? g : g * a.slope;
+          const float dxh = g * mul;
+          if (a.mode == 1) {
+            acc[0][j] += g * m * xh;
+            acc[1][j] += g * m;
+            dm += g * (P.pm[j] * xh + P.pa[j]);
+          } else {
+            acc[0][j] += g * xh;
+            acc[1][j] += g;
+          }
+          acc[2][j] += dxh;
+          acc[3][j] += dxh * xh;
+        }
       }
-      __syncthreads();
+      if (a.mode == 1 && dmask) {
+        if (wave_red) {
+          for (int off = 1; off < C8; off <<= 1) dm += __shfl_xor(dm, off);
+          if (cg == 0 && row < rows && q < q1) dmask[(long)n * HWo + q] = dm;
+        } else {
+          if (row < rows) red[row * C8 + cg] = dm;
+          __syncthreads();
+          const int qt = qb + u * rows + t;
+          if (t < rows && qt < q1) {
+            float s = 0.f;
+            for (int i = 0; i < C8; ++i) s += red[t * C8 + i];
+            dmask[(long)n * HWo + qt] = s;
+          }
+          __syncthreads();
+        }
+      }
     }
   }
   // reduce acc over rows -> ws
   float* sacc = sh + rows * C8;  // [rows][4][C8*8]
   const int W8 = C8 * 8;
-  if (row < rows) {
+  int nrows = rows;
+  if (wave_red) {
+    // the rows of one wave first, by shuffles (lanes l, l^C8, l^2C8, ... share
+    // channels); then one partial row per wave goes through LDS
+    for (int off = C8; off < 64; off <<= 1)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] += __shfl_xor(acc[i][j], off);
+    nrows = NT / 64;
+    if ((t & 63) < C8) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sacc[((t >> 6) * 4 + i) * W8 + c0 + j] = acc[i][j];
+    }
+  } else if (row < rows) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -296,7 +353,7 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_reduce_kernel(ModArgs a, const b
   for (int e = t; e < 4 * C; e += NT) {
     const int i = e / C, c = e - i * C;
     float s = 0.f;
-    for (int r = 0; r < rows; ++r) s += sacc[(r * 4 + i) * W8 + c];
+    for (int r = 0; r < nrows; ++r) s += sacc[(r * 4 + i) * W8 + c];
     out[e] = s;
   }
 }
@@ -337,8 +394,8 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_
   if (row >= rows) return;
   const int n = blockIdx.y, c0 = cg * 8, nv = a.C - c0;
   const int Ho = a.H << a.up2, Wo = a.W << a.up2;
-  const long HW = (long)a.H * a.W;
-  const long q1 = min(HW, (long)(blockIdx.x + 1) * ppc);
+  const int HW = a.H * a.W;
+  const int q1 = min(HW, ((int)blockIdx.x + 1) * ppc);
   const int nch = a.up2 ? 4 : 1;
   ChanParams P;
   load_params(a, n, c0, P);
@@ -350,34 +407,56 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_
     m1[j] = (float)(chan[c] / count);
     m2[j] = (float)(chan[a.C + c] / count);
   }
-  for (long q = (long)blockIdx.x * ppc + row; q < q1; q += rows) {
-    const int iy = q / a.W, ix = q - (long)iy * a.W;
-    const long ip = (long)n * HW + q;
-    float xh[8], o[8];
-    unpack8(*reinterpret_cast<const uint4*>(a.x + ip * a.ldx + c0), xh);
+  for (int qb = (int)blockIdx.x * ppc + row; qb < q1; qb += 2 * rows) {
+    // two input pixels x (1 or 4) output children per iteration, loads first
+    uint4 xr[2], gr[2][4];
+    float mr[2][4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      xh[j] = (xh[j] - P.mean[j]) * P.istd[j];
-      o[j] = 0.f;
-    }
-    for (int ch = 0; ch < nch; ++ch) {
-      const int oy = (iy << a.up2) + (ch >> 1), ox = (ix << a.up2) + (ch & 1);
-      const long op = ((long)n * Ho + oy) * Wo + ox;
-      const float m = a.mode == 1 ? a.mask[op] : 0.f;
-      float gv[8];
-      unpack8(*reinterpret_cast<const uint4*>(dt + op * lddt + c0), gv);
+    for (int u = 0; u < 2; ++u) {
+      const int q = qb + u * rows;
+      if (q < q1) {
+        const int iy = (unsigned)q / (unsigned)a.W, ix = q - iy * a.W;
+        xr[u] = *reinterpret_cast<const uint4*>(a.x + ((long)n * HW + q) * a.ldx + c0);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float mul, add;
-        coeffs(a, P, j, m, mul, add);
-        const float tv = xh[j] * mul + add;
-        float g = gv[j];
-        if (a.act == ACT_RELU) g = tv > 0.f ? g : 0.f;
-        else if (a.act == ACT_LRELU) g = tv > 0.f ? g : g * a.slope;
-        o[j] += P.istd[j] * (g * mul - m1[j] - vg[j] * xh[j] * m2[j]);
+        for (int ch = 0; ch < 4; ++ch) {
+          if (ch < nch) {
+            const int oy = (iy << a.up2) + (ch >> 1), ox = (ix << a.up2) + (ch & 1);
+            const long op = ((long)n * Ho + oy) * Wo + ox;
+            gr[u][ch] = *reinterpret_cast<const uint4*>(dt + op * lddt + c0);
+            mr[u][ch] = a.mode == 1 ? a.mask[op] : 0.f;
+          }
+        }
       }
     }
-    store8(dx + ip * lddx + c0, o, nv);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = qb + u * rows;
+      if (q >= q1) break;
+      float xh[8], o[8];
+      unpack8(xr[u], xh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xh[j] = (xh[j] - P.mean[j]) * P.istd[j];
+        o[j] = 0.f;
+      }
+#pragma unroll
+      for (int ch = 0; ch < 4; ++ch) {
+        if (ch >= nch) break;
+        float gv[8];
+        unpack8(gr[u][ch], gv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float mul, add;
+          coeffs(a, P, j, mr[u][ch], mul, add);
+          const float tv = xh[j] * mul + add;
+          float g = gv[j];
+          if (a.act == ACT_RELU) g = tv > 0.f ? g : 0.f;
+          else if (a.act == ACT_LRELU) g = tv > 0.f ? g : g * a.slope;
+          o[j] += P.istd[j] * (g * mul - m1[j] - vg[j] * xh[j] * m2[j]);
+        }
+      }
+      store8(dx + ((long)n * HW + q) * lddx + c0, o, nv);
+    }
   }
 }
 

@@ -234,14 +234,19 @@ def test_conv_double_backward(gpu):
         assert rel_l2(m.weight.grad.cpu(), wr.grad) < 3e-2
 
 
-@pytest.mark.parametrize('mode,up2,act', [(0, False, 'relu'), (0, False, 'lrelu'), (1, True, 'relu'),
-                                          (1, False, None), (0, True, None)])
-def test_bn_modulation(gpu, mode, up2, act):
+@pytest.mark.parametrize('mode,up2,act,C,HW', [(0, False, 'relu', 24, 6), (0, False, 'lrelu', 24, 6),
+                                               (1, True, 'relu', 24, 6), (1, False, None, 24, 6),
+                                               (0, True, None, 24, 6),
+                                               # power-of-two channel groups: wave-shuffle dmask path,
+                                               # odd grids for the unrolled pixel loops' tails
+                                               (1, True, 'relu', 64, 13), (1, False, 'relu', 32, 29),
+                                               (0, False, 'lrelu', 256, 11)])
+def test_bn_modulation(gpu, mode, up2, act, C, HW):
     """SyncBN (batch stats) + affine / affine_ssa modulation + act (+ fused nearest-up)."""
     Fn, T, _ = _mods()
     from eegan_hip.nn import SyncBatchNorm2d
     torch.manual_seed(5)
-    N, C, H, W = 3, 24, 6, 6
+    N, H, W = 3, HW, HW
     bn = SyncBatchNorm2d(C, affine=(mode == 0))
     if mode == 0:
         bn.weight.data.normal_(1, 0.2)
