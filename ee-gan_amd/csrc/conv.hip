@@ -78,6 +78,7 @@ struct ConvArgs {
   int res_up2;
   float res_scale;
   int gate_vec;  // same for the activation gate
+  int red_vec4;  // split-K reduce: 4-channel vector path (host-checked alignment)
   int res_vec;  // res rows 8-byte aligned (ldres % 4 == 0, aligned base): vector residual loads
 };
 
@@ -830,6 +831,56 @@ template <int MODE>  // MODE only tags the kernel name (profiles tell fwd / bwd-
 __global__ void conv_splitk_reduce_kernel(ConvArgs a) {
   const long total = (long)a.P * a.Mrows;
   const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
+  if (a.red_vec4) {
+    // 4 consecutive channels of one pixel per thread: 16-byte slab loads (4
+    // splits in flight), 8-byte residual / gate loads and stores; 32-bit
+    // index math (the host enables this path only for total < 2^31)
+    const unsigned total4 = (unsigned)(total >> 2), M = (unsigned)a.Mrows;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
+      const unsigned e = i * 4, p = e / M, co = e - p * M;
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+      const f32x4_t* src = reinterpret_cast<const f32x4_t*>(a.part) + i;
+      int z = 0;
+      for (; z + 4 <= a.nsplit; z += 4) {
+        const f32x4_t v0 = src[(long)z * total4], v1 = src[(long)(z + 1) * total4];
+        const f32x4_t v2 = src[(long)(z + 2) * total4], v3 = src[(long)(z + 3) * total4];
+        acc += v0;  // same order as the scalar path: bit-identical sums
+        acc += v1;
+        acc += v2;
+        acc += v3;
+      }
+      for (; z < a.nsplit; ++z) acc += src[(long)z * total4];
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = act_fwd(acc[r] + (a.bias ? a.bias[co + r] : 0.f), a.act, a.slope);
+      if (a.gate) {
+        const uint2 gv = *reinterpret_cast<const uint2*>(a.gate + (long)p * a.ldgate + co);
+        const float gg[4] = {lo_f(gv.x), hi_f(gv.x), lo_f(gv.y), hi_f(gv.y)};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= act_dgrad_from_y(gg[r], a.gate_act, a.gate_slope);
+      }
+      if (a.res) {
+        long rpix = p;
+        if (a.res_up2) {
+          const unsigned hw = (unsigned)a.OH * (unsigned)a.OW;
+          const unsigned n = p / hw, rem = p - n * hw;
+          const unsigned y = rem / (unsigned)a.OW, x = rem - y * (unsigned)a.OW;
+          rpix = ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
+        }
+        const uint2 rv = *reinterpret_cast<const uint2*>(a.res + rpix * a.ldres + co);
+        const float rr[4] = {lo_f(rv.x), hi_f(rv.x), lo_f(rv.y), hi_f(rv.y)};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = a.res_scale * rr[r] + gam * v[r];
+      }
+      if (a.out_f32) {
+        *reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(a.out) + (long)p * a.ldo + co) = {v[0], v[1], v[2], v[3]};
+      } else {
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(a.out) + (long)p * a.ldo + co) =
+            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+    }
+    return;
+  }
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const long p = e / a.Mrows;
     const int co = e - p * a.Mrows;
@@ -2005,7 +2056,11 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd" : "conv_bwd_data");
   if (rc || a.nsplit == 1) return rc;
   const long total = (long)a.P * a.Mrows;
-  ee_launch(conv_splitk_reduce_kernel<MODE>, dim3((int)std::min<long>((total + 255) / 256, 4096)), dim3(256), 0, s, a);
+  const uintptr_t oal = a.out_f32 ? 15 : 7;
+  a.red_vec4 = a.Mrows % 4 == 0 && total < 0x7fffffffL && a.ldo % 4 == 0 && ((uintptr_t)a.out & oal) == 0 &&
+               ((uintptr_t)a.part & 15) == 0 && (!a.gate || a.gate_vec) && (!a.res || a.res_vec);
+  const long work = a.red_vec4 ? total / 4 : total;
+  ee_launch(conv_splitk_reduce_kernel<MODE>, dim3((int)std::min<long>((work + 255) / 256, 4096)), dim3(256), 0, s, a);
   return ee_check_launch("conv_splitk_reduce");
 }
 
