@@ -2057,8 +2057,10 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   if (rc || a.nsplit == 1) return rc;
   const long total = (long)a.P * a.Mrows;
   const uintptr_t oal = a.out_f32 ? 15 : 7;
+  // EEGAN_CONV_RED_VEC4=0 forces the scalar reduce (A/B and bit-identity tests)
   a.red_vec4 = a.Mrows % 4 == 0 && total < 0x7fffffffL && a.ldo % 4 == 0 && ((uintptr_t)a.out & oal) == 0 &&
-               ((uintptr_t)a.part & 15) == 0 && (!a.gate || a.gate_vec) && (!a.res || a.res_vec);
+               ((uintptr_t)a.part & 15) == 0 && (!a.gate || a.gate_vec) && (!a.res || a.res_vec) &&
+               env_int("EEGAN_CONV_RED_VEC4", 1);
   const long work = a.red_vec4 ? total / 4 : total;
   ee_launch(conv_splitk_reduce_kernel<MODE>, dim3((int)std::min<long>((work + 255) / 256, 4096)), dim3(256), 0, s, a);
   return ee_check_launch("conv_splitk_reduce");

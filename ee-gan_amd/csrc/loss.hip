@@ -1,5 +1,5 @@
-// Loss-side kernels: DAMSM words/sent losses (fused over all B^2 pairs),
-// cross-entropy over the similarity matrices, hinge/mean reductions of the
+// Loss-side kernels: DAMSM sentence similarity (the word-level similarity is
+// in damsm.hip), cross-entropy over the similarity matrices, hinge/mean reductions of the
 // discriminator outputs, BCE-with-logits, the MA gradient penalty, class
 // one-hot labels and the ATTR_Enhance 4x4 self-attention core.
 //
@@ -12,214 +12,7 @@
 
 namespace {
 
-constexpr float GAMMA1 = 5.f, GAMMA2 = 5.f, GAMMA3 = 10.f;
-constexpr int NR = 289;   // 17 x 17 regions
-constexpr int ND = 256;   // embedding dim
-constexpr int TMAX = 20;  // max words per caption (cfg.TEXT.WORDS_NUM)
-
-// ----------------------------------------------------------- words loss --
-// One workgroup per (text i, image j) pair.  Regions are fp32 NHWC
-// [B][NR][ND]; words fp32 [B][ND][T] (the RNN_ENCODER layout), T <= 20
-// (cfg.TEXT.WORDS_NUM, miscc/config.py:66).
-struct WordsArgs {
-  const float* reg;     // [B][NR][ND]
-  const float* words;   // [B][ND][T]
-  const long* lens;     // [B]
-  int B, T;
-  float* sim;           // fwd: [B(img j)][B(txt i)] * gamma3 (unmasked)
-  const float* dsim;    // bwd: d loss / d sim  [j][i]
-  float* dreg;          // bwd: [B][NR][ND] (atomic accumulate)
-  float* dwords;        // bwd: [B][ND][T]  (atomic accumulate) or null
-  float* att;           // fwd: attention maps of the diagonal pairs [B][T][NR] or null
-};
-
-struct WordsSmem {
-  float q[ND][TMAX];
-  float a1[NR][TMAX];        // S -> softmax over words -> (bwd) dS
-  float a2[TMAX][NR + 3];    // softmax over regions
-  float da[TMAX][NR + 3];    // (bwd) dA2 -> dA1^T
-  float dc[ND][TMAX];        // (bwd) dC
-  float red[4][TMAX][3];
-  float cs[TMAX], nq[TMAX], nc[TMAX];
-};
-
-template <bool BWD>
-__global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  WordsSmem& sm = *reinterpret_cast<WordsSmem*>(smem_raw);
-  const int i = blockIdx.x, j = blockIdx.y;  // text i, image j
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int w = (int)a.lens[i];
-  const float* ctx = a.reg + (long)j * NR * ND;
-
-  // 1. words of caption i
-  for (int e = t; e < ND * TMAX; e += 256) {
-    const int d = e / TMAX, k = e % TMAX;
-    sm.q[d][k] = k < w ? a.words[((long)i * ND + d) * a.T + k] : 0.f;
-  }
-  __syncthreads();
-  // 2. S[r][k] = ctx_r . q_k ; softmax over words (DAMSM_losses.py:42-45)
-  for (int r = t; r < NR; r += 256) {
-    float s[TMAX];
-#pragma unroll
-    for (int k = 0; k < TMAX; ++k) s[k] = 0.f;
-    const float* row = ctx + (long)r * ND;
-    for (int d = 0; d < ND; d += 4) {
-      const float4 c4 = *reinterpret_cast<const float4*>(row + d);
-#pragma unroll
-      for (int k = 0; k < TMAX; ++k)
-        s[k] += c4.x * sm.q[d][k] + c4.y * sm.q[d + 1][k] + c4.z * sm.q[d + 2][k] + c4.w * sm.q[d + 3][k];
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < TMAX; ++k)
-      if (k < w) mx = fmaxf(mx, s[k]);
-    float sum = 0.f;
-#pragma unroll
-    for (int k = 0; k < TMAX; ++k) {
-      s[k] = k < w ? __expf(s[k] - mx) : 0.f;
-      sum += s[k];
-    }
-    const float inv = 1.f / sum;
-#pragma unroll
-    for (int k = 0; k < TMAX; ++k) sm.a1[r][k] = s[k] * inv;
-  }
-  __syncthreads();
-  // 3. A2[k][:] = softmax_r(gamma1 * A1[:, k]) (DAMSM_losses.py:53-54); one wave per word
-  for (int k = wv; k < w; k += 4) {
-    float mx = -INFINITY;
-    for (int r = lane; r < NR; r += 64) mx = fmaxf(mx, GAMMA1 * sm.a1[r][k]);
-    mx = wave_max(mx);
-    float sum = 0.f;
-    for (int r = lane; r < NR; r += 64) {
-      const float e = __expf(GAMMA1 * sm.a1[r][k] - mx);
-      sm.a2[k][r] = e;
-      sum += e;
-    }
-    sum = wave_sum(sum);
-    const float inv = 1.f / sum;
-    for (int r = lane; r < NR; r += 64) sm.a2[k][r] *= inv;
-  }
-  for (int e = w * (NR + 3) + t; e < TMAX * (NR + 3); e += 256) (&sm.a2[0][0])[e] = 0.f;  // unused words
-  __syncthreads();
-  if (!BWD && a.att && i == j) {
-    for (int e = t; e < w * NR; e += 256) a.att[((long)i * a.T + e / NR) * NR + e % NR] = sm.a2[e / NR][e % NR];
-  }
-  // 4. C[d][k] = sum_r ctx[r][d] A2[k][r]  (thread = d)
-  const int d = t;
-  float c[TMAX];
-#pragma unroll
-  for (int k = 0; k < TMAX; ++k) c[k] = 0.f;
-  for (int r = 0; r < NR; ++r) {
-    const float v = ctx[(long)r * ND + d];
-#pragma unroll
-    for (int k = 0; k < TMAX; ++k) c[k] += v * sm.a2[k][r];
-  }
-  // 5. cosine per word (DAMSM_losses.py:17-23): block reductions over d
-#pragma unroll
-  for (int k = 0; k < TMAX; ++k) {
-    if (k < w) {
-      const float qv = sm.q[d][k];
-      const float u = wave_sum(qv * c[k]);
-      const float q2 = wave_sum(qv * qv);
-      const float c2 = wave_sum(c[k] * c[k]);
-      if (lane == 0) {
-        sm.red[wv][k][0] = u;
-        sm.red[wv][k][1] = q2;
-        sm.red[wv][k][2] = c2;
-      }
-    }
-  }
-  __syncthreads();
-  if (t < w) {
-    const int k = t;
-    const float u = sm.red[0][k][0] + sm.red[1][k][0] + sm.red[2][k][0] + sm.red[3][k][0];
-    const float q2 = sm.red[0][k][1] + sm.red[1][k][1] + sm.red[2][k][1] + sm.red[3][k][1];
-    const float c2 = sm.red[0][k][2] + sm.red[1][k][2] + sm.red[2][k][2] + sm.red[3][k][2];
-    sm.nq[k] = sqrtf(q2);
-    sm.nc[k] = sqrtf(c2);
-    sm.cs[k] = u / fmaxf(sm.nq[k] * sm.nc[k], 1e-8f);
-  }
-  __syncthreads();
-  // 6. row similarity = log sum_k exp(gamma2 cos_k)   (DAMSM_losses.py:315-317)
-  float se = 0.f;
-  for (int k = 0; k < w; ++k) se += __expf(GAMMA2 * sm.cs[k]);
-  if (!BWD) {
-    if (t == 0) a.sim[(long)j * a.B + i] = GAMMA3 * logf(se);
-    return;
-  }
-  // ================================ backward ================================
-  const float drow = GAMMA3 * a.dsim[(long)j * a.B + i];
-  float dqv[TMAX];
-#pragma unroll
-  for (int k = 0; k < TMAX; ++k) {
-    float dC = 0.f;
-    dqv[k] = 0.f;
-    if (k < w) {
-      const float cs = sm.cs[k], nq = sm.nq[k], nc = sm.nc[k];
-      const float dcos = drow * GAMMA2 * __expf(GAMMA2 * cs) / se;
-      const float den = nq * nc;
-      const float qv = sm.q[d][k];
-      if (den > 1e-8f) {
-        dC = dcos * (qv / den - cs * c[k] / (nc * nc));
-        dqv[k] = dcos * (c[k] / den - cs * qv / (nq * nq));
-      } else {
-        dC = dcos * qv / 1e-8f;
-        dqv[k] = dcos * c[k] / 1e-8f;
-      }
-    }
-    sm.dc[d][k] = dC;
-  }
-  __syncthreads();
-  // dA2[k][r] = sum_d ctx[r][d] dC[d][k]   (thread per region)
-  for (int r = t; r < NR; r += 256) {
-    float s[TMAX];
-#pragma unroll
-    for (int k = 0; k < TMAX; ++k) s[k] = 0.f;
-    const float* row = ctx + (long)r * ND;
-    for (int dd = 0; dd < ND; dd += 4) {
-      const float4 c4 = *reinterpret_cast<const float4*>(row + dd);
-#pragma unroll
-      for (int k = 0; k < TMAX; ++k)
-        s[k] += c4.x * sm.dc[dd][k] + c4.y * sm.dc[dd + 1][k] + c4.z * sm.dc[dd + 2][k] + c4.w * sm.dc[dd + 3][k];
-    }
-#pragma unroll
-    for (int k = 0; k < TMAX; ++k) sm.da[k][r] = s[k];
-  }
-  __syncthreads();
-  // softmax-over-regions backward: dZ = A2 (dA2 - <A2, dA2>); dA1[r][k] = gamma1 dZ[k][r]
-  for (int k = wv; k < w; k += 4) {
-    float s = 0.f;
-    for (int r = lane; r < NR; r += 64) s += sm.a2[k][r] * sm.da[k][r];
-    s = wave_sum(s);
-    for (int r = lane; r < NR; r += 64) sm.da[k][r] = GAMMA1 * sm.a2[k][r] * (sm.da[k][r] - s);
-  }
-  __syncthreads();
-  // softmax-over-words backward: dS[r][k] = A1 (dA1 - <A1, dA1>)  (thread per region)
-  for (int r = t; r < NR; r += 256) {
-    float s = 0.f;
-    for (int k = 0; k < w; ++k) s += sm.a1[r][k] * sm.da[k][r];
-    for (int k = 0; k < TMAX; ++k) sm.a1[r][k] = k < w ? sm.a1[r][k] * (sm.da[k][r] - s) : 0.f;
-  }
-  __syncthreads();
-  // dctx[r][d] = sum_k dC[d][k] A2[k][r] + q[d][k] dS[r][k] ;  dq[d][k] += sum_r ctx[r][d] dS[r][k]
-  float* dreg = a.dreg + (long)j * NR * ND;
-  for (int r = 0; r < NR; ++r) {
-    float g = 0.f;
-    const float v = ctx[(long)r * ND + d];
-#pragma unroll
-    for (int k = 0; k < TMAX; ++k) {
-      g += sm.dc[d][k] * sm.a2[k][r] + sm.q[d][k] * sm.a1[r][k];
-      dqv[k] += v * sm.a1[r][k];
-    }
-    atomicAdd(dreg + (long)r * ND + d, g);
-  }
-  if (a.dwords) {
-#pragma unroll
-    for (int k = 0; k < TMAX; ++k)
-      if (k < w) atomicAdd(a.dwords + ((long)i * ND + d) * a.T + k, dqv[k]);
-  }
-}
+constexpr float GAMMA3 = 10.f;  // cfg.TRAIN.SMOOTH.GAMMA3
 
 // ------------------------------------------ masked bidirectional CE ------
 // sim[a][b] (rows a), mask[a][b] = cls[a]==cls[b] && a!=b  -> -inf.
@@ -278,9 +71,9 @@ __global__ void sim_ce_kernel(const float* sim, int B, const long* cls, const lo
 
 // ------------------------------------------------------------ sent loss --
 // cos[a][b] * gamma3 with norms clamped as in sent_loss (DAMSM_losses.py:253-258)
-__global__ void sent_sim_kernel(const float* cnn, const float* rnn, int B, int D, float* sim) {
+__global__ void sent_sim_kernel(const float* cnn, const float* rnn, int NB, int D, float* sim) {
   const int a = blockIdx.x;
-  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+  for (int b = threadIdx.x; b < NB; b += blockDim.x) {
     float u = 0.f, n1 = 0.f, n2 = 0.f;
     for (int k = 0; k < D; ++k) {
       const float x = cnn[(long)a * D + k], y = rnn[(long)b * D + k];
@@ -288,35 +81,38 @@ __global__ void sent_sim_kernel(const float* cnn, const float* rnn, int B, int D
       n1 += x * x;
       n2 += y * y;
     }
-    sim[(long)a * B + b] = u / fmaxf(sqrtf(n1) * sqrtf(n2), 1e-8f) * GAMMA3;
+    sim[(long)a * NB + b] = u / fmaxf(sqrtf(n1) * sqrtf(n2), 1e-8f) * GAMMA3;
   }
 }
 
-// norms of the rows of cnn (which 0) and rnn (which 1): nrm[which*B + b]
-__global__ void row_norm_kernel(const float* cnn, const float* rnn, int B, int D, float* nrm) {
-  const int b = blockIdx.x, which = blockIdx.y;
+// norms of the rows of cnn (b < NA) and rnn (NA <= b < NA + NB): nrm[b]
+__global__ void row_norm_kernel(const float* cnn, const float* rnn, int NA, int D, float* nrm) {
+  const int b0 = blockIdx.x;
+  const bool which = b0 >= NA;
+  const int b = which ? b0 - NA : b0;
   const float* X = which ? rnn : cnn;
   __shared__ float red[16];
   float s = 0.f;
   for (int k = threadIdx.x; k < D; k += blockDim.x) s += X[(long)b * D + k] * X[(long)b * D + k];
   s = block_sum(s, red);
-  if (threadIdx.x == 0) nrm[which * B + b] = sqrtf(s);
+  if (threadIdx.x == 0) nrm[b0] = sqrtf(s);
 }
 
-// gradient of sim = gamma3 * cos wrt cnn (which=0, rows) or rnn (which=1, cols); thread per (row, k)
-__global__ void sent_sim_bwd_kernel(const float* cnn, const float* rnn, int B, int D, const float* sim,
+// gradient of sim = gamma3 * cos wrt cnn (which=0, rows a < NA) or rnn (which=1, cols b < NB); thread per (row, k)
+__global__ void sent_sim_bwd_kernel(const float* cnn, const float* rnn, int NA, int NB, int D, const float* sim,
                                     const float* nrm, const float* dsim, int which, float* out) {
-  const long total = (long)B * D;
+  const int NX = which == 0 ? NA : NB, NY = which == 0 ? NB : NA;
+  const long total = (long)NX * D;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const int x = e / D, k = e % D;
     const float* X = which == 0 ? cnn : rnn;
     const float* Y = which == 0 ? rnn : cnn;
-    const float nx = nrm[which * B + x];
+    const float nx = nrm[which == 0 ? x : NA + x];
     const float xv = X[(long)x * D + k];
     float g = 0.f;
-    for (int y = 0; y < B; ++y) {
-      const float ny = nrm[(1 - which) * B + y];
-      const long idx = which == 0 ? (long)x * B + y : (long)y * B + x;
+    for (int y = 0; y < NY; ++y) {
+      const float ny = nrm[which == 0 ? NA + y : y];
+      const long idx = which == 0 ? (long)x * NB + y : (long)y * NB + x;
       const float ds = dsim[idx];
       const float yv = Y[(long)y * D + k];
       const float den = nx * ny;
@@ -558,47 +354,6 @@ __global__ void attr_attn_bwd_kernel(const float* q, const float* k, const float
 
 extern "C" {
 
-int eegan_words_sim(const float* regions, const float* words, const long* cap_lens, int B, int T, float* sim,
-                    float* att, hipStream_t s) {
-  if (T > TMAX) {
-    ee_set_error("words_sim: T=%d > %d", T, TMAX);
-    return -22;
-  }
-  WordsArgs a = {};
-  a.reg = regions;
-  a.words = words;
-  a.lens = cap_lens;
-  a.B = B;
-  a.T = T;
-  a.sim = sim;
-  a.att = att;
-  dim3 grid(B, B);
-  words_pair_kernel<false><<<grid, 256, sizeof(WordsSmem), s>>>(a);
-  return ee_check_launch("words_sim");
-}
-
-int eegan_words_sim_bwd(const float* regions, const float* words, const long* cap_lens, int B, int T,
-                        const float* dsim, float* dregions, float* dwords, hipStream_t s) {
-  if (T > TMAX) {
-    ee_set_error("words_sim_bwd: T=%d > %d", T, TMAX);
-    return -22;
-  }
-  (void)hipMemsetAsync(dregions, 0, (size_t)B * NR * ND * sizeof(float), s);
-  if (dwords) (void)hipMemsetAsync(dwords, 0, (size_t)B * ND * T * sizeof(float), s);
-  WordsArgs a = {};
-  a.reg = regions;
-  a.words = words;
-  a.lens = cap_lens;
-  a.B = B;
-  a.T = T;
-  a.dsim = dsim;
-  a.dreg = dregions;
-  a.dwords = dwords;
-  dim3 grid(B, B);
-  words_pair_kernel<true><<<grid, 256, sizeof(WordsSmem), s>>>(a);
-  return ee_check_launch("words_sim_bwd");
-}
-
 int eegan_sim_ce(const float* sim, int B, const long* class_ids, const long* labels, float* loss2, hipStream_t s) {
   sim_ce_kernel<<<1, 256, 2 * B * sizeof(float), s>>>(sim, B, class_ids, labels, loss2, nullptr, nullptr);
   return ee_check_launch("sim_ce");
@@ -610,17 +365,16 @@ int eegan_sim_ce_bwd(const float* sim, int B, const long* class_ids, const long*
   return ee_check_launch("sim_ce_bwd");
 }
 
-int eegan_sent_sim(const float* cnn, const float* rnn, int B, int D, float* sim, hipStream_t s) {
-  sent_sim_kernel<<<B, 64, 0, s>>>(cnn, rnn, B, D, sim);
+int eegan_sent_sim(const float* cnn, const float* rnn, int na, int nb, int D, float* sim, hipStream_t s) {
+  sent_sim_kernel<<<na, 64, 0, s>>>(cnn, rnn, nb, D, sim);
   return ee_check_launch("sent_sim");
 }
 
-int eegan_sent_sim_bwd(const float* cnn, const float* rnn, int B, int D, const float* sim, const float* dsim,
+int eegan_sent_sim_bwd(const float* cnn, const float* rnn, int na, int nb, int D, const float* sim, const float* dsim,
                        float* nrm_ws, float* dcnn, float* drnn, hipStream_t s) {
-  row_norm_kernel<<<dim3(B, 2), 64, 0, s>>>(cnn, rnn, B, D, nrm_ws);
-  const int blocks = ee_cdiv((long)B * D, 256);
-  if (dcnn) sent_sim_bwd_kernel<<<blocks, 256, 0, s>>>(cnn, rnn, B, D, sim, nrm_ws, dsim, 0, dcnn);
-  if (drnn) sent_sim_bwd_kernel<<<blocks, 256, 0, s>>>(cnn, rnn, B, D, sim, nrm_ws, dsim, 1, drnn);
+  row_norm_kernel<<<na + nb, 64, 0, s>>>(cnn, rnn, na, D, nrm_ws);
+  if (dcnn) sent_sim_bwd_kernel<<<ee_cdiv((long)na * D, 256), 256, 0, s>>>(cnn, rnn, na, nb, D, sim, nrm_ws, dsim, 0, dcnn);
+  if (drnn) sent_sim_bwd_kernel<<<ee_cdiv((long)nb * D, 256), 256, 0, s>>>(cnn, rnn, na, nb, D, sim, nrm_ws, dsim, 1, drnn);
   return ee_check_launch("sent_sim_bwd");
 }
 

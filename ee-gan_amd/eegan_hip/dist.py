@@ -138,10 +138,9 @@ def all_gather(x, differentiable=True):
 
 
 class GradReducer(object):
-    """Gradient averaging for DataParallelWithCallback when the caller keeps
-    torch.optim.Adam (reference train.py unchanged): averages every
-    parameter's .grad across ranks when `sync()` is called (FlatAdam does this
-    itself inside step())."""
+    """Explicit gradient averaging: averages every parameter's .grad across
+    ranks when `sync()` is called.  Kept for callers that drive the reduction
+    themselves; the drop-in modules average through GradHooks instead."""
 
     def __init__(self, module):
         self.params = [p for p in module.parameters() if p.requires_grad]
@@ -160,3 +159,99 @@ class GradReducer(object):
             n = g.numel()
             g.copy_(flat[o:o + n].view_as(g))
             o += n
+
+
+class GradHooks(object):
+    """Gradient averaging across ranks for an unchanged reference train.py
+    (torch.optim.Adam, train.py:252-263): the reference's single-process
+    nn.DataParallel reduce-adds replica gradients to GPU0 inside every
+    backward (train.py:220-228); here each parameter of the module gets a
+    post-accumulate-grad hook, parameters are grouped into buckets in reverse
+    registration order (roughly the order backward produces them), a bucket's
+    flattened gradients are all-reduced asynchronously as soon as all of its
+    members have accumulated, and an end-of-backward callback flushes the
+    partial buckets (parameters that got no gradient in this backward, e.g.
+    resD.conv_s when fin == fout, are skipped -- every rank runs the same graph,
+    so the skipped set agrees), waits, divides by the world size and writes the
+    averages back into .grad.
+
+    Averaging the accumulated .grad is exact even when a backward adds to a
+    gradient that an earlier backward already averaged: that earlier part is
+    identical on every rank, and the mean is linear.  Parameters owned by a
+    FlatAdam (eegan_hip.optim) are skipped: it averages its flat buffer
+    itself.  Parameters are flagged `_eegan_hooked`, which turns off the
+    kernels' direct accumulation into .grad for them (that path bypasses
+    AccumulateGrad, whose hooks this relies on)."""
+
+    def __init__(self, module, bucket_bytes=25 << 20):
+        params = [p for p in module.parameters() if p.requires_grad and not hasattr(p, '_eegan_gen')]
+        self.buckets = []
+        cur, size = [], 0
+        for p in reversed(params):
+            if getattr(p, '_eegan_hooked', False):
+                continue  # shared with another hooked module
+            cur.append(p)
+            size += p.numel() * p.element_size()
+            if size >= bucket_bytes:
+                self.buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self._where = {}
+        for bi, b in enumerate(self.buckets):
+            for p in b:
+                p._eegan_hooked = True
+                self._where[id(p)] = bi
+                p.register_post_accumulate_grad_hook(self._hook)
+        self._reset()
+
+    def _reset(self):
+        self._fired = [[] for _ in self.buckets]
+        self._works = []
+        self._queued = False
+
+    def _launch(self, bi):
+        ps = self._fired[bi]
+        if not ps:
+            return
+        flat = torch.cat([p.grad.reshape(-1) for p in ps])
+        work = dist.all_reduce(flat, async_op=True)
+        self._works.append((work, flat, list(ps)))
+        self._fired[bi] = None   # launched
+
+    def _hook(self, p):
+        if not collective() or getattr(p, '_eegan_gen', None) is not None:
+            return
+        bi = self._where[id(p)]
+        if self._fired[bi] is None:    # a second backward over an already-reduced bucket: start over
+            self._fired[bi] = []
+        self._fired[bi].append(p)
+        if len(self._fired[bi]) == len(self.buckets[bi]):
+            self._launch(bi)
+        if not self._queued:
+            self._queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finish)
+
+    def _finish(self):
+        for bi in range(len(self.buckets)):
+            if self._fired[bi]:
+                self._launch(bi)
+        inv = 1.0 / world_size()
+        for work, flat, ps in self._works:
+            work.wait()
+            flat.mul_(inv)
+            o = 0
+            for p in ps:
+                n = p.grad.numel()
+                p.grad.copy_(flat[o:o + n].view_as(p.grad))
+                o += n
+        self._reset()
+
+
+def ensure_grad_hooks(module):
+    """Install GradHooks on `module` once, when the step is data-parallel
+    (called from the drop-in models' forward, so reference code that wraps D
+    and ATTR_Enhance in torch's own nn.DataParallel gets them too)."""
+    if getattr(module, '_eegan_grad_hooks', None) is None and collective():
+        module._eegan_grad_hooks = GradHooks(module)
+    return getattr(module, '_eegan_grad_hooks', None)

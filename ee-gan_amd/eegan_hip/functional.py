@@ -27,6 +27,25 @@ SKIP_PARAM_GRADS_IN_AUTOGRAD_GRAD = True
 # Process-group hook for SyncBN statistics (set by eegan_hip.dist)
 SYNC_BN_ALLREDUCE = None   # callable(tensor fp64) -> None (in-place sum over ranks)
 SYNC_BN_WORLD = 1
+# The reference's multi-device numerics (clamp(var, eps)^-1/2, zero gradient
+# through the clamp, running_var from the unbiased variance:
+# sync_batchnorm/batchnorm.py:113-125) are used whenever the world is > 1;
+# EEGAN_SYNCBN_MULTI=1 (or this flag) selects them at world 1 too, so one GPU
+# can test the kernels' clamp path against the oracle's restatement.
+SYNC_BN_FORCE_MULTI = os.environ.get('EEGAN_SYNCBN_MULTI', '0') == '1'
+
+
+def _syncbn_world():
+    """World size of the SyncBN statistics.  A process group started by the
+    caller (reference train.py under torchrun, not eegan_hip.dist.init_from_env)
+    is picked up on first use, so the drop-in modules synchronise without any
+    call into this package."""
+    if SYNC_BN_ALLREDUCE is None:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            from . import dist as D
+            D.install_syncbn_hook()
+    return SYNC_BN_WORLD
 
 
 def _needed(ctx, i):
@@ -57,8 +76,8 @@ def _grad_sink(ctx, i):
         return None
     node = ctx.next_functions[i][0]
     var = getattr(node, 'variable', None)
-    if var is None:
-        return None
+    if var is None or getattr(var, '_eegan_hooked', False):
+        return None   # hooked parameters (eegan_hip.dist.GradHooks) need AccumulateGrad to run
     g = var.grad
     if g is None or g.dtype != F32 or g.shape != var.shape or g.stride() != var.stride():
         return None
@@ -1046,12 +1065,12 @@ class BnModFn(torch.autograd.Function):
         ws = workspace(ops.bn_stats_workspace(P, C), dev)
         sums = torch.empty(2 * C, dtype=torch.float64, device=dev)
         ops.bn_stats(x.data_ptr(), P, C, ld_of(x), ws.data_ptr(), sums.data_ptr(), s)
-        world = SYNC_BN_WORLD
+        world = _syncbn_world()
         if world > 1:
             _allreduce_f64(sums)
             count *= world
         stats = torch.empty(3 * C, dtype=F32, device=dev)
-        clamp_mode = 1 if world > 1 else 0
+        clamp_mode = 1 if (world > 1 or SYNC_BN_FORCE_MULTI) else 0
         rm = bn.running_mean if (bn is not None and bn.track_running_stats) else None
         rv = bn.running_var if rm is not None else None
         ops.bn_finalize(sums.data_ptr(), C, count, 4.0 if up2 else 1.0, bn.eps if bn is not None else 1e-5,
@@ -1458,23 +1477,29 @@ class SimCEFn(torch.autograd.Function):
 
 
 class WordsSimFn(torch.autograd.Function):
-    """similarity matrix of words_loss (DAMSM_losses.py:281-331) before masking."""
+    """Word-level similarity block of words_loss (DAMSM_losses.py:281-331)
+    before masking: sim[j][i] for this rank's images j (regions) x the given
+    captions i (words, cap_lens -- all ranks' captions when data-parallel).
+    `diag_off`: caption index of image 0's own caption (rank * B_local), used
+    for the attention maps of the matching pairs."""
 
     @staticmethod
-    def forward(ctx, regions, words, cap_lens, want_att):
-        # regions: (B, 256, 17, 17) fp32 NHWC-dense or NCHW
-        B = regions.shape[0]
-        if regions.dtype == F32 and T.is_nhwc(regions) and ld_of(regions) == regions.shape[1]:
+    def forward(ctx, regions, words, cap_lens, want_att, diag_off=0):
+        # regions: (n_img, 256, 17, 17) fp32, NHWC-dense (the Inception projection output) or NCHW
+        n_img = regions.shape[0]
+        if regions.dtype == F32 and T.is_nhwc(regions) and ld_of(regions) == regions.shape[1] \
+                and regions.data_ptr() % 16 == 0:
             reg = regions
         else:
             reg = regions.float().permute(0, 2, 3, 1).contiguous().permute(0, 3, 1, 2)
         wd = words.float().contiguous()
-        lens = cap_lens.to(device=regions.device, dtype=torch.long).contiguous()
-        Tn = wd.shape[2]
-        sim = torch.empty((B, B), dtype=F32, device=regions.device)
-        att = torch.zeros((B, Tn, 289) if want_att else (0,), dtype=F32, device=regions.device)
-        ops.words_sim(reg.data_ptr(), wd.data_ptr(), lens.data_ptr(), B, Tn, sim.data_ptr(),
-                      att.data_ptr() if want_att else 0, stream())
+        n_txt, Tn = wd.shape[0], wd.shape[2]
+        lens = cap_lens.to(device=regions.device, dtype=torch.long).reshape(-1).contiguous()
+        sim = torch.empty((n_img, n_txt), dtype=F32, device=regions.device)
+        att = torch.zeros((n_img, Tn, 289) if want_att else (0,), dtype=F32, device=regions.device)
+        ws = workspace(ops.words_workspace(n_img, n_txt, 0, 0), regions.device)
+        ops.words_sim(reg.data_ptr(), wd.data_ptr(), lens.data_ptr(), n_img, n_txt, Tn, int(diag_off), sim.data_ptr(),
+                      att.data_ptr() if want_att else 0, ws.data_ptr(), stream())
         ctx.save_for_backward(reg, wd, lens)
         ctx.mark_non_differentiable(att)
         return sim, att
@@ -1482,36 +1507,43 @@ class WordsSimFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dsim, _datt):
         reg, wd, lens = ctx.saved_tensors
-        B, Tn = wd.shape[0], wd.shape[2]
+        n_img, n_txt, Tn = reg.shape[0], wd.shape[0], wd.shape[2]
         dsim = dsim.float().contiguous()
-        dreg = torch.empty((B, 17, 17, 256), dtype=F32, device=dsim.device)
-        dw = torch.empty_like(wd) if ctx.needs_input_grad[1] else None
-        ops.words_sim_bwd(reg.data_ptr(), wd.data_ptr(), lens.data_ptr(), B, Tn, dsim.data_ptr(), dreg.data_ptr(),
-                          ptr(dw), stream())
-        return dreg.permute(0, 3, 1, 2), dw, None, None
+        need_dw = ctx.needs_input_grad[1]
+        dreg = torch.empty((n_img, 17, 17, 256), dtype=F32, device=dsim.device)
+        dw = torch.empty_like(wd) if need_dw else None
+        ws = workspace(ops.words_workspace(n_img, n_txt, 1, int(need_dw)), dsim.device)
+        ops.words_sim_bwd(reg.data_ptr(), wd.data_ptr(), lens.data_ptr(), n_img, n_txt, Tn, dsim.data_ptr(),
+                          dreg.data_ptr(), ptr(dw), ws.data_ptr(), stream())
+        return dreg.permute(0, 3, 1, 2), dw, None, None, None
 
 
 class SentSimFn(torch.autograd.Function):
+    """gamma3 * cos(cnn_a, rnn_b) for this rank's images a x the given
+    captions b (DAMSM_losses.py:246-258)."""
+
     @staticmethod
     def forward(ctx, cnn, rnn):
         c = cnn.float().contiguous()
         r = rnn.float().contiguous()
-        B, Dm = c.shape
-        sim = torch.empty((B, B), dtype=F32, device=c.device)
-        ops.sent_sim(c.data_ptr(), r.data_ptr(), B, Dm, sim.data_ptr(), stream())
+        na, Dm = c.shape
+        nb = r.shape[0]
+        sim = torch.empty((na, nb), dtype=F32, device=c.device)
+        ops.sent_sim(c.data_ptr(), r.data_ptr(), na, nb, Dm, sim.data_ptr(), stream())
         ctx.save_for_backward(c, r, sim)
         return sim
 
     @staticmethod
     def backward(ctx, dsim):
         c, r, sim = ctx.saved_tensors
-        B, Dm = c.shape
+        na, Dm = c.shape
+        nb = r.shape[0]
         dsim = dsim.float().contiguous()
-        nrm = torch.empty(2 * B, dtype=F32, device=c.device)
+        nrm = torch.empty(na + nb, dtype=F32, device=c.device)
         dc = torch.empty_like(c) if ctx.needs_input_grad[0] else None
         dr = torch.empty_like(r) if ctx.needs_input_grad[1] else None
-        ops.sent_sim_bwd(c.data_ptr(), r.data_ptr(), B, Dm, sim.data_ptr(), dsim.data_ptr(), nrm.data_ptr(), ptr(dc),
-                         ptr(dr), stream())
+        ops.sent_sim_bwd(c.data_ptr(), r.data_ptr(), na, nb, Dm, sim.data_ptr(), dsim.data_ptr(), nrm.data_ptr(),
+                         ptr(dc), ptr(dr), stream())
         return dc, dr
 
 

@@ -16,6 +16,7 @@ import torch
 
 from . import functional as Fn
 from . import dist as D
+from . import damsm as G
 from .optim import FlatAdam
 
 
@@ -170,22 +171,26 @@ class Trainer(object):
 
     def DAMSM_loss(self, fake_imgs, sent_emb, words_embs, attrs_emb, class_ids, batch_size, match_labels, cap_lens,
                    image_encoder):
-        """train.py:419-435 over the GLOBAL batch when data-parallel."""
+        """train.py:419-435 over the GLOBAL batch when data-parallel: this rank's
+        image rows against every rank's captions, the similarity blocks gathered
+        (eegan_hip.damsm; damsm_global=False keeps the losses per rank)."""
         region_features, cnn_code = image_encoder(fake_imgs)
-        if self.damsm_global and D.collective():
-            region_features = D.all_gather(region_features)
-            cnn_code = D.all_gather(cnn_code)
-            sent_emb = D.all_gather(sent_emb, differentiable=False)
-            attrs_emb = D.all_gather(attrs_emb)
-            words_embs = D.all_gather(words_embs, differentiable=False)
-            cap_lens = D.all_gather(torch.as_tensor(cap_lens, device=sent_emb.device), differentiable=False)
-            class_ids = D.all_gather(class_ids, differentiable=False) if class_ids is not None else None
-            batch_size = batch_size * D.world_size()
-            match_labels = torch.arange(batch_size, device=sent_emb.device)
-        s = Fn.SimCEFn.apply(Fn.SentSimFn.apply(cnn_code, sent_emb), class_ids, match_labels)
-        wsim, _ = Fn.WordsSimFn.apply(region_features, words_embs, cap_lens, False)
-        w = Fn.SimCEFn.apply(wsim, class_ids, match_labels)
-        a = Fn.SimCEFn.apply(Fn.SentSimFn.apply(cnn_code, attrs_emb), class_ids, match_labels)
+        dev = cnn_code.device
+        if self.damsm_global:
+            cls = G.global_class_ids(class_ids, dev)
+            lab = G.global_labels(match_labels, batch_size, dev)
+            s_sim = G.sent_block(cnn_code, sent_emb)
+            w_sim, _ = G.words_block(region_features, words_embs, cap_lens)
+            a_sim = G.sent_block(cnn_code, attrs_emb)
+        else:
+            cls = G._dev_long(class_ids, dev)
+            lab = G._dev_long(match_labels, dev)
+            s_sim = Fn.SentSimFn.apply(cnn_code, sent_emb)
+            w_sim, _ = Fn.WordsSimFn.apply(region_features, words_embs, G._dev_long(cap_lens, dev), False)
+            a_sim = Fn.SentSimFn.apply(cnn_code, attrs_emb)
+        s = Fn.SimCEFn.apply(s_sim, cls, lab)
+        w = Fn.SimCEFn.apply(w_sim, cls, lab)
+        a = Fn.SimCEFn.apply(a_sim, cls, lab)
         lam = 1.0
         return (w[0] + w[1]) * lam, (s[0] + s[1]) * lam, (a[0] + a[1]) * lam
 

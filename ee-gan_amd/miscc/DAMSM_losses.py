@@ -3,10 +3,18 @@
 Hot path: ``words_loss`` (DAMSM_losses.py:272-342) and ``sent_loss``
 (233-270) run as fused HIP kernels: ONE launch computes func_attention
 (25-63), the word-level cosine similarity (17-23) and the log-sum-exp row
-similarity for all B^2 (image, text) pairs, one launch applies the
-same-class -inf mask and the bidirectional cross-entropy, and the backward
-recomputes the attention in-kernel (no per-sample Python loop, no
-``cap_lens.tolist()`` host sync).
+similarity for every (image, caption) pair on bf16 MFMA (csrc/damsm.hip), one
+launch applies the same-class -inf mask and the bidirectional cross-entropy,
+and the backward recomputes the attention in-kernel (no per-sample Python
+loop, no ``cap_lens.tolist()`` host sync).
+
+Data parallel (a process group with world > 1): the losses keep the
+reference's global-batch semantics (its DataParallel gathers the batch onto
+one device, train.py:220-228, 419-435) -- each rank computes its images'
+rows against every rank's captions and the blocks are gathered into the
+B_global x B_global matrix (eegan_hip.damsm); ``labels`` are the rank's
+local match labels (arange(batch_size) from prepare_labels), ``class_ids``
+its local ids, and ``batch_size`` the local batch size.
 
 ``cosine_similarity``, ``func_attention``, ``GlobalAttentionGeneral``,
 ``sent_similarity`` and ``words_similarity`` are kept for API completeness
@@ -18,6 +26,7 @@ import torch.nn as nn
 
 from miscc.config import cfg
 from eegan_hip import functional as Fn
+from eegan_hip import damsm as G
 
 
 def cosine_similarity(x1, x2, dim=1, eps=1e-8):
@@ -58,33 +67,26 @@ class GlobalAttentionGeneral(nn.Module):
         return wc.reshape(B, -1, ih, iw), attn.reshape(B, -1, ih, iw)
 
 
-def _cls_dev(class_ids, device):
-    if class_ids is None:
-        return None
-    return torch.as_tensor(class_ids).to(device=device, dtype=torch.long, non_blocking=True).contiguous()
-
-
-def _labels_dev(labels, device):
-    if labels is None:
-        return None
-    return torch.as_tensor(labels).to(device=device, dtype=torch.long, non_blocking=True).contiguous()
+def _masked(sim, class_ids, batch_size):
+    cls = G.global_class_ids(class_ids, sim.device)
+    if cls is not None:
+        n = sim.shape[0]
+        m = (cls[None, :] == cls[:n, None]) & ~torch.eye(n, dtype=torch.bool, device=sim.device)
+        sim = sim.masked_fill(m, -float('inf'))
+    return sim
 
 
 def sent_similarity(cnn_code, rnn_code, class_ids, batch_size, eps=1e-8):
-    sim = Fn.SentSimFn.apply(cnn_code, rnn_code)
-    cls = _cls_dev(class_ids, sim.device)
-    if cls is not None:
-        m = (cls[None, :] == cls[:batch_size, None]) & ~torch.eye(batch_size, dtype=torch.bool, device=sim.device)
-        sim = sim.masked_fill(m, -float('inf'))
-    return sim
+    return _masked(G.sent_block(cnn_code, rnn_code), class_ids, batch_size)
 
 
 def sent_loss(cnn_code, rnn_code, labels, class_ids, batch_size, eps=1e-8):
     """(CE(scores, labels), CE(scores^T, labels)); scores = gamma3 * cos, same-class masked."""
     if labels is None:
         return None, None
-    sim = Fn.SentSimFn.apply(cnn_code, rnn_code)
-    losses = Fn.SimCEFn.apply(sim, _cls_dev(class_ids, sim.device), _labels_dev(labels, sim.device))
+    sim = G.sent_block(cnn_code, rnn_code)
+    losses = Fn.SimCEFn.apply(sim, G.global_class_ids(class_ids, sim.device),
+                              G.global_labels(labels, batch_size, sim.device))
     return losses[0], losses[1]
 
 
@@ -107,19 +109,16 @@ class _AttMaps(object):
 
 
 def words_similarity(img_features, words_emb, cap_lens, class_ids, batch_size):
-    sim, att = Fn.WordsSimFn.apply(img_features, words_emb, torch.as_tensor(cap_lens), True)
-    cls = _cls_dev(class_ids, sim.device)
-    if cls is not None:
-        m = (cls[None, :] == cls[:batch_size, None]) & ~torch.eye(batch_size, dtype=torch.bool, device=sim.device)
-        sim = sim.masked_fill(m, -float('inf'))
-    return sim, _AttMaps(att, cap_lens)
+    sim, att = G.words_block(img_features, words_emb, cap_lens, True)
+    return _masked(sim, class_ids, batch_size), _AttMaps(att, cap_lens)
 
 
 def words_loss(img_features, words_emb, labels, cap_lens, class_ids, batch_size):
     """Returns (loss0, loss1, att_maps) like DAMSM_losses.py:272-342."""
-    sim, att = Fn.WordsSimFn.apply(img_features, words_emb, torch.as_tensor(cap_lens), True)
+    sim, att = G.words_block(img_features, words_emb, cap_lens, True)
     maps = _AttMaps(att, cap_lens)
     if labels is None:
         return None, None, maps
-    losses = Fn.SimCEFn.apply(sim, _cls_dev(class_ids, sim.device), _labels_dev(labels, sim.device))
+    losses = Fn.SimCEFn.apply(sim, G.global_class_ids(class_ids, sim.device),
+                              G.global_labels(labels, batch_size, sim.device))
     return losses[0], losses[1], maps

@@ -25,6 +25,7 @@ import torch.nn as nn
 from miscc.config import cfg
 from sync_batchnorm import SynchronizedBatchNorm2d
 from eegan_hip import functional as Fn
+from eegan_hip import dist as D
 from eegan_hip.nn import Conv2d, Linear
 
 BatchNorm = SynchronizedBatchNorm2d
@@ -181,6 +182,7 @@ class ATTR_Enhance(nn.Module):
         self._norm_fact = 1 / math.sqrt(ntf)
 
     def forward(self, sent, attrs):
+        D.ensure_grad_hooks(self)   # data-parallel gradient averaging (no-op at world 1)
         combine = torch.cat([sent.unsqueeze(1), attrs], dim=1).float()
         q = self.attr_query(combine)
         k = self.attr_key(combine)
@@ -243,6 +245,7 @@ class Gen(nn.Module):
         return gb
 
     def forward(self, x, sent, attrs):
+        D.ensure_grad_hooks(self)
         gb = self.affine_mlps(sent, attrs) if Fn.GROUPED_MLP else [None] * 7
         out = self.fc(x.float())
         out = Fn.FcToNhwcFn.apply(out, 8 * self.ngf)
@@ -345,6 +348,7 @@ class DiscCond(nn.Module):
 
 class _DisBase(nn.Module):
     def _stem(self, x):
+        D.ensure_grad_hooks(self)   # covers COND_DNET, which train.py calls outside forward
         if x.dtype != torch.bfloat16:
             x = Fn.ImageToNhwcFn.apply(x)
         return self.conv_img(x)

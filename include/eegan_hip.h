@@ -26,7 +26,8 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 3  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate */
+#define EEGAN_ABI_VERSION 4  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
+                                4: rectangular (local x global) DAMSM words / sentence blocks on MFMA */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
@@ -216,18 +217,27 @@ int eegan_act_bwd_f32(const float* dy, const float* y, long n, int act, float sl
 /* ------------------------------------------------------------------ losses --
  * replaces: miscc/DAMSM_losses.py:17-63 (cosine_similarity, func_attention),
  * 233-342 (sent_loss, words_loss); train.py:99-103, 336-417; models.py:155-180 */
-/* sim[j][i] = gamma3 * log sum_k exp(gamma2 cos(word_ik, attn-context_jk)) for every (image j, text i) */
-int eegan_words_sim(const float* regions, const float* words, const long* cap_lens, int B, int T, float* sim,
-                    float* att, hipStream_t s);
-int eegan_words_sim_bwd(const float* regions, const float* words, const long* cap_lens, int B, int T,
-                        const float* dsim, float* dregions, float* dwords, hipStream_t s);
+/* Word-level DAMSM similarity (csrc/damsm.hip; replaces DAMSM_losses.py:17-63 and the per-caption loop of
+ * words_loss, 272-331): sim[j][i] = gamma3 * log sum_k exp(gamma2 cos(word_ik, attn-context_jk)) for every
+ * (image j < n_img, caption i < n_txt) -- a data-parallel rank passes its own images and ALL ranks' captions
+ * (B_local x B_global block).  regions fp32 [n_img][289][256] (16-B aligned), words fp32 [n_txt][256][T]
+ * (T <= 32), cap_lens int64 [n_txt].  att (optional): the attention maps of the pairs (j, j + diag_off),
+ * [n_img][T][289].  Workspace bytes from eegan_words_workspace (backward: 1 for the _bwd call, want_dwords:
+ * dwords != NULL).  dregions [n_img][289][256] and dwords [n_txt][256][T] are overwritten, deterministically. */
+long eegan_words_workspace(int n_img, int n_txt, int backward, int want_dwords);
+int eegan_words_sim(const float* regions, const float* words, const long* cap_lens, int n_img, int n_txt, int T,
+                    int diag_off, float* sim, float* att, void* ws, hipStream_t s);
+int eegan_words_sim_bwd(const float* regions, const float* words, const long* cap_lens, int n_img, int n_txt, int T,
+                        const float* dsim, float* dregions, float* dwords, void* ws, hipStream_t s);
 /* loss2 = (CE(sim, labels), CE(sim^T, labels)) with same-class off-diagonal entries masked to -inf
  * (labels == NULL means arange(B), the reference's match_labels) */
 int eegan_sim_ce(const float* sim, int B, const long* class_ids, const long* labels, float* loss2, hipStream_t s);
 int eegan_sim_ce_bwd(const float* sim, int B, const long* class_ids, const long* labels, const float* gloss2,
                      float* dsim, hipStream_t s);
-int eegan_sent_sim(const float* cnn, const float* rnn, int B, int D, float* sim, hipStream_t s);
-int eegan_sent_sim_bwd(const float* cnn, const float* rnn, int B, int D, const float* sim, const float* dsim,
+/* sentence cosine block sim[a][b] = gamma3 cos(cnn_a, rnn_b), a < na (this rank's images), b < nb (all
+ * ranks' captions) (DAMSM_losses.py:246-258); nrm_ws holds na + nb floats */
+int eegan_sent_sim(const float* cnn, const float* rnn, int na, int nb, int D, float* sim, hipStream_t s);
+int eegan_sent_sim_bwd(const float* cnn, const float* rnn, int na, int nb, int D, const float* sim, const float* dsim,
                        float* nrm_ws, float* dcnn, float* drnn, hipStream_t s);
 /* mode 0 mean(relu(1-x)), 1 mean(relu(1+x)), 2 -mean(x), 3 mean(x) */
 int eegan_dout_reduce(const float* x, int n, int mode, float* out, hipStream_t s);

@@ -91,6 +91,59 @@ def _case_grad_reducer(rank):
         assert torch.allclose(p.grad, torch.full_like(p, (1 + WORLD) / 2.0))
 
 
+def _case_grad_hooks_adam(rank):
+    """GradHooks (installed by the drop-in models' forward) under an unchanged
+    train.py loop: torch.optim.Adam, no explicit sync call.  Each rank's loss
+    is the mean over its half of the batch; after backward + step on every
+    rank the parameters equal one single-process step on the whole batch (the
+    reference's nn.DataParallel semantics).  Includes a parameter that never
+    receives a gradient (resD.conv_s when fin == fout), two backwards
+    accumulated before one step, and small buckets so several all-reduces are
+    in flight."""
+    from eegan_hip import dist as D
+    torch.manual_seed(3)
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = torch.nn.Linear(6, 16)
+            self.b = torch.nn.Linear(16, 4)
+            self.unused = torch.nn.Linear(4, 4)
+
+        def forward(self, x):
+            return self.b(torch.relu(self.a(x)))
+
+    net, ref = Net(), Net()
+    ref.load_state_dict(net.state_dict())
+    hooks = D.GradHooks(net, bucket_bytes=64)   # several buckets
+    net._eegan_grad_hooks = hooks
+    assert D.ensure_grad_hooks(net) is hooks and len(hooks.buckets) > 2
+    opt = torch.optim.Adam(net.parameters(), lr=1e-2, betas=(0.0, 0.9))
+    opt_r = torch.optim.Adam(ref.parameters(), lr=1e-2, betas=(0.0, 0.9))
+    g = torch.Generator().manual_seed(11)
+    for it in range(3):
+        xs = [torch.randn(2 * WORLD, 6, generator=g) for _ in range(2)]
+        opt.zero_grad()
+        opt_r.zero_grad()
+        for x in xs:   # two backwards accumulate before the step
+            net(x[rank * 2:(rank + 1) * 2]).square().mean().backward()
+            ref(x).square().mean().backward()
+        for p, q in zip(net.parameters(), ref.parameters()):
+            if q.grad is None:
+                assert p.grad is None
+            else:
+                assert torch.allclose(p.grad, q.grad, atol=1e-6), it
+        opt.step()
+        opt_r.step()
+    for p, q in zip(net.parameters(), ref.parameters()):
+        assert torch.allclose(p, q, atol=1e-5)
+    # FlatAdam-owned parameters are averaged by FlatAdam itself, never hooked
+    m = torch.nn.Linear(3, 3)
+    m.weight._eegan_gen = [0]
+    h2 = D.GradHooks(m)
+    assert all(p is not m.weight for b in h2.buckets for p in b)
+
+
 def _case_syncbn_stats(rank):
     """Per-rank fp64 (sum, sumsq) -> all-reduce -> mean / clamp(var, eps)^-1/2
     on the global count, as the SyncBN Functions combine them across ranks,
@@ -121,6 +174,6 @@ def _case_syncbn_stats(rank):
     assert torch.allclose(rv.float(), sd['bn.running_var'], atol=1e-5)
 
 
-@pytest.mark.parametrize('case', ['all_gather', 'flat_adam_allreduce', 'grad_reducer', 'syncbn_stats'])
+@pytest.mark.parametrize('case', ['all_gather', 'flat_adam_allreduce', 'grad_reducer', 'grad_hooks_adam', 'syncbn_stats'])
 def test_gloo_world2(case):
     _run(globals()['_case_' + case])

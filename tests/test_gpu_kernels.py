@@ -148,6 +148,43 @@ def test_conv_thin_wgrad(gpu, monkeypatch):
         assert torch.allclose(outs[0], outs[1], rtol=1e-5, atol=1e-4)
 
 
+def test_splitk_reduce_vector_path_bit_identical(gpu, monkeypatch):
+    """The split-K reduce's 4-channel vector path (default) against the scalar
+    path (EEGAN_CONV_RED_VEC4=0): same summation order, so torch.equal, over
+    forward (bias, act, residual + gain) and backward-data (activation gate,
+    half-resolution residual of resD's pooled shortcut) epilogues; odd channel
+    counts take the scalar path in both runs.  EEGAN_CONV_TARGET forces the
+    K split on these small grids."""
+    Fn, T, _ = _mods()
+    monkeypatch.setenv('EEGAN_CONV_TARGET', '4096')
+    monkeypatch.setenv('EEGAN_CONV_MINK', '2')
+    lrelu = Fn.ACT_CODES['lrelu']
+    for N, Cin, H, W, Cout, k, st, pad in [(2, 256, 4, 4, 128, 3, 1, 1), (2, 96, 8, 8, 64, 4, 2, 1),
+                                            (3, 128, 6, 6, 36, 3, 1, 1), (2, 64, 8, 8, 9, 4, 2, 1),
+                                            (2, 9, 8, 8, 64, 3, 1, 1)]:
+        torch.manual_seed(N * Cin + Cout)
+        g = Fn.Geom(Cout, k, k, st, pad, pad, 0)
+        x = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        Wt = (torch.randn(Cout, Cin, k, k) * 0.05).to(gpu)
+        b = torch.randn(Cout).to(gpu)
+        gam = torch.tensor([0.7]).to(gpu)
+        Ho, Wo = g.out_hw(H, W)
+        res = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
+        dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
+        gate = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        halfres = _nhwc(torch.randn(N, Cin, H // 2, W // 2), gpu)
+        outs = []
+        for vec in ('0', '1'):
+            monkeypatch.setenv('EEGAN_CONV_RED_VEC4', vec)
+            o = [Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, res=res, gamma=gam).float().cpu(),
+                 Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, out_f32=True).cpu(),
+                 Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), gate=gate, gate_act=lrelu).float().cpu(),
+                 Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), res=halfres, res_up2=1, res_scale=0.25).float().cpu()]
+            outs.append(o)
+        for a, c in zip(*outs):
+            assert torch.equal(a, c)
+
+
 def test_cat_channels(gpu):
     """Inception branch concat (one launch when every part has C % 8 == 0,
     else the per-part path) against torch.cat, with strided (sliced) parts."""

@@ -182,6 +182,58 @@ def test_syncbn_module(gpu):
     assert x.grad.dtype == torch.float32 and x.grad.shape == x.shape
 
 
+@pytest.mark.parametrize('affine', [True, False])
+def test_syncbn_multi_device_formula(gpu, monkeypatch, affine):
+    """The kernels' multi-device SyncBN numerics (bn_finalize clamp mode,
+    selected at world 1 by Fn.SYNC_BN_FORCE_MULTI / EEGAN_SYNCBN_MULTI=1)
+    against the oracle's restatement of sync_batchnorm/batchnorm.py:57-75,
+    113-125: clamp(var_biased, eps)^-1/2, running_var from the unbiased
+    variance, and the gradient flowing through the batch statistics (zero
+    through the clamp).  Channel 3 is constant up to 1e-4 noise (variance
+    below eps), so the clamp branch and its zero gradient are exercised.
+    affine=False is affine_ssa's modulated path (mode 1, gamma = beta = 0)."""
+    from sync_batchnorm import SynchronizedBatchNorm2d
+    from eegan_hip import functional as Fn
+    from oracle import eegan_oracle as O
+    monkeypatch.setattr(Fn, 'SYNC_BN_FORCE_MULTI', True)
+    C = 8
+    x = seeded_tensor('bnm:x', (4, C, 5, 5), 1) * 0.7 + 0.3
+    x[:, 3] = 0.5 + 1e-4 * seeded_tensor('bnm:c', (4, 5, 5), 1)
+    x = x.to(torch.bfloat16).float()            # the kernels read bf16 activations
+    r = seeded_tensor('bnm:r', (4, C, 5, 5), 2).to(torch.bfloat16).float()
+    bn = SynchronizedBatchNorm2d(C, affine=affine)
+    sd = {'running_mean': seeded_tensor('bnm:rm', (C,), 1) * 0.1, 'running_var': 1 + seeded_tensor('bnm:rv', (C,), 1).abs()}
+    if affine:
+        sd['weight'] = 1 + 0.2 * seeded_tensor('bnm:w', (C,), 1)
+        sd['bias'] = 0.1 * seeded_tensor('bnm:b', (C,), 1)
+    bn.load_state_dict(sd, strict=False)
+    bn = bn.to(gpu)
+    xd = x.to(gpu).requires_grad_()
+    if affine:
+        y = bn(xd)
+    else:
+        zeros = torch.zeros(4, C, device=gpu)
+        y = bn.modulate(xd, zeros, zeros, torch.ones(4, 1, 5, 5, device=gpu))
+    (y.float() * r.to(gpu)).sum().backward()
+    sdo = {k: v.clone() for k, v in sd.items()}
+    for k in ('weight', 'bias'):
+        if k in sdo:
+            sdo[k].requires_grad_(True)
+    xo = x.clone().requires_grad_()
+    yo = O.sync_bn(xo, sdo, '', affine=affine, mode='multi')
+    (yo * r).sum().backward()
+    assert torch.isfinite(y.float()).all() and torch.isfinite(xd.grad).all()
+    _check('syncbn_multi/out', y, summary(yo.detach()), TOL_FWD)
+    _check('syncbn_multi/dx', xd.grad, summary(xo.grad), TOL_BWD)
+    # channel 3: inv_std = eps^-1/2 (clamped) and no gradient through the variance
+    assert abs(float(y.float()[:, 3].abs().max()) - float(yo.detach()[:, 3].abs().max())) < 2e-2
+    _check('syncbn_multi/rm', bn.running_mean, summary(sdo['running_mean']), 1e-5)
+    _check('syncbn_multi/rv', bn.running_var, summary(sdo['running_var']), 1e-5)
+    if affine:
+        _check('syncbn_multi/dw', bn.weight.grad, summary(sdo['weight'].grad), 1e-2)
+        _check('syncbn_multi/db', bn.bias.grad, summary(sdo['bias'].grad), 1e-2)
+
+
 def test_generator(gpu):
     import models
     g = golden()
@@ -316,6 +368,17 @@ def test_discriminator_and_gradient_penalty(gpu, kind):
     _grads(tag + '_gp', D, TOL_DEEP)
 
 
+# DAMSM words similarity on bf16 MFMA (csrc/damsm.hip): the attention logits
+# S = ctx q^T use split-bf16 products (hi*hi + lo*hi + hi*lo, ~fp32), the
+# context C = A2 ctx and the backward contractions plain bf16 with fp32
+# accumulation.  Emulating exactly that rounding in fp32 torch on these golden
+# inputs gives losses within 7e-5 relative and d regions / d words within
+# 3.6e-3 rel-L2 of the fp32 reference (1.0e-4 / 2.5e-3 at realistic region
+# scales); the gates below leave ~3x headroom.
+TOL_DAMSM_LOSS = 3e-4
+TOL_DAMSM_GRAD = 1.2e-2
+
+
 def test_damsm_losses(gpu):
     from miscc.DAMSM_losses import words_loss, sent_loss
     g = golden()
@@ -326,12 +389,12 @@ def test_damsm_losses(gpu):
     class_ids = torch.LongTensor([3, 7, 3, 1, 7, 3])
     labels = torch.arange(Bd).to(gpu)
     w0, w1, maps = words_loss(reg, words, labels, cap_lens, class_ids, Bd)
-    _check('damsm/w0', w0.reshape(1), g['damsm/w0'].reshape(1), 1e-4)
-    _check('damsm/w1', w1.reshape(1), g['damsm/w1'].reshape(1), 1e-4)
-    _check('damsm/att_map0', maps[0], g['damsm/att_map0'], 1e-4)
+    _check('damsm/w0', w0.reshape(1), g['damsm/w0'].reshape(1), TOL_DAMSM_LOSS)
+    _check('damsm/w1', w1.reshape(1), g['damsm/w1'].reshape(1), TOL_DAMSM_LOSS)
+    _check('damsm/att_map0', maps[0], g['damsm/att_map0'], 2e-3)
     (w0 + 0.7 * w1).backward()
-    _check('damsm/dreg', reg.grad, g['damsm/dreg'], 1e-3)
-    _check('damsm/dwords', words.grad, g['damsm/dwords'], 1e-3)
+    _check('damsm/dreg', reg.grad, g['damsm/dreg'], TOL_DAMSM_GRAD)
+    _check('damsm/dwords', words.grad, g['damsm/dwords'], TOL_DAMSM_GRAD)
     code = seeded_tensor('dm:code', (Bd, 256), 1).to(gpu).requires_grad_()
     rnn = seeded_tensor('dm:rnn', (Bd, 256), 1).to(gpu).requires_grad_()
     s0, s1 = sent_loss(code, rnn, labels, class_ids, Bd)
@@ -344,8 +407,57 @@ def test_damsm_losses(gpu):
     _check('damsm/s0_nocls', s0n.reshape(1), g['damsm/s0_nocls'].reshape(1), 1e-5)
     _check('damsm/s1_nocls', s1n.reshape(1), g['damsm/s1_nocls'].reshape(1), 1e-5)
     w0n, w1n, _ = words_loss(reg.detach(), words.detach(), labels, cap_lens, None, Bd)
-    _check('damsm/w0_nocls', w0n.reshape(1), g['damsm/w0_nocls'].reshape(1), 1e-4)
-    _check('damsm/w1_nocls', w1n.reshape(1), g['damsm/w1_nocls'].reshape(1), 1e-4)
+    _check('damsm/w0_nocls', w0n.reshape(1), g['damsm/w0_nocls'].reshape(1), TOL_DAMSM_LOSS)
+    _check('damsm/w1_nocls', w1n.reshape(1), g['damsm/w1_nocls'].reshape(1), TOL_DAMSM_LOSS)
+
+
+@pytest.mark.parametrize('n_img,n_txt,T,off', [(3, 7, 20, 2), (16, 16, 18, 0), (2, 5, 32, 3)])
+def test_words_block_rectangular(gpu, n_img, n_txt, T, off):
+    """The B_local x B_global block a data-parallel rank computes: rows for
+    n_img images against n_txt captions (lengths 1..T, > 16 words use both
+    word tiles), against the oracle's func_attention / cosine restatement at
+    realistic region scale; attention maps of the pairs (j, j + off); the
+    backward is deterministic (two runs bit-identical: no atomics)."""
+    from eegan_hip import functional as Fn
+    from oracle import eegan_oracle as O
+    torch.manual_seed(n_img * 100 + n_txt)
+    reg = torch.randn(n_img, 256, 17, 17) * 0.3
+    words = torch.randn(n_txt, 256, T).tanh()
+    lens = torch.randint(1, T + 1, (n_txt,))
+    lens[0] = T
+    lens[-1] = 1
+    dsim = torch.randn(n_img, n_txt)
+    # oracle: rows j (images) x columns i (captions)
+    rr = reg.clone().requires_grad_()
+    wr = words.clone().requires_grad_()
+    cols, maps = [], {}
+    for i in range(n_txt):
+        w = int(lens[i])
+        q = wr[i:i + 1, :, :w].expand(n_img, -1, -1)
+        wc, att = O.func_attention(q, rr, O.GAMMA1)
+        cos = O.cosine_similarity(q.transpose(1, 2).reshape(n_img * w, -1), wc.transpose(1, 2).reshape(n_img * w, -1))
+        cols.append(torch.log(torch.exp(cos.reshape(n_img, w) * O.GAMMA2).sum(1, keepdim=True)))
+        if 0 <= i - off < n_img:
+            maps[i - off] = att[i - off]
+    simr = torch.cat(cols, 1) * O.GAMMA3
+    (simr * dsim).sum().backward()
+    outs = []
+    for _ in range(2):
+        rd = reg.to(gpu).requires_grad_()
+        wd = words.to(gpu).requires_grad_()
+        sim, att = Fn.WordsSimFn.apply(rd, wd, lens.to(gpu), True, off)
+        (sim * dsim.to(gpu)).sum().backward()
+        outs.append((sim.detach().cpu(), att.cpu(), rd.grad.cpu(), wd.grad.cpu()))
+    sim, att, dreg, dwords = outs[0]
+    from _util import rel_l2
+    assert (sim - simr.detach()).abs().max() < 2e-3 * simr.detach().abs().max()
+    for j, m in maps.items():
+        w = int(lens[j + off])
+        assert rel_l2(att[j, :w].reshape(1, w, 17, 17), m.detach().reshape(1, w, 17, 17)) < 2e-3
+    assert rel_l2(dreg, rr.grad) < TOL_DAMSM_GRAD, rel_l2(dreg, rr.grad)
+    assert rel_l2(dwords, wr.grad) < TOL_DAMSM_GRAD, rel_l2(dwords, wr.grad)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
 
 
 def test_rnn_encoder(gpu):
@@ -509,16 +621,15 @@ def test_full_step(gpu):
 
 def test_step_graph_matches_eager(gpu):
     """The captured step graph (bench.py's execution mode) replays the eager
-    step bit for bit.  Only the DAMSM region/word gradients accumulate with
-    fp32 atomics (order-dependent last bits, which Adam with beta1=0 turns
-    into lr-sized steps on near-zero gradients), so DAMSM is weighted 0 here:
-    every other kernel is deterministic and the runs must agree exactly."""
+    step bit for bit, DAMSM included (sim_coe 0.05, the reference default):
+    every kernel of the step is deterministic -- the DAMSM region / word
+    gradients are fixed-order reductions (csrc/damsm.hip), no atomics."""
     import bench
     from eegan_hip.trainer import StepGraph
     from eegan_hip.synthetic import make_batch
     state = {}
     for mode in ('eager', 'graph'):
-        T, B, ncls = bench.build('T8', gpu, sim_coe=0.0)
+        T, B, ncls = bench.build('T8', gpu, sim_coe=0.05)
         batch = make_batch(B, gpu, seed=11, class_num=ncls, with_class=True)
         noise = seeded_tensor('graph:noise', (B, 100), 1).to(gpu)
         if mode == 'eager':
