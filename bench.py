@@ -147,7 +147,7 @@ def main():
     device = torch.device('cuda', local_rank)
     rank, world = D.init_from_env()
     T, B, ncls = build(args.config, device)
-    batch = make_batch(B, device, seed=3407 + rank, class_num=max(ncls, 1), with_class=True)
+    batch = make_batch(B, device, seed=3407 + rank, class_num=ncls, with_class=True, id_offset=rank * B)
 
     # the whole step, collectives included (own per-lane RCCL communicators,
     # eegan_hip.rccl), is one captured HIP graph on every rank

@@ -2,14 +2,17 @@
 reference data pipeline (datasets.py:192-445 via train.py:58-88), used by
 bench.py: images U(-1,1) at 64/128/256 (NHWC bf16), captions (B,20) int64
 tokens U[1,n_words) with lengths U[5,18] zero-padded, attributes (B,3,5) with
-lengths U[1,5], unpaired captions, class ids U[1,class_num]."""
+lengths U[1,5], unpaired captions, class ids U[1,class_num].  class_num 0
+(MS-COCO: no class_info.pickle, so every image is its own class --
+datasets.py:287-295 falls back to np.arange) gives distinct ids, offset by
+`id_offset` (rank * B on a data-parallel rank)."""
 import torch
 
 from . import functional as Fn
 
 
 def make_batch(B, device, seed=3407, n_words=5450, words_num=20, class_num=200, attr_num=3, attr_len=5,
-               sizes=(64, 128, 256), with_class=True):
+               sizes=(64, 128, 256), with_class=True, id_offset=0):
     g = torch.Generator(device='cpu')
     g.manual_seed(seed)
     imgs = []
@@ -30,5 +33,8 @@ def make_batch(B, device, seed=3407, n_words=5450, words_num=20, class_num=200, 
         'unpair_caps': un.to(device), 'unpair_cap_lens': un_lens.to(device),
     }
     if with_class:
-        batch['cls_ids'] = torch.randint(1, class_num + 1, (B,), generator=g).to(device)
+        if class_num > 0:
+            batch['cls_ids'] = torch.randint(1, class_num + 1, (B,), generator=g).to(device)
+        else:
+            batch['cls_ids'] = (torch.arange(B) + id_offset).to(device)
     return batch

@@ -56,12 +56,51 @@ def sync_bn(x, sd, p, affine=True, training=True, mode='single'):
     return y.reshape(x.shape)
 
 
+class _RoundBF16(torch.autograd.Function):
+    """Straight-through bf16 rounding of an activation (forward) and of the
+    gradient flowing back through it (backward)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+# bf16 SIMULATION switch (tests only): when True every conv input and output
+# -- the activations and data gradients the HIP path stores as bf16 -- is
+# rounded to bf16, so the fp32 oracle measures how far bf16 storage alone
+# moves a result from the reference (the basis of the deep-gradient gates in
+# tests/test_gpu_models.py).  Off by default: the oracle is the fp32 reference.
+SIM_BF16 = False
+
+
+def _r(x):
+    return _RoundBF16.apply(x) if SIM_BF16 else x
+
+
+# gain-gradient PROBE (tests only): when a dict, every residual gain
+# out = shortcut + gamma * h records (h, out) under its parameter prefix, so a
+# test can form the Cauchy-Schwarz scale ||d out|| * ||h|| that bounds how far
+# d gamma = <d out, h> moves when d out carries a relative error.
+PROBE = None
+
+
+def _probe(p, h, out):
+    if PROBE is not None:
+        if out.requires_grad:
+            out.retain_grad()
+        PROBE[p] = (h, out)
+
+
 def linear(x, sd, p, bias=True):
     return F.linear(x, sd[p + 'weight'], sd[p + 'bias'] if bias else None)
 
 
 def conv(x, sd, p, stride=1, pad=0, bias=False):
-    return F.conv2d(x, sd[p + 'weight'], sd.get(p + 'bias') if bias else None, stride, pad)
+    return _r(F.conv2d(_r(x), sd[p + 'weight'], sd.get(p + 'bias') if bias else None, stride, pad))
 
 
 # --------------------------------------------------------------------------
@@ -102,7 +141,8 @@ def sagb_block(sd, p, feat, conds, smask, learnable_sc, pred_mask, bn_mode='sing
     h = conv(h, sd, p + 'c1.', 1, 1)
     h = F.relu(affine_ssa(sd, p + 'affine2.', h, conds[1], smask, bn_mode))
     h = conv(h, sd, p + 'c2.', 1, 1)
-    out = sc + sd[p + 'gamma'] * h
+    out = _r(sc + sd[p + 'gamma'] * h)
+    _probe(p, h, out)
     m = mask_head(sd, p + 'conv_mask.', out, bn_mode) if pred_mask else None
     return out, m
 
@@ -112,7 +152,9 @@ def cum_block(sd, p, prev, cur):
     u = conv(prev, sd, p + 'up_block.0.')
     u = F.interpolate(u, scale_factor=2, mode='nearest')
     u = conv(u, sd, p + 'up_block.2.', 1, 1)
-    return conv(u + cur * sd[p + 'gamma'], sd, p + 'fuse_block.', 1, 1)
+    s = u + cur * sd[p + 'gamma']
+    _probe(p, cur, s)
+    return conv(s, sd, p + 'fuse_block.', 1, 1)
 
 
 def gen_channels(ngf):
@@ -126,7 +168,7 @@ def gen_forward(sd, z, sent, attrs, ngf, bn_mode='single', stages=3):
     stage-1 slice of config C1: up to img_64 only."""
     chans = gen_channels(ngf)
     B = z.shape[0]
-    out = linear(z, sd, 'fc.').view(B, 8 * ngf, 4, 4)
+    out = _r(linear(z, sd, 'fc.').view(B, 8 * ngf, 4, 4))
     m = mask_head(sd, 'init_mask.', out, bn_mode)
     out, m = sagb_block(sd, 'blocks.0.', out, (sent, sent), torch.sigmoid(m),
                         chans[0][0] != chans[0][1], chans[0][2], bn_mode)
@@ -573,9 +615,14 @@ def cnn_encoder(sd, x):
 
 
 def standin_image_encoder(sd, x):
-    """The small image encoder used by the golden full-step fixture in place
+    """The small image encoder used by the golden full-step fixtures in place
     of Inception-v3 (which needs torchvision): regions = conv15x15/s15 (3->256)
-    of the 256^2 image (17x17 grid); code = Linear(256,256)(mean of regions)."""
+    of the 256^2 image (17x17 grid); code = Linear(256,256)(mean of regions).
+    Smaller images (the stage-1 slice's img_64) are first resized to 256^2
+    (bilinear, align_corners=False -- as CNN_ENCODER resizes to 299,
+    DAMSM.py:173)."""
+    if x.shape[-1] != 256:
+        x = F.interpolate(x, size=(256, 256), mode='bilinear', align_corners=False)
     regions = F.conv2d(x, sd['standin.regions.weight'], None, 15)
     code = F.linear(regions.mean(dim=(2, 3)), sd['standin.code.weight'], sd['standin.code.bias'])
     return regions, code

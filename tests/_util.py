@@ -19,9 +19,14 @@ _GOLD = None
 
 
 def golden():
+    """Golden vectors captured from the reference (tests/golden/make_golden.py):
+    golden.npz (blocks, networks, losses, the round-1 step) and
+    golden_steps.npz (the C4 / non-32-width / stage-1 steps)."""
     global _GOLD
     if _GOLD is None:
-        _GOLD = dict(np.load(os.path.join(HERE, 'golden', 'golden.npz')))
+        _GOLD = {}
+        for f in ('golden.npz', 'golden_steps.npz'):
+            _GOLD.update(dict(np.load(os.path.join(HERE, 'golden', f))))
     return _GOLD
 
 

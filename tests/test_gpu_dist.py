@@ -1,0 +1,61 @@
+"""The drop-in boundary at N > 1 on one GPU box: two ranks (torchrun, gloo --
+RCCL refuses two ranks on one device) run the reference train.py's inner step
+(tests/dp_dropin_worker.py: torch.optim.Adam, nn.DataParallel-wrapped D and
+ATTR_Enhance, words_loss / sent_loss from miscc.DAMSM_losses, no explicit
+synchronisation call) on halves of one batch.  Checked: the ranks end the
+step with bit-identical parameters (gradient averaging by the models' own
+post-accumulate-grad hooks), and they match ONE process stepping the whole
+batch (the reference's DataParallel semantics: global-batch SyncBN
+statistics with the multi-device numerics, global DAMSM similarity matrices,
+means over the global batch) within bf16 rounding."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def test_dropin_train_step_two_ranks(gpu, tmp_path, monkeypatch):
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
+           os.path.join(HERE, 'dp_dropin_worker.py'), str(tmp_path)]
+    env = dict(os.environ, OMP_NUM_THREADS='2')
+    r = subprocess.run(cmd, env=env, timeout=240, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    ranks = [torch.load(os.path.join(tmp_path, 'rank%d.pt' % i)) for i in range(2)]
+    p0, p1 = ranks[0]['params'], ranks[1]['params']
+    assert set(p0) == set(p1)
+    for k in p0:   # averaged gradients -> identical Adam steps on every rank
+        assert torch.equal(p0[k], p1[k]), k
+    # DAMSM losses are global: the same value on both ranks
+    for k in ('s', 'w', 'a'):
+        assert ranks[0]['rec'][k] == ranks[1]['rec'][k], k
+
+    import dp_dropin_worker as W
+    from eegan_hip import functional as Fn
+    monkeypatch.setattr(Fn, 'SYNC_BN_FORCE_MULTI', True)   # the reference's multi-device BN numerics
+    rec, params = W.run_step(0, 1, gpu)
+    for k, v in rec.items():
+        got = 0.5 * (ranks[0]['rec'][k] + ranks[1]['rec'][k])   # per-rank means over equal halves
+        e = abs(got - v) / max(abs(v), 1e-3)
+        print('DP2 %-4s 2-rank %.6g  1-process %.6g  rel %.2e' % (k, got, v, e))
+        assert e < (0.08 if k.startswith('gp') else 3e-2), (k, got, v)
+    worst = 0.0
+    for k, v in params.items():
+        a, b = p0[k].double().reshape(-1), v.double().reshape(-1)
+        e = float((a - b).norm() / b.norm().clamp_min(1e-30))
+        worst = max(worst, e)
+        assert e < 2e-2, (k, e)
+    print('DP2 worst post-step parameter rel-L2 vs one process: %.3e' % worst)

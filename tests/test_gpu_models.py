@@ -25,14 +25,27 @@ TOL_BWD = 6e-2
 # gives: generator input grads 8-9% rel-L2, Inception-v3 input grads 29%; the
 # kernels here measure 9% and 30%.  Deep-gradient tolerances reflect that.
 TOL_DEEP = 0.15
-# Per-parameter generator gradients under the same simulation: median 8.8%,
-# worst 0.22 (blocks.0.conv_mask.1.bias, a 100-channel BN bias deep in the
-# mask head).  Each parameter is held to TOL_GEN_PARAM, the median to 0.12.
-TOL_GEN_PARAM = 0.3
-# entries whose reference value is ill-conditioned: attr_key.bias has an
-# identically-zero true gradient (softmax shift invariance); sagb_id's gamma
-# gradient is sum(dout*h) = -0.43 against sum|dout*h| = 193 (condition ~450).
-ILL_CONDITIONED = ('attr/grad/attr_key.bias', 'sagb_id/grad/gamma')
+# Deep per-parameter gradients (whole generator, discriminator under the
+# gradient penalty) are gated against their OWN bf16 simulation: the fp32
+# oracle with every conv input / output and its gradient rounded to bf16
+# (oracle.eegan_oracle.SIM_BF16) lands at sim_p from the reference; each
+# parameter p must stay within max(TOL_SIM_FLOOR, TOL_SIM_FACTOR * sim_p),
+# and the median over parameters of (GPU error / simulated error) within
+# TOL_SIM_MEDIAN.  Generator: median sim 8.8%; the GPU / sim ratio has median
+# 1.09 and worst 2.85 (a BN bias: a sum, one rounding realisation each).
+TOL_SIM_FACTOR = 4.0
+TOL_SIM_FLOOR = 0.06
+TOL_SIM_MEDIAN = 1.6
+# Residual gains (gamma, models.py:101,138,275): d gamma = <d out, h> over every
+# activation of the block, the TRUE value being 1e-4..2e-2 of the
+# Cauchy-Schwarz scale ||d out|| ||h|| (heavy cancellation).  A relative error
+# e of d out moves it by up to e ||d out|| ||h||, so the gate is
+# |got - ref| <= TOL_GAIN * ||d out|| ||h||  with the scale from the oracle
+# (oracle.eegan_oracle.PROBE): measured 4e-3 on the GPU, 1.5e-3 simulated.
+TOL_GAIN = 1e-2
+# attr_key.bias has an identically-zero true gradient (softmax shift
+# invariance): its gradient must vanish against the key weight's.
+ZERO_GRAD = ('attr/grad/attr_key.bias',)
 _LOG = []
 
 
@@ -68,25 +81,65 @@ def _load(mod, name, seed, dev):
     return mod.to(dev)
 
 
-def _grads(tag, mod, tol=TOL_BWD, skip=(), median_tol=None):
+def _oracle_grads(run, sim):
+    """Parameter gradients of an oracle forward/backward `run(O)` -> (grads
+    by key, gain scales ||d out|| ||h|| by gamma key); sim=True rounds every
+    conv input / output and gradient to bf16."""
+    from oracle import eegan_oracle as O
+    O.SIM_BF16, O.PROBE = sim, {}
+    try:
+        sd = run(O)
+        grads = {k: v.grad for k, v in sd.items() if v.grad is not None}
+        scales = {p + 'gamma': float(out.grad.norm() * h.norm()) for p, (h, out) in O.PROBE.items()
+                  if out.grad is not None}
+    finally:
+        O.SIM_BF16, O.PROBE = False, None
+    return grads, scales
+
+
+def _gain_check(key, got_t, ref, scale):
+    got = float(got_t.float().reshape(-1)[0])
+    ref = float(np.asarray(ref).reshape(-1)[0])
+    e = abs(got - ref) / scale
+    _LOG.append((key + ' (|err| / ||dout|| ||h||)', e))
+    print('PARITY %-50s |err|/(|dout||h|)=%.3e (tol %.0e; rel %.3e)' % (key, e, TOL_GAIN, abs(got - ref) / abs(ref)))
+    assert e <= TOL_GAIN, (key, e)
+
+
+def _grads(tag, mod, tol=TOL_BWD, skip=(), median_tol=None, sim=None, gains=None):
+    """Every parameter gradient of `mod` against golden `tag/grad/*`.  sim:
+    {key: bf16-simulated rel error} -> per-parameter gates (TOL_SIM_*);
+    gains: {gamma key: Cauchy-Schwarz scale} -> the TOL_GAIN gate."""
     g = golden()
     n = 0
     errs = []
     for k, p in mod.named_parameters():
         key = tag + '/grad/' + k
-        if key in g and not any(s in k for s in skip):
-            assert p.grad is not None, key
-            if key in ILL_CONDITIONED or (tol >= TOL_DEEP and p.numel() == 1):
-                # scalar residual gains: d gamma = sum(dout * h) over every activation of the
-                # block -- a cancellation-prone dot product (see ILL_CONDITIONED); reported only
-                e = _rel_fp(p.grad, g[key])
-                print('PARITY %-50s rel_l2=%.3e (scalar reduction, reported only)' % (key, e))
-                continue
-            errs.append(_check(key, p.grad, g[key], tol))
-            n += 1
+        if key not in g or any(s in k for s in skip):
+            continue
+        assert p.grad is not None, key
+        if key in ZERO_GRAD:
+            ref_w = mod.get_parameter(k.replace('.bias', '.weight')).grad
+            z = float(p.grad.norm() / ref_w.norm())
+            _LOG.append((key + ' (||g|| / ||g_weight||)', z))
+            print('PARITY %-50s ||g||/||g_w||=%.3e (true value 0)' % (key, z))
+            assert z < 1e-4, (key, z)
+            continue
+        if gains is not None and k in gains:
+            _gain_check(key, p.grad, g[key], gains[k])
+            continue
+        t = tol if sim is None else max(TOL_SIM_FLOOR, TOL_SIM_FACTOR * sim[k])
+        e = _check(key, p.grad, g[key], t)
+        errs.append(e if sim is None else e / max(sim[k], 1e-12))
+        n += 1
     assert n > 0
     if median_tol is not None:
         assert float(np.median(errs)) <= median_tol, (tag, float(np.median(errs)))
+    if sim is not None:
+        med = float(np.median(errs))
+        _LOG.append((tag + ' (median GPU / bf16-simulated error)', med))
+        print('PARITY %-50s median GPU/sim error ratio %.3f (tol %.1f)' % (tag, med, TOL_SIM_MEDIAN))
+        assert med <= TOL_SIM_MEDIAN, (tag, med)
 
 
 @pytest.mark.parametrize('tag,cin,cout,pm,res', [('sagb_sc', 16, 8, True, 8), ('sagb_id', 16, 16, True, 4),
@@ -109,7 +162,22 @@ def test_sagb_block(gpu, tag, cin, cout, pm, res):
     loss.backward()
     for nm, t in [('feat', feat), ('c0', c0), ('c1', c1), ('m', sm)]:
         _check(tag + '/d' + nm, t.grad, g[tag + '/dinput/' + nm], TOL_BWD)
-    _grads(tag, blk)
+
+    def run(O):
+        sd = golden_state(tag, 11)
+        for k, v in sd.items():
+            if v.is_floating_point() and 'running' not in k:
+                v.requires_grad_(True)
+        inp = [seeded_tensor(tag + ':feat', (B, cin, res, res), 1), seeded_tensor(tag + ':c0', (B, 256), 1),
+               seeded_tensor(tag + ':c1', (B, 256), 1), torch.sigmoid(seeded_tensor(tag + ':m', (B, 1, res, res), 1))]
+        o, mo = O.sagb_block(sd, '', inp[0], (inp[1], inp[2]), inp[3], cin != cout, pm)
+        lo = (o * seeded_tensor(tag + ':r', o.shape, 2)).sum()
+        if pm:
+            lo = lo + (mo * seeded_tensor(tag + ':rm', mo.shape, 2)).sum()
+        lo.backward()
+        return sd
+
+    _grads(tag, blk, gains=_oracle_grads(run, False)[1])
     for k, v in blk.state_dict().items():
         if 'running' in k:
             _check(tag + '/' + k, v, g[tag + '/after/' + k], 1e-2)
@@ -249,7 +317,20 @@ def test_generator(gpu):
     loss.backward()
     _check('gen/ds', s.grad, g['gen/dinput/s'], TOL_DEEP)
     _check('gen/da', a.grad, g['gen/dinput/a'], TOL_DEEP)
-    _grads('gen', G, TOL_GEN_PARAM, median_tol=0.12)
+    def run(O):
+        sd = golden_state('gen', 21)
+        for k, v in sd.items():
+            if v.is_floating_point() and 'running' not in k:
+                v.requires_grad_(True)
+        so, ao = seeded_tensor('g:s', (2, 256), 1), seeded_tensor('g:a', (2, 256), 1)
+        ims = O.gen_forward(sd, seeded_tensor('g:z', (2, 100), 1), so, ao, 8)
+        sum((im * seeded_tensor('g:r%d' % k, im.shape, 2)).sum() for k, im in enumerate(ims)).backward()
+        return sd
+
+    _, gains = _oracle_grads(run, False)
+    sim_grads, _ = _oracle_grads(run, True)
+    sim = {k: _rel_fp(v, g['gen/grad/' + k]) for k, v in sim_grads.items() if 'gen/grad/' + k in g}
+    _grads('gen', G, sim=sim, gains=gains)
     for k, v in G.state_dict().items():
         if 'running' in k:
             _check('gen/' + k, v, g['gen/after/' + k], 2e-2)
@@ -542,22 +623,59 @@ def test_cnn_encoder_stages(gpu):
     assert not bad, bad
 
 
-def test_full_step(gpu):
-    """train.py:186-206 on the GPU vs the golden d_update+g_update (W=8, B=4,
-    stand-in image encoder): losses and every post-Adam parameter."""
-    import models
-    from eegan_hip.trainer import Trainer
+# Full-step loss gates.  Losses evaluated before any parameter moved (the D
+# hinge / class terms, the DAMSM losses) within TOL_STEP_LOSS (measured
+# <= 1.4%).  The gradient penalty (after D's first Adam step) and the G hinge
+# terms errG/G_i (after D's two steps) read a discriminator that Adam's first
+# steps moved by ~lr * sign(grad) per weight WHATEVER the gradient's size, so
+# the ~2% of weights whose gradient is within bf16 noise of zero can step the
+# other way, and that step is a large part of those quantities (the update
+# moves the penalty by 4-73% on these fixtures).  They are gated in units of
+# the update's own effect U = ref - (the quantity at D's initial weights,
+# fp32 oracle): |got - ref| <= TOL_STEP_LOSS |ref| + TOL_STEP_UPDATE |U|
+# (measured up to 0.34 |U| on the GPU, 0.13 |U| in the bf16 simulation).
+TOL_STEP_LOSS = 3e-2
+TOL_STEP_UPDATE = 0.5
+# Adam's first steps move each weight by ~lr * sign(grad), so post-step
+# weights are compared by the direction of the move where the reference moved
+# by > lr/2: measured sign agreement 0.980, gated at TOL_STEP_SIGN.
+TOL_STEP_SIGN = 0.95
+
+
+def _pre_update_values(tag, B, W, ncls, disc_class, stages, sb):
+    """fp32 oracle values of the post-update losses at D's INITIAL weights:
+    {'errG/G_i_fake_sent': ..., 'errD_i/d_loss_gp': ...}."""
+    from oracle import eegan_oracle as O
+    nd = 3 if stages == 3 else 1
+    sd_g, sd_a = golden_state(tag + '_g', sb), golden_state(tag + '_a', sb + 1)
+    sd_ds = [golden_state(tag + '_d%d' % i, sb + 2 + i) for i in range(nd)]
+    nets = O.OracleNets(sd_g, sd_a, sd_ds, W, W, disc_class, ncls)
+    batch = synthetic_batch(B, seed=7, class_num=ncls, sizes=(64, 128, 256))
+    sent = seeded_tensor(tag + ':sent', (B, 256), 1)
+    attrs = seeded_tensor(tag + ':attrs', (B, 3, 256), 1)
+    _, att = O.attr_enhance(sd_a, sent, attrs)
+    fakes = O.gen_forward(sd_g, batch['noise'], sent, O.attr_merge(att), W, 'single', stages)
+    out = {}
+    for i in range(nd):
+        with torch.no_grad():
+            o = nets.d_cond(i, nets.d_feat(i, fakes[i]), sent)
+        out['errG/G_%d_fake_sent' % i] = -float((o[0] if (disc_class and i == 2) else o).mean())
+        xi, si = batch['imgs'][i].clone().requires_grad_(), sent.clone().requires_grad_()
+        o = nets.d_cond(i, nets.d_feat(i, xi), si)
+        o = o[0] if (disc_class and i == 2) else o
+        gx, gs = torch.autograd.grad(o, (xi, si), torch.ones_like(o))
+        out['errD_%d/d_loss_gp' % i] = float(O.gradient_penalty(gx, gs))
+    return out
+
+
+# tag: (batch, GF = DF, class count, USE_CLASS, stages, seed base) -- tests/golden/make_golden.py STEP_CASES
+STEP_CASES = {'step': (4, 8, 10, True, 3, 50), 'stepnc': (4, 8, 10, False, 3, 110),
+              'step12': (2, 12, 10, True, 3, 80), 'step1': (4, 8, 10, True, 1, 90)}
+
+
+def _standin_encoder(sd_enc, gpu):
     from eegan_hip import functional as Fn
     from eegan_hip.nn import Conv2d, Linear
-    from sync_batchnorm import DataParallelWithCallback
-    from oracle.eegan_oracle import STANDIN_SPEC
-    g = golden()
-    B, W, ncls = 4, 8, 10
-    G = _load(models.Gen(W, 100), 'step_g', 50, gpu)
-    A = _load(models.ATTR_Enhance(), 'step_a', 51, gpu)
-    Ds = [_load(models.Dis64(W), 'step_d0', 52, gpu), _load(models.Dis128(W), 'step_d1', 53, gpu),
-          _load(models.Dis256(W, True, ncls), 'step_d2', 54, gpu)]
-    sd_enc = seeded_state(STANDIN_SPEC, 60)
     rconv = Conv2d(3, 256, 15, 15, 0, bias=False).to(gpu)
     rconv.weight.data.copy_(sd_enc['standin.regions.weight'].to(gpu))
     rconv.weight.requires_grad_(False)
@@ -568,42 +686,84 @@ def test_full_step(gpu):
         p.requires_grad_(False)
 
     def standin(x):
+        if x.shape[-1] != 256:   # the stage-1 slice's img_64 (oracle.standin_image_encoder)
+            x = Fn.BilinearFn.apply(x, 256, 256)
         r = rconv(x, out_f32=True)
         return r, clin(Fn.GlobalAvgPoolFn.apply(Fn.CastF32Bf16Fn.apply(r)))
+    return standin
 
+
+@pytest.mark.parametrize('tag', sorted(STEP_CASES))
+def test_full_step(gpu, tag):
+    """train.py:186-206 on the GPU vs the golden d_update + g_update captured
+    from the reference (stand-in image encoder): losses and every post-Adam
+    parameter.  'step': CUB-like W=8 step; 'stepnc': config C4's discriminator
+    (Dis256 with the DiscSent head, USE_CLASS=False); 'step12': W=12, whose
+    channel counts (12..192) are not multiples of 32 -- the padded-K paths
+    config C3's W=48 takes; 'step1': config C1's stage-1 slice (Gen.stages=1,
+    Dis64 only, DAMSM on img_64)."""
+    import models
+    from eegan_hip.trainer import Trainer
+    from eegan_hip import functional as Fn
+    from sync_batchnorm import DataParallelWithCallback
+    from oracle.eegan_oracle import STANDIN_SPEC
+    g = golden()
+    B, W, ncls, disc_class, stages, sb = STEP_CASES[tag]
+    nd = 3 if stages == 3 else 1
+    G = _load(models.Gen(W, 100), tag + '_g', sb, gpu)
+    G.stages = stages
+    A = _load(models.ATTR_Enhance(), tag + '_a', sb + 1, gpu)
+    makers = [lambda: models.Dis64(W), lambda: models.Dis128(W), lambda: models.Dis256(W, disc_class, ncls)]
+    Ds = [_load(makers[i](), tag + '_d%d' % i, sb + 2 + i, gpu) for i in range(nd)]
+    standin = _standin_encoder(seeded_state(STANDIN_SPEC, sb + 10), gpu)
     T = Trainer(DataParallelWithCallback(G), DataParallelWithCallback(A), [DataParallelWithCallback(d) for d in Ds],
-                standin, None, B, disc_class=True, class_nums=ncls, class_coe=10.0, sim_coe=0.05, device=gpu)
+                standin, None, B, disc_class=disc_class, class_nums=ncls, class_coe=10.0, sim_coe=0.05, device=gpu)
     batch = synthetic_batch(B, seed=7, class_num=ncls, sizes=(64, 128, 256))
-    dbatch = {'imgs': [Fn.ImageToNhwcFn.apply(t.to(gpu)) for t in batch['imgs']],
+    dbatch = {'imgs': [Fn.ImageToNhwcFn.apply(t.to(gpu)) for t in batch['imgs'][:nd]],
               'cls_ids': batch['cls_ids'].to(gpu), 'cap_lens': batch['cap_lens'].to(gpu)}
-    words = seeded_tensor('step:words', (B, 256, 18), 1).to(gpu)
-    sent = seeded_tensor('step:sent', (B, 256), 1).to(gpu)
-    attrs = seeded_tensor('step:attrs', (B, 3, 256), 1).to(gpu)
-    unpair = seeded_tensor('step:unpair', (B, 256), 1).to(gpu)
+    words = seeded_tensor(tag + ':words', (B, 256, 18), 1).to(gpu)
+    sent = seeded_tensor(tag + ':sent', (B, 256), 1).to(gpu)
+    attrs = seeded_tensor(tag + ':attrs', (B, 3, 256), 1).to(gpu)
+    unpair = seeded_tensor(tag + ':unpair', (B, 256), 1).to(gpu)
     fakes, _ = T.train_step(dbatch, noise=batch['noise'].to(gpu), emb=(words, sent, attrs, unpair), iter_rec=True)
+    assert len(fakes) == nd
     for k, f in enumerate(fakes):
-        _check('step/fake%d' % k, f, g['step/fake%d' % k], TOL_FWD)
-    names = json.loads(g['step/scalars/names'].tobytes().decode())
-    vals = dict(zip(names, g['step/scalars/values']))
+        _check('%s/fake%d' % (tag, k), f, g['%s/fake%d' % (tag, k)], TOL_FWD)
+    names = json.loads(g[tag + '/scalars/names'].tobytes().decode())
+    vals = dict(zip(names, g[tag + '/scalars/values']))
+    assert set(T.records) == set(vals), (sorted(T.records), sorted(vals))
+    pre = _pre_update_values(tag, B, W, ncls, disc_class, stages, sb)
     for k, v in T.records.items():
         ref = vals[k]
-        e = abs(v.item() - ref) / max(abs(ref), 1e-3)
-        print('PARITY step/%-40s got=%.6g ref=%.6g rel=%.3e' % (k, v.item(), ref, e))
-        _LOG.append(('step/' + k, e))
-        assert e < (0.15 if 'gp' in k else 5e-2), (k, v.item(), ref)
+        err = abs(v.item() - ref)
+        if k in pre:   # read a discriminator that Adam already moved
+            U = ref - pre[k]
+            e = err / max(abs(U), 1e-12)
+            ok = err <= TOL_STEP_LOSS * abs(ref) + TOL_STEP_UPDATE * abs(U)
+            print('PARITY %s/%-40s got=%.6g ref=%.6g |err|/|U|=%.3e (U=%.4g)' % (tag, k, v.item(), ref, e, U))
+        else:
+            e = err / max(abs(ref), 1e-3)
+            ok = e < TOL_STEP_LOSS
+            print('PARITY %s/%-40s got=%.6g ref=%.6g rel=%.3e' % (tag, k, v.item(), ref, e))
+        _LOG.append(('%s/%s' % (tag, k), e))
+        if os.environ.get('EEGAN_PARITY_SOFT') != '1':   # diagnostics: report every entry, then fail
+            assert ok, (k, v.item(), ref)
     # post-Adam parameters: the update is ~lr*sign(g), so compare the parameter
     # CHANGE direction where the reference moved it
     worst = 0.0
     agree = tot = 0
-    for nm, mod in [('g', G), ('a', A), ('d0', Ds[0]), ('d1', Ds[1]), ('d2', Ds[2])]:
-        init = golden_state({'g': 'step_g', 'a': 'step_a', 'd0': 'step_d0', 'd1': 'step_d1', 'd2': 'step_d2'}[nm],
-                            {'g': 50, 'a': 51, 'd0': 52, 'd1': 53, 'd2': 54}[nm])
+    mods = [('g', G, sb), ('a', A, sb + 1)] + [('d%d' % i, d, sb + 2 + i) for i, d in enumerate(Ds)]
+    for nm, mod, seed in mods:
+        init = golden_state('%s_%s' % (tag, nm), seed)
         lr = 1e-4 if nm in ('g', 'a') else 4e-4
         for k, v in mod.state_dict().items():
-            ref = np.asarray(g['step/after_%s/%s' % (nm, k)], np.float64).reshape(-1)
+            ref = np.asarray(g['%s/after_%s/%s' % (tag, nm, k)], np.float64).reshape(-1)
             e = _rel_fp(v, ref)
             worst = max(worst, e)
-            assert e < 2e-2, (nm, k, e)
+            if os.environ.get('EEGAN_PARITY_SOFT') == '1':
+                print('PARAM %s/%s/%s rel %.3e' % (tag, nm, k, e))
+            else:
+                assert e < 2e-2, (nm, k, e)
             if 'running' in k or 'num_batches' in k:
                 continue
             got = np.asarray(fp(v.float().cpu()), np.float64).reshape(-1)
@@ -614,9 +774,40 @@ def test_full_step(gpu):
             agree += int((np.sign(dref[sel]) == np.sign(dgot[sel])).sum())
             tot += int(sel.sum())
     frac = agree / max(tot, 1)
-    print('PARITY step/params worst rel_l2 %.3e; Adam-update sign agreement %.4f over %d entries' % (worst, frac, tot))
-    _LOG.append(('step/update_sign_agreement', frac))
-    assert frac > 0.8
+    print('PARITY %s/params worst rel_l2 %.3e; Adam-update sign agreement %.4f over %d entries'
+          % (tag, worst, frac, tot))
+    _LOG.append(('%s/update_sign_agreement' % tag, frac))
+    assert frac > TOL_STEP_SIGN
+
+
+def _graph_vs_eager(gpu, cfg, n_eager, sim_coe=0.05):
+    import bench
+    from eegan_hip.trainer import StepGraph
+    from eegan_hip.synthetic import make_batch
+    state, fakes = {}, {}
+    for mode in ('eager', 'graph'):
+        T, B, ncls = bench.build(cfg, gpu, sim_coe=sim_coe)
+        batch = make_batch(B, gpu, seed=11, class_num=ncls, with_class=True)
+        noise = seeded_tensor('graph:noise', (B, 100), 1).to(gpu)
+        if mode == 'eager':
+            for _ in range(n_eager):
+                out, _ = T.train_step(batch, noise=noise)
+        else:
+            sg = StepGraph(T, batch, warmup=1, noise=noise)
+            for _ in range(n_eager - 1):
+                out, _ = sg.replay()
+        torch.cuda.synchronize()
+        fakes[mode] = [f.float().cpu() for f in out]
+        state[mode] = torch.cat([o.flat for o in [T.optimizerG] + list(T.optimizerDs)] +
+                                [o.v for o in [T.optimizerG] + list(T.optimizerDs)])
+        del T
+        torch.cuda.empty_cache()
+    d = (state['graph'] - state['eager']).abs()
+    print('STEPGRAPH %s max |graph - eager| over params and Adam moments: %.3e' % (cfg, float(d.max())))
+    assert torch.isfinite(state['eager']).all()
+    for f in fakes['eager']:
+        assert torch.isfinite(f).all() and f.abs().max() <= 1.0   # tanh images
+    return state, fakes
 
 
 def test_step_graph_matches_eager(gpu):
@@ -646,3 +837,18 @@ def test_step_graph_matches_eager(gpu):
     d = (state['graph'] - state['eager']).abs()
     print('STEPGRAPH max |graph - eager| over params and Adam moments: %.3e' % float(d.max()))
     assert torch.equal(state['graph'], state['eager'])
+
+
+@pytest.mark.parametrize('cfg', ['C3', 'C4'])
+def test_config_step_graph_matches_eager(gpu, cfg):
+    """Full-size steps of the configs the bench line does not time: C3
+    (Oxford-102 Flowers, GF=DF=48 -> 48/96/192/384/768 channels on the padded-K
+    conv paths, batch 32, 102 classes) and C4's per-GPU shard (MS-COCO,
+    GF=DF=64, batch 8, USE_CLASS=False: Dis256 with the DiscSent head).  Size-
+    independent properties (the golden fixtures pin the arithmetic at small
+    width): finite parameters / moments, images in [-1, 1], and the captured
+    step graph equal to the eager step bit for bit."""
+    state, fakes = _graph_vs_eager(gpu, cfg, 2)
+    assert torch.equal(state['graph'], state['eager'])
+    for a, b in zip(fakes['graph'], fakes['eager']):
+        assert torch.equal(a, b)

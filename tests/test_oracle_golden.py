@@ -262,29 +262,40 @@ def test_rnn_encoder():
     assert_close_fp('sent', fp(s), g['rnn/sent'], 1e-4, 1e-6)
 
 
-def test_full_step():
-    """One d_update + g_update (train.py:437-502) at W=8, B=4 with the
-    stand-in image encoder: every post-Adam parameter and every logged loss."""
+# tag: (batch, GF = DF, class count, USE_CLASS, stages, seed base) -- tests/golden/make_golden.py STEP_CASES
+STEP_CASES = {'step': (4, 8, 10, True, 3, 50), 'stepnc': (4, 8, 10, False, 3, 110),
+              'step12': (2, 12, 10, True, 3, 80), 'step1': (4, 8, 10, True, 1, 90)}
+
+
+@pytest.mark.parametrize('tag', sorted(STEP_CASES))
+def test_full_step(tag):
+    """One d_update + g_update (train.py:437-502) with the stand-in image
+    encoder: every post-Adam parameter and every logged loss.  'step' is the
+    CUB-like W=8 step, 'stepnc' config C4's no-class-head discriminator,
+    'step12' a width whose channel counts are not multiples of 32, 'step1'
+    config C1's stage-1 slice."""
     g = golden()
     from oracle.eegan_oracle import STANDIN_SPEC
-    B, W, ncls = 4, 8, 10
-    sd_g = golden_state('step_g', 50)
-    sd_a = golden_state('step_a', 51)
-    sd_ds = [golden_state('step_d%d' % i, 52 + i) for i in range(3)]
-    nets = O.OracleNets(sd_g, sd_a, sd_ds, W, W, True, ncls)
+    B, W, ncls, disc_class, stages, sb = STEP_CASES[tag]
+    nd = 3 if stages == 3 else 1
+    sd_g = golden_state(tag + '_g', sb)
+    sd_a = golden_state(tag + '_a', sb + 1)
+    sd_ds = [golden_state(tag + '_d%d' % i, sb + 2 + i) for i in range(nd)]
+    nets = O.OracleNets(sd_g, sd_a, sd_ds, W, W, disc_class, ncls)
     og, ods = O.make_adams(nets)
-    sd_enc = seeded_state(STANDIN_SPEC, 60)
+    sd_enc = seeded_state(STANDIN_SPEC, sb + 10)
     batch = synthetic_batch(B, seed=7, class_num=ncls, sizes=(64, 128, 256))
-    words = seeded_tensor('step:words', (B, 256, 18), 1)
-    sent = seeded_tensor('step:sent', (B, 256), 1)
-    attrs = seeded_tensor('step:attrs', (B, 3, 256), 1)
-    unpair = seeded_tensor('step:unpair', (B, 256), 1)
+    words = seeded_tensor(tag + ':words', (B, 256, 18), 1)
+    sent = seeded_tensor(tag + ':sent', (B, 256), 1)
+    attrs = seeded_tensor(tag + ':attrs', (B, 3, 256), 1)
+    unpair = seeded_tensor(tag + ':unpair', (B, 256), 1)
     fakes, drec, grec = O.train_step(nets, og, ods, batch, (words, sent, attrs, unpair),
-                                     lambda x: O.standin_image_encoder(sd_enc, x), 10.0, 0.05)
+                                     lambda x: O.standin_image_encoder(sd_enc, x), 10.0, 0.05, stages=stages)
+    assert len(fakes) == nd
     for k, f in enumerate(fakes):
-        assert_close_fp('fake%d' % k, fp(f), g['step/fake%d' % k], 5e-4, 5e-5)
-    names = json.loads(g['step/scalars/names'].tobytes().decode())
-    vals = dict(zip(names, g['step/scalars/values']))
+        assert_close_fp('fake%d' % k, fp(f), g[tag + '/fake%d' % k], 5e-4, 5e-5)
+    names = json.loads(g[tag + '/scalars/names'].tobytes().decode())
+    vals = dict(zip(names, g[tag + '/scalars/values']))
     for i, (_, gp) in enumerate(drec):
         assert np.isclose(gp.item(), vals['errD_%d/d_loss_gp' % i], rtol=2e-3), i
     _, errs, damsm = grec
@@ -293,8 +304,9 @@ def test_full_step():
     assert np.isclose(damsm[0].item(), vals['errG/w_loss'], rtol=1e-4)
     assert np.isclose(damsm[1].item(), vals['errG/s_loss'], rtol=1e-4)
     assert np.isclose(damsm[2].item(), vals['errG/a_loss'], rtol=1e-4)
+    assert ('errD_2/real_class' in vals) == (disc_class and nd == 3)
     # post-Adam parameters: Adam's first step moves each weight by ~lr*sign(g),
     # so the post-step weights are compared at lr-scale tolerance
-    for nm, sd in [('g', sd_g), ('a', sd_a), ('d0', sd_ds[0]), ('d1', sd_ds[1]), ('d2', sd_ds[2])]:
+    for nm, sd in [('g', sd_g), ('a', sd_a)] + [('d%d' % i, d) for i, d in enumerate(sd_ds)]:
         for k, v in sd.items():
-            assert_close_fp(nm + ':' + k, fp(v), g['step/after_%s/%s' % (nm, k)], 1e-4, 2e-5)
+            assert_close_fp(nm + ':' + k, fp(v), g[tag + '/after_%s/%s' % (nm, k)], 1e-4, 2e-5)
