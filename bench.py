@@ -37,6 +37,9 @@ CONFIGS = {
     'C5': ('CUB-200', 32, 32, 200),
     'T8': ('CUB-200 (test size)', 8, 4, 10),   # parity tests only, not a bench line
 }
+# whole-step ceilings per GPU (BASELINE.md roofline table: algorithmic FLOPs /
+# bf16 conv-path bytes per image over 2.5 PFLOP/s and 8 TB/s): (MFMA, HBM) img/s
+CEILINGS = {'C2': (8300.0, 6300.0), 'C3': (3760.0, 4300.0), 'C4': (2140.0, 2520.0), 'C5': (8300.0, 6500.0)}
 MFMA_PEAK_TFLOPS = 2500.0   # dense bf16 (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 
@@ -71,56 +74,88 @@ def build(cfg_name, device, sim_coe=0.05):
     return T, B, ncls
 
 
-def pmc_traffic(kind):
-    """HBM bytes per launch of kernel family `kind` from the newest committed
-    rocprofv3 PMC summary (profiles/rNN_families.json, written by
-    tools/rocprof_families.py: FETCH_SIZE x2 (gfx950 wide-read correction) +
-    WRITE_SIZE, separate counter passes)."""
+def pmc_family(kind):
+    """PMC figures of kernel family `kind` from the newest committed rocprofv3
+    summary (profiles/rNN_families.json, written by tools/rocprof_families.py,
+    one counter pass each): HBM bytes per launch (FETCH_SIZE x2 -- the gfx950
+    wide-read correction -- + WRITE_SIZE) and the MFMA-busy fraction
+    (SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE x SIMDs)."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_families.json')))
     if not files:
-        return None, None
+        return {}, None
     with open(files[-1]) as f:
         fam = json.load(f).get('families', {}).get(kind, {})
-    return fam.get('hbm_bytes_per_call'), 'profiles/' + os.path.basename(files[-1])
+    return fam, 'profiles/' + os.path.basename(files[-1])
 
 
-def cpu_baseline(seconds_budget=20.0):
-    """Time the CPU oracle's full step (oracle.eegan_oracle.train_step incl.
-    the Inception-v3 encoder restatement) at B=4, W=32 (BASELINE.md CPU plan)."""
+def _cpu_model():
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
+def cpu_baseline(seconds_budget=30.0):
+    """The CPU oracle (oracle.eegan_oracle, the PyTorch-CPU restatement of the
+    reference step, pinned to golden vectors captured from the reference)
+    timed on the host: BASELINE.md's CPU plan -- W=32, B=4, the five frozen
+    text-encoder calls (train.py:169-184) inside the step, the full 3-stage
+    step (incl. the Inception-v3 restatement) and the C1 stage-1 slice,
+    median of up to 10 steps after 2 warm-ups, threads = all affinity cores."""
     from oracle import eegan_oracle as O
-    from oracle.seeding import seeded_state, synthetic_batch, seeded_tensor
+    from oracle.seeding import seeded_state, synthetic_batch
     import models
     import DAMSM
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    torch.set_num_threads(threads)
+    affinity = len(os.sched_getaffinity(0))
+    torch.set_num_threads(affinity)
     B, W, ncls = 4, 32, 200
     spec = lambda m: [(k, tuple(v.shape)) for k, v in m.state_dict().items()]  # noqa: E731
-    sd_g = seeded_state(spec(models.Gen(W, 100)), 1)
-    sd_a = seeded_state(spec(models.ATTR_Enhance()), 2)
-    sd_ds = [seeded_state(spec(m), 3 + i) for i, m in enumerate([models.Dis64(W), models.Dis128(W),
-                                                                  models.Dis256(W, True, ncls)])]
     sd_e = seeded_state(spec(DAMSM.CNN_ENCODER(256)), 9)
-    nets = O.OracleNets(sd_g, sd_a, sd_ds, W, W, True, ncls)
-    og, ods = O.make_adams(nets)
+    sd_t = seeded_state(spec(DAMSM.RNN_ENCODER(5450, nhidden=256)), 10)
     batch = synthetic_batch(B, seed=5, class_num=ncls)
-    emb = (seeded_tensor('w', (B, 256, 18)), seeded_tensor('s', (B, 256)), seeded_tensor('a', (B, 3, 256)),
-           seeded_tensor('u', (B, 256)))
     enc = lambda x: O.cnn_encoder(sd_e, x)  # noqa: E731
-    O.train_step(nets, og, ods, batch, emb, enc)  # warm-up
-    times = []
-    t_end = time.time() + seconds_budget
-    while time.time() < t_end or len(times) < 2:
-        t0 = time.time()
-        O.train_step(nets, og, ods, batch, emb, enc)
-        times.append(time.time() - t0)
-        if len(times) >= 10:
-            break
-    times.sort()
-    med = times[len(times) // 2]
-    return {'value': B / med, 'unit': 'images/sec', 'cores': threads, 'kind': 'port',
-            'sample': 'oracle train_step (full 3-stage, W=32, B=4, Inception-v3 restatement), median of %d steps '
-                      'after 1 warm-up, %d threads' % (len(times), threads)}
+
+    def encode_text():
+        with torch.no_grad():
+            words, sent = O.rnn_encoder(sd_t, batch['caps'], batch['cap_lens'])
+            attrs = torch.stack([O.rnn_encoder(sd_t, batch['attrs'][:, i], batch['attrs_len'][:, i])[1]
+                                 for i in range(3)], 1)
+            _, unpair = O.rnn_encoder(sd_t, batch['unpair_caps'], batch['unpair_cap_lens'])
+        return words, sent, attrs, unpair
+
+    def timed(stages, budget):
+        sd_g = seeded_state(spec(models.Gen(W, 100)), 1)
+        sd_a = seeded_state(spec(models.ATTR_Enhance()), 2)
+        nd = 3 if stages == 3 else 1
+        sd_ds = [seeded_state(spec(m), 3 + i) for i, m in enumerate([models.Dis64(W), models.Dis128(W),
+                                                                      models.Dis256(W, True, ncls)][:nd])]
+        nets = O.OracleNets(sd_g, sd_a, sd_ds, W, W, True, ncls)
+        og, ods = O.make_adams(nets)
+        for _ in range(2):  # warm-ups
+            O.train_step(nets, og, ods, batch, encode_text(), enc, stages=stages)
+        times = []
+        t_end = time.time() + budget
+        while len(times) < 10 and (time.time() < t_end or len(times) < 3):
+            t0 = time.time()
+            O.train_step(nets, og, ods, batch, encode_text(), enc, stages=stages)
+            times.append(time.time() - t0)
+        times.sort()
+        return B / times[len(times) // 2], len(times)
+
+    full, n_full = timed(3, seconds_budget)
+    c1, n_c1 = timed(1, 0.25 * seconds_budget)
+    return {'value': full, 'unit': 'images/sec', 'cores': torch.get_num_threads(), 'kind': 'port',
+            'affinity_cores': affinity, 'cpu_model': _cpu_model(),
+            'sample': 'oracle train_step (full 3-stage, W=32, B=4: 5 text-encoder calls, G, 3 x d_update incl. '
+                      'the gradient penalty, g_update incl. the Inception-v3 restatement), median of %d steps after '
+                      '2 warm-ups' % n_full,
+            'c1_stage1': {'value': c1, 'unit': 'images/sec', 'sample': 'C1 stage-1 slice (img_64, Dis64, DAMSM on '
+                                                                       'img_64), B=4, median of %d steps' % n_c1}}
 
 
 def main():
@@ -130,7 +165,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--config', default='C2', choices=sorted(CONFIGS))
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-seconds', type=float, default=20.0)
+    ap.add_argument('--cpu-seconds', type=float, default=30.0)
     ap.add_argument('--no-timer', action='store_true', help='diagnostic: skip the roofline timing pass')
     ap.add_argument('--timing-steps', type=int, default=2, help='eager steps of the roofline timing pass')
     ap.add_argument('--graph', default='auto', choices=['auto', 'on', 'off'],
@@ -216,7 +251,8 @@ def main():
     dom = max(((k, v) for k, v in kern.items() if k.startswith('conv')), key=lambda kv: kv[1][3])
     kind, (n, fl, nb, tsec) = dom
     achieved = fl / tsec / 1e12
-    traffic, traffic_src = pmc_traffic(kind)
+    pf, traffic_src = pmc_family(kind)
+    traffic = pf.get('hbm_bytes_per_call')
     roof = {'kernel': kind, 'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': MFMA_PEAK_TFLOPS,
             'unit': 'TFLOP/s', 'frac': round(achieved / MFMA_PEAK_TFLOPS, 4), 'traffic': traffic,
             'traffic_unit': 'HBM bytes per launch (rocprofv3 PMC)', 'traffic_source': traffic_src,
@@ -226,6 +262,8 @@ def main():
             'timing': 'HIP start/stop events per dispatch (hipExtLaunchKernel) over %d eager step(s) of the same '
                       'workload right after the timed region' % per,
             'algorithmic_hbm_GBs': round(nb / tsec / 1e9, 1),
+            'mfma_busy': pf.get('mfma_util'),
+            'mfma_busy_unit': 'SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE per XCD x 1024 SIMDs), rocprofv3 PMC',
             'families': {k: {'ms_per_step': round(v[3] / per * 1e3, 3),
                              'TFLOPs': round(v[1] / max(v[3], 1e-12) / 1e12, 1)} for k, v in kern.items()}}
     out = {'metric': 'train images/sec at 256x256 CUB, G+D step', 'value': round(value, 3), 'unit': 'images/sec',
@@ -239,6 +277,11 @@ def main():
            'host_issue_ms_per_step': round(t_issue / args.steps * 1e3, 3),
            'execution': 'hip-graph replay of the captured step' if use_graph else 'eager',
            'roofline': roof}
+    if args.config in CEILINGS:
+        cm, ch = CEILINGS[args.config]
+        out['step_roofline'] = {'img_s_per_gpu': round(value / world, 2), 'mfma_ceiling': cm, 'hbm_ceiling': ch,
+                                'frac_of_bound': round(value / world / min(cm, ch), 4),
+                                'source': 'BASELINE.md roofline ceilings per GPU'}
     if graph_error:
         out['graph_capture_error'] = graph_error
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

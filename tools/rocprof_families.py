@@ -11,8 +11,15 @@ used, its reduce kernel -- the same bracket bench.py's HIP events time).
 `--pmc WRITE_SIZE` runs of the same command.  Per the MI355X guide (HBM
 section) FETCH_SIZE on gfx950 counts half the bytes of wide coalesced reads,
 so it is doubled; WRITE_SIZE is taken as is.  Both are in KB.
-Output JSON: {family: {calls, avg_call_us, total_ms, hbm_bytes_per_call}}
-plus totals (GPU busy time per step), read by bench.py for `traffic`.
+--mfma: directory of a `rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES
+GRBM_GUI_ACTIVE` run: MFMA-busy SIMD cycles and GPU-active cycles (summed
+over the 8 XCDs, so /8 per XCD) per call; mfma_util = busy / (active/8 x 1024
+SIMDs), the fraction of the dense bf16 MFMA peak at the clock the kernel ran
+(a 16x16x32 bf16 MFMA is 16 busy cycles for 16384 FLOP: 1024 FLOP per busy
+cycle per SIMD -- MI355X_MICROARCH.md, matrix cores).
+Output JSON: {family: {calls, avg_call_us, total_ms, hbm_bytes_per_call,
+mfma_util}} plus totals (GPU busy time per step), read by bench.py for
+`traffic` and `mfma_busy`.
 """
 import argparse
 import csv
@@ -89,12 +96,15 @@ def main():
     ap.add_argument('--trace', required=True)
     ap.add_argument('--fetch')
     ap.add_argument('--write')
+    ap.add_argument('--mfma')
     ap.add_argument('--steps', type=int, default=0, help='steps in the traced run (warmup+timed) for per-step totals')
     ap.add_argument('--out')
     a = ap.parse_args()
     fams = kernel_trace(a.trace)
     fetch = pmc(a.fetch, 'FETCH_SIZE') if a.fetch else None
     write = pmc(a.write, 'WRITE_SIZE') if a.write else None
+    busy = pmc(a.mfma, 'SQ_VALU_MFMA_BUSY_CYCLES') if a.mfma else None
+    gui = pmc(a.mfma, 'GRBM_GUI_ACTIVE') if a.mfma else None
     out = {}
     for fam, o in sorted(fams.items(), key=lambda kv: -kv[1]['ns']):
         calls = max(o['calls'], 1)
@@ -107,6 +117,12 @@ def main():
             e['hbm_read_bytes_per_call'] = round(rd)
             e['hbm_write_bytes_per_call'] = round(wr)
             e['hbm_bytes_per_call'] = round(rd + wr)
+        if busy and gui and gui[0].get(fam):
+            b, gcy = busy[0][fam], gui[0][fam]
+            n = max(busy[1][fam], 1)
+            e['mfma_busy_cycles_per_call'] = round(b / n)
+            e['gpu_active_cycles_per_call'] = round(gcy / 8 / n)
+            e['mfma_util'] = round(b / (gcy / 8 * 1024), 4)
         out[fam] = e
     total_ns = sum(o['ns'] for o in fams.values())
     res = {'families': out, 'gpu_busy_ms_total': round(total_ns * 1e-6, 3)}
