@@ -45,6 +45,8 @@ def main():
     ap.add_argument('--shapes', default='all')
     ap.add_argument('--dirs', default='fwd,bwdd,wgrad')
     ap.add_argument('--iters', type=int, default=50)
+    ap.add_argument('--device-time', action='store_true',
+                    help='sum of per-dispatch HIP event times (kernel + split-K reduce), no host gaps')
     args = ap.parse_args()
     from eegan_hip import functional as Fn
     from eegan_hip.tensor import empty_nhwc
@@ -74,13 +76,21 @@ def main():
             for _ in range(3):
                 fn()
             torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(args.iters):
-                fn()
-            e1.record()
-            torch.cuda.synchronize()
-            us = e0.elapsed_time(e1) * 1e3 / args.iters
+            if args.device_time:
+                Fn.TIMER = Fn.LaunchTimer()
+                for _ in range(args.iters):
+                    fn()
+                summ = Fn.TIMER.summary()
+                Fn.TIMER = None
+                us = sum(v[3] for v in summ.values()) * 1e6 / args.iters
+            else:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.iters):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) * 1e3 / args.iters
             print('%-16s %-6s %9.2f us %8.1f TF/s' % (name, dname, us, flops / us / 1e6), flush=True)
 
 
