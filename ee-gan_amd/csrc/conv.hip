@@ -2023,16 +2023,9 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   dim3 grid(ee_cdiv(Pc_max, p.tpix), ee_cdiv(a.Mrows, p.tco), a.ncls * p.nsplit);
   const long w_bytes = (long)ee_round_up(a.Mrows, 128) * a.Kw * 2;
 #define GL(TC, TP) ee_launch(conv_glds_kernel<MODE, TC, TP>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
-  // small grids (about one block per CU) are bound by the LDS-DMA latency of
-  // each K-step: a deeper ring keeps more K-steps in flight (8 stages: two
-  // K-step pairs ahead instead of one); larger grids keep 4 stages (occupancy)
-  const long nblocks = (long)grid.x * grid.y * grid.z;
-  const int deep = nblocks <= env_int("EEGAN_CONV_DEEP_GRID", 512) ? env_int("EEGAN_CONV_DEEP_STAGES", 8) : 4;
 #define FA(TC, TP)                                                                                          \
   do {                                                                                                       \
-    if (ksv == 22 && deep == 8) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 8, 2>, grid, dim3(256), 0, s, a, src_bytes, w_bytes); \
-    else if (ksv == 22 && deep == 6) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 6, 2>, grid, dim3(256), 0, s, a, src_bytes, w_bytes); \
-    else if (ksv == 22) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 4, 2>, grid, dim3(256), 0, s, a, src_bytes, w_bytes); \
+    if (ksv == 22) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 4, 2>, grid, dim3(256), 0, s, a, src_bytes, w_bytes); \
     else if (ksv == 2) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 4>, grid, dim3(256), 0, s, a, src_bytes, w_bytes); \
     else ee_launch(conv_fast_kernel<MODE, TC, TP, 1, 4>, grid, dim3(256), 0, s, a, src_bytes, w_bytes);                     \
   } while (0)

@@ -6,7 +6,7 @@
 // (func_attention) and the per-caption loop of 272-331 (words_loss); the
 // masked bidirectional cross-entropy stays in loss.hip (sim_ce).
 //
-// Per pair (one workgroup, 4 waves), with ctx = regions of image j
+// Per pair (one workgroup, 8 waves), with ctx = regions of image j
 // (289 x 256) and q = words of caption i (w <= 32 valid of T):
 //   S  = ctx q^T           (289 x w)    MFMA, split-bf16 (hi*hi + lo*hi + hi*lo:
 //                                        the logits feed a sharp softmax, so they
@@ -40,6 +40,10 @@ constexpr int NW = 32;     // words per caption (padded; cfg.TEXT.WORDS_NUM = 20
 constexpr int QLD = ND + 8;    // bf16 row stride of q / dC in LDS (conflict-free b128 row reads)
 constexpr int A2LD = NRK + 8;  // bf16 row stride of A2 / dS^T in LDS
 constexpr int A1LD = NW + 4;   // fp32 row stride of A1 in LDS (16-byte aligned rows)
+constexpr int NWV = 8;         // waves per pair workgroup (latency: more waves, shorter per-wave chains)
+constexpr int PT = NWV * 64;   // threads per pair workgroup
+constexpr int MS = (NRP / 16 + NWV - 1) / NWV;  // region tiles per wave (19 tiles)
+constexpr int DT = (ND / 16) / NWV;             // 16-dim tiles per wave (16 tiles)
 
 EE_DEV bf16x8_t frag(const bf16_t* p) { return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(p)); }
 EE_DEV f32x4_t mfma(bf16x8_t a, bf16x8_t b, f32x4_t c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
@@ -102,18 +106,33 @@ struct WordsArgs {
 
 // ----------------------------------------------------------------- prep --
 // regions fp32 [n_img][289][256] -> ctx hi/lo [n_img][304][256], ctx^T [n_img][256][320]
-__global__ __launch_bounds__(256) void words_prep_ctx_kernel(const float* __restrict__ reg, bf16_t* ctxh,
-                                                             bf16_t* ctxl, bf16_t* ctxT) {
-  __shared__ float tile[32][ND + 4];
-  const int j = blockIdx.x, r0 = blockIdx.y * 32, t = threadIdx.x;
-  for (int e = t; e < 32 * (ND / 4); e += 256) {
+EE_DEV void prep_q(const float* __restrict__ words, const long* lens, int T, bf16_t* qh, bf16_t* ql, bf16_t* qT,
+                   int i, int d, float (*stage)[NW + 1]);
+
+constexpr int PREP_ROWS = 16;  // region rows per workgroup: n_img * 20 + n_txt workgroups
+
+// one launch prepares both operands: workgroups [0, n_img * NRK / 16) the
+// regions (16 region rows each), the rest one caption each
+__global__ __launch_bounds__(256) void words_prep_kernel(const float* __restrict__ reg, bf16_t* ctxh, bf16_t* ctxl,
+                                                         bf16_t* ctxT, int n_img, const float* __restrict__ words,
+                                                         const long* lens, int T, bf16_t* qh, bf16_t* ql, bf16_t* qT) {
+  __shared__ float tile[ND * (NW + 1)];  // regions: [16][ND + 4]; captions: [ND][NW + 1]
+  constexpr int RB = NRK / PREP_ROWS;
+  if ((int)blockIdx.x >= n_img * RB) {
+    prep_q(words, lens, T, qh, ql, qT, blockIdx.x - n_img * RB, threadIdx.x,
+           reinterpret_cast<float(*)[NW + 1]>(tile));
+    return;
+  }
+  float(*rt)[ND + 4] = reinterpret_cast<float(*)[ND + 4]>(tile);
+  const int j = blockIdx.x / RB, r0 = (blockIdx.x % RB) * PREP_ROWS, t = threadIdx.x;
+  for (int e = t; e < PREP_ROWS * (ND / 4); e += 256) {
     const int row = e / (ND / 4), d = (e % (ND / 4)) * 4, r = r0 + row;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (r < NR) v = *reinterpret_cast<const float4*>(reg + ((long)j * NR + r) * ND + d);
-    tile[row][d] = v.x;
-    tile[row][d + 1] = v.y;
-    tile[row][d + 2] = v.z;
-    tile[row][d + 3] = v.w;
+    rt[row][d] = v.x;
+    rt[row][d + 1] = v.y;
+    rt[row][d + 2] = v.z;
+    rt[row][d + 3] = v.w;
     if (r < NRP) {
       const float f[4] = {v.x, v.y, v.z, v.w};
       uint32_t h[2], lo[2];
@@ -129,20 +148,22 @@ __global__ __launch_bounds__(256) void words_prep_ctx_kernel(const float* __rest
     }
   }
   __syncthreads();
-  const int d = t;  // 256 threads = 256 dims: 32 regions -> 64 contiguous bytes of ctx^T
-  uint32_t p[16];
+  const int d = t;  // 256 threads = 256 dims: 16 regions -> 32 contiguous bytes of ctx^T
+  uint32_t p[PREP_ROWS / 2];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) p[c] = pack2(tile[2 * c][d], tile[2 * c + 1][d]);
+  for (int c = 0; c < PREP_ROWS / 2; ++c) p[c] = pack2(rt[2 * c][d], rt[2 * c + 1][d]);
   uint4* dst = reinterpret_cast<uint4*>(ctxT + ((long)j * ND + d) * NRK + r0);
 #pragma unroll
-  for (int c = 0; c < 4; ++c) dst[c] = make_uint4(p[4 * c], p[4 * c + 1], p[4 * c + 2], p[4 * c + 3]);
+  for (int c = 0; c < PREP_ROWS / 8; ++c) dst[c] = make_uint4(p[4 * c], p[4 * c + 1], p[4 * c + 2], p[4 * c + 3]);
 }
 
 // words fp32 [n_txt][256][T] -> q hi/lo [n_txt][32][256], q^T (hi) [n_txt][256][32]
-__global__ __launch_bounds__(256) void words_prep_q_kernel(const float* __restrict__ words, const long* lens, int T,
-                                                           bf16_t* qh, bf16_t* ql, bf16_t* qT) {
-  const int i = blockIdx.x, d = threadIdx.x;
+EE_DEV void prep_q(const float* __restrict__ words, const long* lens, int T, bf16_t* qh, bf16_t* ql, bf16_t* qT,
+                   int i, int d, float (*stage)[NW + 1]) {
   const int w = max(1, min((int)lens[i], min(T, NW)));
+  // the caption's [256][T] block is contiguous: stage it coalesced
+  for (int e = d; e < ND * T; e += 256) stage[e / T][e % T] = words[(long)i * ND * T + e];
+  __syncthreads();
   uint32_t p[16];
 #pragma unroll
   for (int k2 = 0; k2 < 16; ++k2) {
@@ -150,7 +171,7 @@ __global__ __launch_bounds__(256) void words_prep_q_kernel(const float* __restri
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int k = 2 * k2 + u;
-      const float v = k < w ? words[((long)i * ND + d) * T + k] : 0.f;
+      const float v = k < w ? stage[d][k] : 0.f;
       hh[u] = f2bf(v);
       qh[((long)i * NW + k) * ND + d] = hh[u];
       ql[((long)i * NW + k) * ND + d] = f2bf(v - bf2f(hh[u]));
@@ -166,8 +187,8 @@ __global__ __launch_bounds__(256) void words_prep_q_kernel(const float* __restri
 struct SmemF {   // forward part (also the first part of the backward's)
   bf16_t qh[NW][QLD], ql[NW][QLD];
   bf16_t a2[NW][A2LD];                  // A2 [k][r] (phase 2 operand); bwd: dS^T [k][r]
-  float colsum[4][NW], colinv[NW];
-  float cred[4][NW][3], red2[4][NW];
+  float colsum[NWV][NW], colinv[NW];
+  float cred[NWV][NW][3], red2[NWV][NW];
   float cs[NW], nq[NW], nc[NW];
 };
 struct SmemB {
@@ -177,7 +198,7 @@ struct SmemB {
 };
 
 template <bool BWD>
-__global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
+__global__ __launch_bounds__(PT) void words_pair_kernel(WordsArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   SmemF& sm = *reinterpret_cast<SmemF*>(smem_raw);
   SmemB& sb = *reinterpret_cast<SmemB*>(smem_raw);
@@ -192,12 +213,12 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
   {
     const uint4* sh = reinterpret_cast<const uint4*>(a.qh + (long)i * NW * ND);
     const uint4* sl = reinterpret_cast<const uint4*>(a.ql + (long)i * NW * ND);
-    for (int e = t; e < NW * ND / 8; e += 256) {
+    for (int e = t; e < NW * ND / 8; e += PT) {
       const int k = e / (ND / 8), c = (e % (ND / 8)) * 8;
       *reinterpret_cast<uint4*>(&sm.qh[k][c]) = sh[e];
       *reinterpret_cast<uint4*>(&sm.ql[k][c]) = sl[e];
     }
-    for (int e = t; e < NW * (NRK - NRP) / 2; e += 256)
+    for (int e = t; e < NW * (NRK - NRP) / 2; e += PT)
       *reinterpret_cast<uint32_t*>(&sm.a2[e / 8][NRP + (e % 8) * 2]) = 0u;
   }
   __syncthreads();
@@ -205,11 +226,11 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
   // ---- phase 1: S = ctx q^T (split bf16), softmax over words, exp(gamma1 A1)
   const bf16_t* ch = a.ctxh + (long)j * NRP * ND;
   const bf16_t* cl = a.ctxl + (long)j * NRP * ND;
-  f32x4_t ev[5][2];
+  f32x4_t ev[MS][2];
   float colp[2] = {0.f, 0.f};
 #pragma unroll
-  for (int s = 0; s < 5; ++s) {
-    const int mt = wv + 4 * s;
+  for (int s = 0; s < MS; ++s) {
+    const int mt = wv + NWV * s;
     ev[s][0] = ev[s][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     if (mt >= NRP / 16) break;  // wave-uniform
     f32x4_t acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -258,7 +279,9 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
   }
   __syncthreads();
   if (t < NW) {
-    const float c = sm.colsum[0][t] + sm.colsum[1][t] + sm.colsum[2][t] + sm.colsum[3][t];
+    float c = 0.f;
+#pragma unroll
+    for (int x = 0; x < NWV; ++x) c += sm.colsum[x][t];
     sm.colinv[t] = c > 0.f ? 1.f / c : 0.f;
   }
   __syncthreads();
@@ -266,8 +289,8 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
     const float inv0 = sm.colinv[fr], inv1 = sm.colinv[16 + fr];
     const bool want_att = !BWD && a.att && i == j + a.diag_off;
 #pragma unroll
-    for (int s = 0; s < 5; ++s) {
-      const int mt = wv + 4 * s;
+    for (int s = 0; s < MS; ++s) {
+      const int mt = wv + NWV * s;
       if (mt >= NRP / 16) break;
       const int row0 = mt * 16 + fq * 4;
 #pragma unroll
@@ -290,11 +313,11 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
 
   // ---- phase 2: C[k][d] = sum_r A2[k][r] ctx[r][d]  (wave: 64 dims)
   const bf16_t* cT = a.ctxT + (long)j * ND * NRK;
-  f32x4_t cacc[2][4];
+  f32x4_t cacc[2][DT];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) cacc[m][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < DT; ++n) cacc[m][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
   for (int kk = 0; kk < NRK / 32; ++kk) {
     bf16x8_t am[2];
@@ -302,8 +325,8 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
     for (int m = 0; m < 2; ++m)
       if (m < nn) am[m] = frag(&sm.a2[m * 16 + fr][kk * 32 + fq * 8]);
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const bf16x8_t b = frag(cT + ((wv * 4 + n) * 16 + fr) * NRK + kk * 32 + fq * 8);
+    for (int n = 0; n < DT; ++n) {
+      const bf16x8_t b = frag(cT + ((wv * DT + n) * 16 + fr) * NRK + kk * 32 + fq * 8);
 #pragma unroll
       for (int m = 0; m < 2; ++m)
         if (m < nn) cacc[m][n] = mfma(am[m], b, cacc[m][n]);
@@ -311,7 +334,7 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
   }
 
   // ---- phase 3: cosine(q_k, C_k) over the 256 dims (DAMSM_losses.py:17-23)
-  float qv[2][4][4];
+  float qv[2][DT][4];
   {
     float dp[2][4], c2[2][4], q2[2][4];
 #pragma unroll
@@ -321,8 +344,8 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
         dp[m][r] = c2[m][r] = q2[m][r] = 0.f;
         const int k = m * 16 + fq * 4 + r;
 #pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          const int d = (wv * 4 + n) * 16 + fr;
+        for (int n = 0; n < DT; ++n) {
+          const int d = (wv * DT + n) * 16 + fr;
           const float q = (m < nn && k < w) ? a.words[((long)i * ND + d) * a.T + k] : 0.f;
           const float c = m < nn ? cacc[m][n][r] : 0.f;
           qv[m][n][r] = q;
@@ -344,7 +367,7 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
   if (t < NW) {
     float u = 0.f, q2 = 0.f, c2 = 0.f;
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
+    for (int x = 0; x < NWV; ++x) {
       u += sm.cred[x][t][0];
       q2 += sm.cred[x][t][1];
       c2 += sm.cred[x][t][2];
@@ -364,7 +387,7 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
 
   // ================================ backward ================================
   const float drow = G3 * a.dsim[pair];
-  float dqc[2][4][4];  // d loss / d q through the cosine, phase-2 layout
+  float dqc[2][DT][4];  // d loss / d q through the cosine, phase-2 layout
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -379,7 +402,7 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
       }
       const float den = nq * nc;
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
+      for (int n = 0; n < DT; ++n) {
         const float q = qv[m][n][r], c = m < nn ? cacc[m][n][r] : 0.f;
         float dC, dq;
         if (den > 1e-8f) {
@@ -391,26 +414,26 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
         }
         dqc[m][n][r] = dq;
         cacc[m][n][r] = dC;  // the accumulator now holds dC
-        sb.dc[k][(wv * 4 + n) * 16 + fr] = f2bf(dC);
+        sb.dc[k][(wv * DT + n) * 16 + fr] = f2bf(dC);
       }
     }
   // V factor: dC^T [d][k] (4 consecutive words of one dim per lane)
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int d = (wv * 4 + n) * 16 + fr;
+    for (int n = 0; n < DT; ++n) {
+      const int d = (wv * DT + n) * 16 + fr;
       *reinterpret_cast<uint2*>(a.V + (pair * ND + d) * NW + m * 16 + fq * 4) =
           make_uint2(pack2(cacc[m][n][0], cacc[m][n][1]), pack2(cacc[m][n][2], cacc[m][n][3]));
     }
   __syncthreads();
 
   // ---- phase 4: dA2[k][r] = sum_d dC[k][d] ctx[r][d]  (wave: region tiles wv, wv+4, ...)
-  f32x4_t da[5][2];
+  f32x4_t da[MS][2];
 #pragma unroll
-  for (int s = 0; s < 5; ++s) {
+  for (int s = 0; s < MS; ++s) {
     da[s][0] = da[s][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    const int nt = wv + 4 * s;
+    const int nt = wv + NWV * s;
     if (nt >= NRP / 16) break;
     const bf16_t* bp = ch + (nt * 16 + fr) * ND + fq * 8;
 #pragma unroll
@@ -428,8 +451,8 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) rd[m][r] = 0.f;
 #pragma unroll
-  for (int s = 0; s < 5; ++s) {
-    const int nt = wv + 4 * s;
+  for (int s = 0; s < MS; ++s) {
+    const int nt = wv + NWV * s;
     if (nt >= NRP / 16) break;
     const int row = nt * 16 + fr;
 #pragma unroll
@@ -455,8 +478,8 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
   __syncthreads();
   // dS = A1 (dA1 - <A1, dA1>_k) per region; U factor = [A2^T | dS]; dS^T to LDS for dwords
 #pragma unroll
-  for (int s = 0; s < 5; ++s) {
-    const int nt = wv + 4 * s;
+  for (int s = 0; s < MS; ++s) {
+    const int nt = wv + NWV * s;
     if (nt >= NRP / 16) break;
     const int row = nt * 16 + fr;
     float a2v[2][4], a1v[2][4], dA1[2][4];
@@ -471,7 +494,9 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
         const int k = k0 + r;
         const bool ok = row < NR && m < nn && k < w;
         const float a2 = ok ? __expf(G1 * a1s[r]) * sm.colinv[k] : 0.f;
-        const float rdot = sm.red2[0][k] + sm.red2[1][k] + sm.red2[2][k] + sm.red2[3][k];
+        float rdot = 0.f;
+#pragma unroll
+        for (int x = 0; x < NWV; ++x) rdot += sm.red2[x][k];
         a2v[m][r] = a2;
         a1v[m][r] = ok ? a1s[r] : 0.f;
         dA1[m][r] = ok ? G1 * a2 * (da[s][m][r] - rdot) : 0.f;
@@ -500,7 +525,7 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) cacc[m][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < DT; ++n) cacc[m][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
   for (int kk = 0; kk < NRK / 32; ++kk) {
     bf16x8_t am[2];
@@ -508,8 +533,8 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
     for (int m = 0; m < 2; ++m)
       if (m < nn) am[m] = frag(&sm.a2[m * 16 + fr][kk * 32 + fq * 8]);
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const bf16x8_t b = frag(cT + ((wv * 4 + n) * 16 + fr) * NRK + kk * 32 + fq * 8);
+    for (int n = 0; n < DT; ++n) {
+      const bf16x8_t b = frag(cT + ((wv * DT + n) * 16 + fr) * NRK + kk * 32 + fq * 8);
 #pragma unroll
       for (int m = 0; m < 2; ++m)
         if (m < nn) cacc[m][n] = mfma(am[m], b, cacc[m][n]);
@@ -519,8 +544,8 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int d = (wv * 4 + n) * 16 + fr;
+    for (int n = 0; n < DT; ++n) {
+      const int d = (wv * DT + n) * 16 + fr;
       f32x4_t v;
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = m < nn ? cacc[m][n][r] + dqc[m][n][r] : 0.f;
@@ -528,47 +553,68 @@ __global__ __launch_bounds__(256) void words_pair_kernel(WordsArgs a) {
     }
 }
 
-// dregions[j][r][d] = sum_i sum_c U[j,i][r][c] V'[j,i][c][d],  V' = [dC ; q] (K = 64 per caption)
+// dregions[j][r][d] = sum_i sum_c U[j,i][r][c] V'[j,i][c][d],  V' = [dC ; q] (K = 64 per caption).
+// Workgroup = 64 regions x 64 dims; each of its 4 waves accumulates the whole
+// 64 x 64 tile (16 MFMA tiles: 8 fragment loads per 16 MFMAs) over captions
+// i = wave, wave + 4, ..., and the four partial tiles are added in a fixed
+// order through LDS (deterministic; no atomics).
 __global__ __launch_bounds__(256) void words_dctx_kernel(const bf16_t* __restrict__ U, const bf16_t* __restrict__ V,
                                                          const bf16_t* __restrict__ qT, int n_txt,
                                                          float* __restrict__ dreg) {
+  __shared__ float red[3][64][64 + 4];
   const int t = threadIdx.x, l = t & 63, wv = t >> 6, fr = l & 15, fq = l >> 4;
   const int j = blockIdx.z;
-  const int r0 = blockIdx.y * 64 + (wv >> 1) * 32, d0 = blockIdx.x * 64 + (wv & 1) * 32;
-  f32x4_t acc[2][2];
+  const int r0 = blockIdx.y * 64, d0 = blockIdx.x * 64;
+  f32x4_t acc[4][4];
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
+  for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < 2; ++n) acc[m][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  const bool rok[2] = {r0 + fr < NRP, r0 + 16 + fr < NRP};
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  bool rok[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) rok[m] = r0 + m * 16 + fr < NRP;
   const bf16x8_t zero = __builtin_bit_cast(bf16x8_t, make_uint4(0u, 0u, 0u, 0u));
-  for (int i = 0; i < n_txt; ++i) {
+  for (int i = wv; i < n_txt; i += 4) {
     const long pair = (long)j * n_txt + i;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      bf16x8_t am[2], bn[2];
+      bf16x8_t am[4], bn[4];
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+      for (int m = 0; m < 4; ++m)
         am[m] = rok[m] ? frag(U + (pair * NRP + r0 + m * 16 + fr) * 64 + c * 32 + fq * 8) : zero;
 #pragma unroll
-      for (int n = 0; n < 2; ++n) {
+      for (int n = 0; n < 4; ++n) {
         const int d = d0 + n * 16 + fr;
         bn[n] = c == 0 ? frag(V + (pair * ND + d) * NW + fq * 8) : frag(qT + ((long)i * ND + d) * NW + fq * 8);
       }
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+      for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int n = 0; n < 2; ++n) acc[m][n] = mfma(am[m], bn[n], acc[m][n]);
+        for (int n = 0; n < 4; ++n) acc[m][n] = mfma(am[m], bn[n], acc[m][n]);
     }
   }
+  if (wv > 0) {
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[wv - 1][m * 16 + fq * 4 + r][n * 16 + fr] = acc[m][n][r];
+  }
+  __syncthreads();
+  if (wv != 0) return;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = r0 + m * 16 + fq * 4 + r;
-        if (row < NR) dreg[((long)j * NR + row) * ND + d0 + n * 16 + fr] = acc[m][n][r];
+        const int row = m * 16 + fq * 4 + r, col = n * 16 + fr;
+        float v = acc[m][n][r];
+        v += red[0][row][col];
+        v += red[1][row][col];
+        v += red[2][row][col];
+        if (r0 + row < NR) dreg[((long)j * NR + r0 + row) * ND + d0 + col] = v;
       }
 }
 
@@ -586,13 +632,10 @@ __global__ void words_dq_reduce_kernel(const float* __restrict__ dq, int n_img, 
 
 int prep(const float* regions, const float* words, const long* lens, int n_img, int n_txt, int T, const Ws& L,
          char* ws, hipStream_t s) {
-  ee_launch(words_prep_ctx_kernel, dim3(n_img, NRK / 32), dim3(256), 0, s, regions, (bf16_t*)(ws + L.ctxh),
-            (bf16_t*)(ws + L.ctxl), (bf16_t*)(ws + L.ctxT));
-  int rc = ee_check_launch("words_prep_ctx");
-  if (rc) return rc;
-  ee_launch(words_prep_q_kernel, dim3(n_txt), dim3(256), 0, s, words, lens, T, (bf16_t*)(ws + L.qh),
+  ee_launch(words_prep_kernel, dim3(n_img * (NRK / PREP_ROWS) + n_txt), dim3(256), 0, s, regions, (bf16_t*)(ws + L.ctxh),
+            (bf16_t*)(ws + L.ctxl), (bf16_t*)(ws + L.ctxT), n_img, words, lens, T, (bf16_t*)(ws + L.qh),
             (bf16_t*)(ws + L.ql), (bf16_t*)(ws + L.qT));
-  return ee_check_launch("words_prep_q");
+  return ee_check_launch("words_prep");
 }
 
 WordsArgs make_args(const float* words, const long* lens, int n_img, int n_txt, int T, const Ws& L, char* ws) {
@@ -641,23 +684,23 @@ int eegan_words_sim(const float* regions, const float* words, const long* cap_le
   a.sim = sim;
   a.att = att;
   a.diag_off = diag_off;
-  ee_launch(words_pair_kernel<false>, dim3(n_txt, n_img), dim3(256), (uint32_t)sizeof(SmemF), s, a);
+  ee_launch(words_pair_kernel<false>, dim3(n_txt, n_img), dim3(PT), (uint32_t)sizeof(SmemF), s, a);
   return ee_check_launch("words_sim");
 }
 
 int eegan_words_sim_bwd(const float* regions, const float* words, const long* cap_lens, int n_img, int n_txt, int T,
-                        const float* dsim, float* dregions, float* dwords, void* ws, hipStream_t s) {
+                        const float* dsim, float* dregions, float* dwords, void* ws, int prepared, hipStream_t s) {
   if (!check(regions, n_img, n_txt, T, "words_sim_bwd")) return -22;
   const Ws L = ws_layout(n_img, n_txt, 1, dwords != nullptr);
   char* w = static_cast<char*>(ws);
-  int rc = prep(regions, words, cap_lens, n_img, n_txt, T, L, w, s);
+  int rc = prepared ? 0 : prep(regions, words, cap_lens, n_img, n_txt, T, L, w, s);
   if (rc) return rc;
   WordsArgs a = make_args(words, cap_lens, n_img, n_txt, T, L, w);
   a.dsim = dsim;
   a.U = (bf16_t*)(w + L.U);
   a.V = (bf16_t*)(w + L.V);
   a.dq = dwords ? (float*)(w + L.dq) : nullptr;
-  ee_launch(words_pair_kernel<true>, dim3(n_txt, n_img), dim3(256), (uint32_t)sizeof(SmemB), s, a);
+  ee_launch(words_pair_kernel<true>, dim3(n_txt, n_img), dim3(PT), (uint32_t)sizeof(SmemB), s, a);
   rc = ee_check_launch("words_sim_bwd");
   if (rc) return rc;
   ee_launch(words_dctx_kernel, dim3(ND / 64, (NRP + 63) / 64, n_img), dim3(256), 0, s, (const bf16_t*)a.U,

@@ -96,9 +96,12 @@ _SIGS = {
     'eegan_act_bwd_f32': ([P, P, L, I, F, P, P], I),
     'eegan_words_workspace': ([I, I, I, I], L),
     'eegan_words_sim': ([P, P, P, I, I, I, I, P, P, P, P], I),
-    'eegan_words_sim_bwd': ([P, P, P, I, I, I, P, P, P, P, P], I),
+    'eegan_words_sim_bwd': ([P, P, P, I, I, I, P, P, P, P, I, P], I),
     'eegan_sim_ce': ([P, I, P, P, P, P], I),
     'eegan_sim_ce_bwd': ([P, I, P, P, P, P, P], I),
+    'eegan_gag_fwd': ([P, P, P, P, I, I, I, I, I, P, P, P], I),
+    'eegan_gag_workspace': ([I, I, I, I, I], L),
+    'eegan_gag_bwd': ([P, P, P, P, P, P, I, I, I, I, I, P, P, P, P, P], I),
     'eegan_sent_sim': ([P, P, I, I, I, P, P], I),
     'eegan_sent_sim_bwd': ([P, P, I, I, I, P, P, P, P, P, P], I),
     'eegan_dout_reduce': ([P, I, I, P, P], I),
@@ -131,7 +134,7 @@ def _load():
 
 LIB = _load()
 ABI_VERSION = LIB.eegan_abi_version()
-EXPECTED_ABI = 4
+EXPECTED_ABI = 5
 if ABI_VERSION != EXPECTED_ABI:
     raise ImportError('%s has ABI %d, these bindings need %d: rebuild (make -C ee-gan_amd/csrc)'
                       % (LIB_PATH, ABI_VERSION, EXPECTED_ABI))

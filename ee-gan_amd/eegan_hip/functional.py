@@ -1497,9 +1497,14 @@ class WordsSimFn(torch.autograd.Function):
         lens = cap_lens.to(device=regions.device, dtype=torch.long).reshape(-1).contiguous()
         sim = torch.empty((n_img, n_txt), dtype=F32, device=regions.device)
         att = torch.zeros((n_img, Tn, 289) if want_att else (0,), dtype=F32, device=regions.device)
-        ws = workspace(ops.words_workspace(n_img, n_txt, 0, 0), regions.device)
+        # when a backward will follow, the workspace is sized for it and kept:
+        # the backward reuses the operands prepared here
+        bwd = bool(ctx.needs_input_grad[0] or ctx.needs_input_grad[1])
+        ws = workspace(ops.words_workspace(n_img, n_txt, int(bwd), int(bool(ctx.needs_input_grad[1]))),
+                       regions.device)
         ops.words_sim(reg.data_ptr(), wd.data_ptr(), lens.data_ptr(), n_img, n_txt, Tn, int(diag_off), sim.data_ptr(),
                       att.data_ptr() if want_att else 0, ws.data_ptr(), stream())
+        ctx.ws = ws if bwd else None
         ctx.save_for_backward(reg, wd, lens)
         ctx.mark_non_differentiable(att)
         return sim, att
@@ -1512,10 +1517,49 @@ class WordsSimFn(torch.autograd.Function):
         need_dw = ctx.needs_input_grad[1]
         dreg = torch.empty((n_img, 17, 17, 256), dtype=F32, device=dsim.device)
         dw = torch.empty_like(wd) if need_dw else None
-        ws = workspace(ops.words_workspace(n_img, n_txt, 1, int(need_dw)), dsim.device)
+        ws, prepared = ctx.ws, 1
+        if ws is None or ws.numel() < ops.words_workspace(n_img, n_txt, 1, int(need_dw)):
+            ws, prepared = workspace(ops.words_workspace(n_img, n_txt, 1, int(need_dw)), dsim.device), 0
         ops.words_sim_bwd(reg.data_ptr(), wd.data_ptr(), lens.data_ptr(), n_img, n_txt, Tn, dsim.data_ptr(),
-                          dreg.data_ptr(), ptr(dw), ws.data_ptr(), stream())
+                          dreg.data_ptr(), ptr(dw), ws.data_ptr(), prepared, stream())
+        ctx.ws = None
         return dreg.permute(0, 3, 1, 2), dw, None, None, None
+
+
+class GlobalAttentionFn(torch.autograd.Function):
+    """GlobalAttentionGeneral.forward (DAMSM_losses.py:65-132) as one HIP
+    launch (csrc/gag.hip): input (B, idf, ih, iw), context_key (B, idf, S),
+    content_value (B, cdf, S), mask (B, S) bool or None ->
+    (weightedContext (B, cdf, ih, iw), attn (B, S, ih, iw)); the mask is
+    applied with the reference's ``mask.repeat(queryL, 1)`` row indexing."""
+
+    @staticmethod
+    def forward(ctx, inp, key, value, mask):
+        B, idf, ih, iw = inp.shape
+        Lq, S, cdf = ih * iw, key.shape[2], value.shape[1]
+        x = inp.float().contiguous()
+        k = key.float().contiguous()
+        v = value.float().contiguous()
+        m = mask.to(device=inp.device, dtype=torch.uint8).contiguous() if mask is not None else None
+        wc = torch.empty((B, cdf, ih, iw), dtype=F32, device=inp.device)
+        att = torch.empty((B, S, ih, iw), dtype=F32, device=inp.device)
+        ops.gag_fwd(x.data_ptr(), k.data_ptr(), v.data_ptr(), ptr(m), B, idf, cdf, Lq, S, wc.data_ptr(),
+                    att.data_ptr(), stream())
+        ctx.save_for_backward(x, k, v, att)
+        return wc, att
+
+    @staticmethod
+    def backward(ctx, dwc, datt):
+        x, k, v, att = ctx.saved_tensors
+        B, idf, ih, iw = x.shape
+        Lq, S, cdf = ih * iw, k.shape[2], v.shape[1]
+        dwc = dwc.float().contiguous() if dwc is not None else None
+        datt = datt.float().contiguous() if datt is not None else None
+        dx, dk, dv = torch.empty_like(x), torch.empty_like(k), torch.empty_like(v)
+        ws = workspace(ops.gag_workspace(B, idf, cdf, Lq, S), x.device)
+        ops.gag_bwd(x.data_ptr(), k.data_ptr(), v.data_ptr(), att.data_ptr(), ptr(dwc), ptr(datt), B, idf, cdf, Lq,
+                    S, dx.data_ptr(), dk.data_ptr(), dv.data_ptr(), ws.data_ptr(), stream())
+        return dx, dk, dv, None
 
 
 class SentSimFn(torch.autograd.Function):

@@ -16,10 +16,11 @@ B_global x B_global matrix (eegan_hip.damsm); ``labels`` are the rank's
 local match labels (arange(batch_size) from prepare_labels), ``class_ids``
 its local ids, and ``batch_size`` the local batch size.
 
-``cosine_similarity``, ``func_attention``, ``GlobalAttentionGeneral``,
-``sent_similarity`` and ``words_similarity`` are kept for API completeness
-(the reference never calls them on the training path) and are thin tensor
-expressions.
+``GlobalAttentionGeneral`` (defined but never called by the reference) runs
+as its own HIP kernel (csrc/gag.hip, split-bf16 MFMA, the reference's -inf
+mask indexing); ``cosine_similarity``, ``func_attention``, ``sent_similarity``
+and ``words_similarity`` are kept for API completeness (also never called on
+the training path) as thin tensor expressions.
 """
 import torch
 import torch.nn as nn
@@ -45,7 +46,9 @@ def func_attention(query, context, gamma1):
 
 
 class GlobalAttentionGeneral(nn.Module):
-    """word <-> feature-map attention (DAMSM_losses.py:65-132; unused by the reference step)."""
+    """word <-> feature-map attention (DAMSM_losses.py:65-132; unused by the reference step).
+    sourceL <= 64; the mask (B, sourceL) bool is applied like the reference's
+    ``mask.repeat(queryL, 1)`` (row b*queryL + q reads mask[(b*queryL + q) % B])."""
 
     def __init__(self, idf, cdf):
         super().__init__()
@@ -56,15 +59,8 @@ class GlobalAttentionGeneral(nn.Module):
         self.mask = mask
 
     def forward(self, input, context_key, content_value):
-        B, _, ih, iw = input.shape
-        Lq = ih * iw
-        S = context_key.size(2)
-        attn = torch.bmm(input.reshape(B, -1, Lq).transpose(1, 2), context_key).reshape(B * Lq, S)
-        if self.mask is not None:
-            attn = attn.masked_fill(self.mask.repeat(Lq, 1), -float('inf'))
-        attn = self.sm(attn).reshape(B, Lq, S).transpose(1, 2)
-        wc = torch.bmm(content_value, attn)
-        return wc.reshape(B, -1, ih, iw), attn.reshape(B, -1, ih, iw)
+        """-> (weightedContext (B, cdf, ih, iw), attn (B, sourceL, ih, iw)), DAMSM_losses.py:75-132."""
+        return Fn.GlobalAttentionFn.apply(input, context_key, content_value, self.mask)
 
 
 def _masked(sim, class_ids, batch_size):

@@ -26,8 +26,9 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 4  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
-                                4: rectangular (local x global) DAMSM words / sentence blocks on MFMA */
+#define EEGAN_ABI_VERSION 5  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
+                                4: rectangular (local x global) DAMSM words / sentence blocks on MFMA;
+                                5: GlobalAttentionGeneral (eegan_gag_*), words backward reuses the forward's prep */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
@@ -223,12 +224,14 @@ int eegan_act_bwd_f32(const float* dy, const float* y, long n, int act, float sl
  * (B_local x B_global block).  regions fp32 [n_img][289][256] (16-B aligned), words fp32 [n_txt][256][T]
  * (T <= 32), cap_lens int64 [n_txt].  att (optional): the attention maps of the pairs (j, j + diag_off),
  * [n_img][T][289].  Workspace bytes from eegan_words_workspace (backward: 1 for the _bwd call, want_dwords:
- * dwords != NULL).  dregions [n_img][289][256] and dwords [n_txt][256][T] are overwritten, deterministically. */
+ * dwords != NULL).  dregions [n_img][289][256] and dwords [n_txt][256][T] are overwritten, deterministically.
+ * prepared = 1: ws is the (backward-sized) workspace a preceding eegan_words_sim call on the same inputs
+ * prepared its operands in, so the backward skips that pass. */
 long eegan_words_workspace(int n_img, int n_txt, int backward, int want_dwords);
 int eegan_words_sim(const float* regions, const float* words, const long* cap_lens, int n_img, int n_txt, int T,
                     int diag_off, float* sim, float* att, void* ws, hipStream_t s);
 int eegan_words_sim_bwd(const float* regions, const float* words, const long* cap_lens, int n_img, int n_txt, int T,
-                        const float* dsim, float* dregions, float* dwords, void* ws, hipStream_t s);
+                        const float* dsim, float* dregions, float* dwords, void* ws, int prepared, hipStream_t s);
 /* loss2 = (CE(sim, labels), CE(sim^T, labels)) with same-class off-diagonal entries masked to -inf
  * (labels == NULL means arange(B), the reference's match_labels) */
 int eegan_sim_ce(const float* sim, int B, const long* class_ids, const long* labels, float* loss2, hipStream_t s);
@@ -239,6 +242,19 @@ int eegan_sim_ce_bwd(const float* sim, int B, const long* class_ids, const long*
 int eegan_sent_sim(const float* cnn, const float* rnn, int na, int nb, int D, float* sim, hipStream_t s);
 int eegan_sent_sim_bwd(const float* cnn, const float* rnn, int na, int nb, int D, const float* sim, const float* dsim,
                        float* nrm_ws, float* dcnn, float* drnn, hipStream_t s);
+/* GlobalAttentionGeneral.forward (DAMSM_losses.py:65-132; defined, never called by the reference step):
+ * input [B][idf][queryL] (queryL = ih*iw), context_key [B][idf][sourceL], content_value [B][cdf][sourceL],
+ * mask (optional) uint8 [B][sourceL], row (b, q) masked by mask[(b*queryL + q) % B] exactly like the
+ * reference's mask.repeat(queryL, 1); sourceL <= 64.  weighted_context [B][cdf][queryL], attn [B][sourceL][queryL].
+ * Backward: d_weighted_context / d_attn may be NULL (no gradient); d_input [B][idf][queryL], d_key, d_value
+ * overwritten; ws of eegan_gag_workspace bytes. */
+int eegan_gag_fwd(const float* input, const float* context_key, const float* content_value, const unsigned char* mask,
+                  int B, int idf, int cdf, int queryL, int sourceL, float* weighted_context, float* attn,
+                  hipStream_t s);
+long eegan_gag_workspace(int B, int idf, int cdf, int queryL, int sourceL);
+int eegan_gag_bwd(const float* input, const float* context_key, const float* content_value, const float* attn,
+                  const float* d_weighted_context, const float* d_attn, int B, int idf, int cdf, int queryL,
+                  int sourceL, float* d_input, float* d_key, float* d_value, void* ws, hipStream_t s);
 /* mode 0 mean(relu(1-x)), 1 mean(relu(1+x)), 2 -mean(x), 3 mean(x) */
 int eegan_dout_reduce(const float* x, int n, int mode, float* out, hipStream_t s);
 int eegan_dout_reduce_bwd(const float* x, int n, int mode, const float* gout, float* dx, hipStream_t s);
