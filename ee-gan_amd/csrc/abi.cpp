@@ -46,6 +46,16 @@ int eegan_abi_version(void) { return EEGAN_ABI_VERSION; }
 // re-times every bracketed launch.
 int eegan_event_create(hipEvent_t* ev) { return ee_hip(hipEventCreate(ev), "hipEventCreate"); }
 int eegan_event_destroy(hipEvent_t ev) { return ee_hip(hipEventDestroy(ev), "hipEventDestroy"); }
+int eegan_stream_create(hipStream_t* s, int priority) {
+  if (priority == 0) return ee_hip(hipStreamCreateWithFlags(s, hipStreamNonBlocking), "hipStreamCreateWithFlags");
+  int least = 0, greatest = 0;
+  int rc = ee_hip(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+  if (rc) return rc;
+  // priority > 0: the device's highest priority; < 0: its lowest
+  return ee_hip(hipStreamCreateWithPriority(s, hipStreamNonBlocking, priority > 0 ? greatest : least),
+                "hipStreamCreateWithPriority");
+}
+int eegan_stream_destroy(hipStream_t s) { return ee_hip(hipStreamDestroy(s), "hipStreamDestroy"); }
 int eegan_event_record(hipEvent_t ev, hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   int rc = ee_hip(hipStreamIsCapturing(s, &st), "hipStreamIsCapturing");

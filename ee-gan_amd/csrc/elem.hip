@@ -749,6 +749,16 @@ int eegan_global_avgpool_bwd(const void* dy, int dy_f32, int N, int HW, int C, u
   return ee_check_launch("global_avgpool_bwd");
 }
 
+// device time stamp (100 MHz constant clock) for phase timing inside captured graphs
+__global__ void stamp_kernel(unsigned long long* slot) {
+  if (threadIdx.x == 0) *slot = wall_clock64();
+}
+
+int eegan_stamp(unsigned long long* slot, hipStream_t s) {
+  stamp_kernel<<<1, 64, 0, s>>>(slot);
+  return ee_check_launch("stamp");
+}
+
 int eegan_fill_f32(float* x, long n, float v, hipStream_t s) {
   fill_kernel<<<grid_for(n), NT, 0, s>>>(x, n, v);
   return ee_check_launch("fill_f32");

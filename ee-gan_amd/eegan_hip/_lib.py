@@ -41,6 +41,8 @@ _SIGS = {
     'eegan_abi_version': ([], I),
     'eegan_event_create': ([P], I),
     'eegan_event_destroy': ([P], I),
+    'eegan_stream_create': ([P, I], I),
+    'eegan_stream_destroy': ([P], I),
     'eegan_event_record': ([P, P], I),
     'eegan_event_elapsed': ([P, P, P], I),
     'eegan_timing_arm': ([P, P, P, P], I),
@@ -90,6 +92,7 @@ _SIGS = {
     'eegan_global_avgpool': ([P, I, I, I, I, P, I, P], I),
     'eegan_global_avgpool_bwd': ([P, I, I, I, I, P, I, P], I),
     'eegan_fill_f32': ([P, L, F, P], I),
+    'eegan_stamp': ([P, P], I),
     'eegan_gemm_f32': ([P, L, L, P, L, L, P, L, I, I, I, P, I, F, F, P], I),
     'eegan_colsum_f32': ([P, L, I, I, P, I, P], I),
     'eegan_gemm_f32_grouped': ([C.POINTER(GemmDesc), I, P], I),

@@ -89,5 +89,18 @@ def ptr(t):
     return 0 if t is None else t.data_ptr()
 
 
+def new_stream(device, priority=0):
+    """A HIP stream of its own (never recycled: torch.cuda.Stream() hands out
+    pool streams round-robin, so after 32 of them two "different" streams can
+    be one HIP stream and lanes meant to overlap -- or a lane and a capture
+    stream -- alias).  Lives for the process.  priority > 0: the device's
+    highest stream priority, < 0 its lowest."""
+    import ctypes
+    from ._lib import ops
+    h = ctypes.c_void_p()
+    ops.stream_create(ctypes.byref(h), int(priority))
+    return torch.cuda.ExternalStream(h.value, device=device)
+
+
 def workspace(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)

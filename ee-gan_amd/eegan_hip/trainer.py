@@ -18,6 +18,7 @@ from . import functional as Fn
 from . import dist as D
 from . import damsm as G
 from .optim import FlatAdam
+from .tensor import new_stream
 
 
 def prepare_labels(batch_size, device):
@@ -32,6 +33,11 @@ def prepare_class_labels(batch_size, class_num, class_ids, device):
     """train.py:99-103 on the device: labels[i][(id_i - 1) mod class_num] = 1 (bit-exact)."""
     lab, _ = Fn.class_onehot(class_ids, batch_size, class_num, device)
     return lab
+
+
+LANE_PRIO = os.environ.get('EEGAN_LANE_PRIO', '1') != '0'
+# EEGAN_DAMSM_EARLY=0: the DAMSM branch runs inside g_update, after d_update (A/B switch).
+DAMSM_EARLY = os.environ.get('EEGAN_DAMSM_EARLY', '1') != '0'
 
 
 class Trainer(object):
@@ -64,7 +70,11 @@ class Trainer(object):
         if not self.use_streams:
             return [None] * n
         if self._streams is None or len(self._streams) < n:
-            self._streams = [torch.cuda.Stream(device=self.device) for _ in range(n)]
+            # the last discriminator's lane (the largest D: the step's critical
+            # path through d_update and g_update) at high priority, the others
+            # filling around it (EEGAN_LANE_PRIO=0: all default)
+            hi = len(self.netsD) - 1 if LANE_PRIO else -1
+            self._streams = [new_stream(self.device, 1 if i == hi else 0) for i in range(n)]
             for i, st in enumerate(self._streams):
                 D.bind_stream(st, i)   # one RCCL communicator per stream lane
         main = torch.cuda.current_stream()
@@ -175,6 +185,8 @@ class Trainer(object):
         image rows against every rank's captions, the similarity blocks gathered
         (eegan_hip.damsm; damsm_global=False keeps the losses per rank)."""
         region_features, cnn_code = image_encoder(fake_imgs)
+        if Fn.STAMPS is not None:   # diagnostics: when the losses' gradient reaches the image encoder
+            region_features.register_hook(lambda g: (Fn.stamp('dregions ready'), g)[1])
         dev = cnn_code.device
         if self.damsm_global:
             cls = G.global_class_ids(class_ids, dev)
@@ -200,8 +212,10 @@ class Trainer(object):
         streams = self._side_streams(len(self.netsD))
         for i in range(len(self.netsD)):
             with self._on(streams[i]):
+                Fn.stamp('D%d start' % i)
                 self._d_update_one(i, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec)
         self._join(streams)
+        Fn.stamp('d_update joined')
 
     def _d_update_one(self, i, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec):
         """One D of d_update (train.py:439-466)."""
@@ -214,13 +228,19 @@ class Trainer(object):
         else:
             e_real, e_fake, e_unpair = self.d_loss(real_img, fake_img, sent_emb, unpair_sent_emb, netD)
             d_loss = e_real + (e_fake + e_unpair) / 2.0
+        Fn.stamp('D%d loss forward' % i)
         optD.zero_grad()
         d_loss.backward(inputs=optD.params)
+        Fn.stamp('D%d loss backward' % i)
         optD.step()
+        Fn.stamp('D%d adam' % i)
         d_loss_gp = self.MA_gradient_penalty(real_img, sent_emb, netD, disc_class)
+        Fn.stamp('D%d gp forward + grad' % i)
         optD.zero_grad()
         d_loss_gp.backward(inputs=optD.params)
+        Fn.stamp('D%d gp backward' % i)
         optD.step()
+        Fn.stamp('D%d gp adam' % i)
         if iter_rec:
             self.records['errD_%d/real_sent' % i] = e_real.detach()
             self.records['errD_%d/fake_sent' % i] = e_fake.detach()
@@ -231,30 +251,53 @@ class Trainer(object):
                 self.records['errD_%d/fake_class' % i] = c_fake.detach()
                 self.records['errD_%d/mismatch_class' % i] = c_unpair.detach()
 
+    def damsm_early(self, fake_imgs, sent_emb, words_emb, attr_emb, class_ids, batch_size, match_labels, cap_lens):
+        """The DAMSM branch of g_update (image encoder forward + the three
+        matching losses), issued on its own stream lane right after the
+        generator's forward so it runs concurrently with d_update.  It reads
+        only the fake images, the text embeddings and the frozen encoder --
+        nothing d_update changes -- so its values are exactly the ones g_update
+        would compute after d_update (train.py:490); the lane is joined in
+        g_update and the losses enter g_loss there."""
+        streams = self._side_streams(len(self.netsD) + 1)
+        with self._on(streams[-1]):
+            Fn.stamp('DAMSM start')
+            out = self.DAMSM_loss(fake_imgs[-1], sent_emb, words_emb, attr_emb, class_ids, batch_size,
+                                  match_labels, cap_lens, self.image_encoder)
+            Fn.stamp('DAMSM forward')
+        return out
+
     def g_update(self, fake_imgs, sent_emb, words_emb, attr_emb, class_ids, batch_size, match_labels, cap_lens,
-                 class_labels, iter_rec=False):
-        """train.py:471-502."""
+                 class_labels, iter_rec=False, damsm=None):
+        """train.py:471-502 (`damsm`: the losses from damsm_early, else computed here)."""
         nD = len(self.netsD)
         streams = self._side_streams(nD + 1)
         terms = []
         for i in range(nD):
             fake_img, netD = fake_imgs[i], self.netsD[i]
             with self._on(streams[i]):
+                Fn.stamp('gD%d start' % i)
                 if self.disc_class and i == 2:
                     errG, errG_class = self.g_loss_class(fake_img, sent_emb, class_labels, netD)
                     term = errG + errG_class * self.g_class_coe
                 else:
                     errG = self.g_loss(fake_img, sent_emb, netD)
                     term = errG
+                Fn.stamp('gD%d forward' % i)
             terms.append(term)
             if iter_rec:
                 self.records['errG/G_%d_fake_sent' % i] = errG.detach()
                 if self.disc_class and i == 2:
                     self.records['errG/G_%d_fake_class' % i] = errG_class.detach()
-        with self._on(streams[nD]):
-            w_loss, s_loss, a_loss = self.DAMSM_loss(fake_imgs[-1], sent_emb, words_emb, attr_emb, class_ids,
-                                                     batch_size, match_labels, cap_lens, self.image_encoder)
+        if damsm is None:
+            with self._on(streams[nD]):
+                Fn.stamp('DAMSM start')
+                damsm = self.DAMSM_loss(fake_imgs[-1], sent_emb, words_emb, attr_emb, class_ids,
+                                        batch_size, match_labels, cap_lens, self.image_encoder)
+                Fn.stamp('DAMSM forward')
+        w_loss, s_loss, a_loss = damsm
         self._join(streams)
+        Fn.stamp('g_update forwards joined')
         g_loss = terms[0]
         for t in terms[1:]:
             g_loss = g_loss + t
@@ -263,6 +306,9 @@ class Trainer(object):
             self.records['errG/s_loss'] = s_loss.detach()
             self.records['errG/w_loss'] = w_loss.detach()
             self.records['errG/a_loss'] = a_loss.detach()
+        if Fn.STAMPS is not None:   # diagnostics: when each fake image's gradient is complete
+            for i, f in enumerate(fake_imgs):
+                f.register_hook(lambda g, i=i: (Fn.stamp('dfake%d ready' % i), g)[1])
         self.optimizerG.zero_grad()
         # only the optimised parameters' gradients are formed: train.py's
         # g_loss.backward() also fills the D parameters' .grad, but d_update
@@ -270,7 +316,9 @@ class Trainer(object):
         # interpolated-image gradient is never read -- skipping them changes no
         # parameter and saves the D weight-gradient passes
         g_loss.backward(inputs=self.optimizerG.params)
+        Fn.stamp('G backward (D, DAMSM, G)')
         self.optimizerG.step()
+        Fn.stamp('G adam')
         return g_loss.detach()
 
     # -------------------------------------------------------- inner step --
@@ -305,7 +353,9 @@ class Trainer(object):
         """One iteration of train.py:163-206 on a device-resident batch."""
         B = self.batch_size
         dev = self.device
+        Fn.stamp('start')
         words, sent, attrs, unpair = emb if emb is not None else self.encode_text(batch)
+        Fn.stamp('text encode')
         class_labels = None
         if self.disc_class:
             class_labels = prepare_class_labels(B, self.class_nums, batch['cls_ids'], dev)
@@ -314,11 +364,17 @@ class Trainer(object):
         _, attn_attr_emb = self.attr_enhance(sent, attrs)
         attn_attr_emb = self.attr_enhance.module.attr_merge(attn_attr_emb)
         fake_imgs = self.netG(noise, sent, attn_attr_emb)
-        self.d_update(batch['imgs'], fake_imgs, sent, unpair, class_labels, iter_rec)
+        Fn.stamp('ATTR + G forward')
         _, _, match_labels = prepare_labels(B, dev)
         cls_ids = batch.get('cls_ids')  # train.py:490 passes class ids to DAMSM_loss even without USE_CLASS
+        damsm = None
+        if DAMSM_EARLY and self.use_streams:
+            damsm = self.damsm_early(fake_imgs, sent, words, attn_attr_emb, cls_ids, B, match_labels,
+                                     batch['cap_lens'])
+        self.d_update(batch['imgs'], fake_imgs, sent, unpair, class_labels, iter_rec)
         g = self.g_update(fake_imgs, sent, words, attn_attr_emb, cls_ids, B, match_labels, batch['cap_lens'],
-                          class_labels, iter_rec)
+                          class_labels, iter_rec, damsm=damsm)
+        Fn.stamp('end')
         return fake_imgs, g
 
 
@@ -337,7 +393,7 @@ class StepGraph(object):
 
     def __init__(self, trainer, batch, warmup=2, timer=None, **step_kw):
         from . import functional as Fn
-        side = torch.cuda.Stream()
+        side = new_stream(torch.cuda.current_device())
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(warmup):
@@ -349,9 +405,37 @@ class StepGraph(object):
         # gathers, gradient buckets) are captured too; thread-local capture
         # keeps the process group's watchdog thread from invalidating it
         mode = 'thread_local' if D.collective() else 'global'
-        try:
-            with torch.cuda.graph(self.graph, capture_error_mode=mode):
+        def capture():
+            # captured on the stream the warm-up ran on: per-stream side streams
+            # (weight gradients) were created there, outside the capture
+            with torch.cuda.graph(self.graph, stream=side, capture_error_mode=mode):
                 self.out = trainer.train_step(batch, **step_kw)
+
+        try:
+            stack_mb = int(os.environ.get('EEGAN_CAPTURE_STACK_MB', '0'))
+            if stack_mb > 0:
+                # capture + instantiate on a thread with a large stack (the runtime's
+                # graph walk recurses per dependency edge)
+                import threading
+                err = []
+
+                def run():
+                    try:
+                        torch.cuda.set_device(side.device)
+                        capture()
+                    except BaseException as e:  # re-raised on the caller's thread
+                        err.append(e)
+                old = threading.stack_size(stack_mb << 20)
+                try:
+                    th = threading.Thread(target=run)
+                    th.start()
+                    th.join()
+                finally:
+                    threading.stack_size(old)
+                if err:
+                    raise err[0]
+            else:
+                capture()
         finally:
             Fn.TIMER = prev
 

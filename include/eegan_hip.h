@@ -39,6 +39,10 @@ int eegan_event_create(hipEvent_t* ev);
 int eegan_event_destroy(hipEvent_t ev);
 int eegan_event_record(hipEvent_t ev, hipStream_t s);
 int eegan_event_elapsed(hipEvent_t start, hipEvent_t stop, float* ms);
+/* a private non-blocking stream (torch's pool streams are recycled round-robin, so two
+ * torch.cuda.Stream() objects can be the same HIP stream; lanes that must stay distinct use these) */
+int eegan_stream_create(hipStream_t* s, int priority);  /* 0 default, > 0 highest, < 0 lowest */
+int eegan_stream_destroy(hipStream_t s);
 /* arm per-dispatch timing for the next op on this host thread: its first
  * (up to two) kernels launch through hipExtLaunchKernel with (start_i, stop_i),
  * stamped at the dispatch's begin and end; disarm returns how many were used */
@@ -193,6 +197,9 @@ int eegan_avgpool3s1(const uint16_t* x, int N, int H, int W, int C, int ld, uint
 int eegan_global_avgpool(const uint16_t* x, int ld, int N, int HW, int C, void* y, int y_f32, hipStream_t s);
 int eegan_global_avgpool_bwd(const void* dy, int dy_f32, int N, int HW, int C, uint16_t* dx, int lddx, hipStream_t s);
 int eegan_fill_f32(float* x, long n, float v, hipStream_t s);
+/* *slot = the device's 100 MHz wall clock when the stream reaches this point (a one-thread kernel, so it
+ * can sit in a captured graph; diagnostics: tools/stamp_phases.py) */
+int eegan_stamp(unsigned long long* slot, hipStream_t s);
 
 /* ------------------------------------------------------------------ linear --
  * replaces: nn.Linear of models.py:51-60,150-152,188,321 and DAMSM.py:163 (fp32) */
