@@ -193,43 +193,6 @@ class _Stacked1x1:
         return Fn.SplitChannelsFn.apply(y, self.sizes)
 
 
-# Off by default: with the branches on their own streams the step graph's
-# capture crashes inside the HIP runtime (a recursive walk of the captured
-# dependency graph overflows any stack: tools/with_bt.py); EEGAN_INCEPTION_PAR=1.
-PAR_BRANCHES = os.environ.get('EEGAN_INCEPTION_PAR', '0') == '1'
-_BRANCH_STREAMS = {}   # block -> its own branch streams (each stream serves ONE block)
-
-
-def _par(owner, *thunks):
-    """Run an Inception block's independent branches concurrently: the first
-    on the current stream, the others on private streams forked from it,
-    joined back before the concat.  The branches are small convolutions at
-    35x35 / 17x17 / 8x8 (a few hundred workgroups each), so one alone leaves
-    most CUs idle; autograd runs each branch's backward on the stream its
-    forward used, so the backward overlaps the same way.  Same kernels, same
-    per-tensor arithmetic: results are unchanged."""
-    if not PAR_BRANCHES or len(thunks) == 1 or not torch.cuda.is_available():
-        return [f() for f in thunks]
-    main = torch.cuda.current_stream()
-    need = len(thunks) - 1
-    streams = _BRANCH_STREAMS.get(id(owner))
-    if streams is None:
-        if torch.cuda.is_current_stream_capturing():
-            return [f() for f in thunks]   # streams are created outside a capture (the warm-up step)
-        from eegan_hip.tensor import new_stream
-        streams = _BRANCH_STREAMS[id(owner)] = [new_stream(main.device) for _ in range(need)]
-    outs = [None] * len(thunks)
-    for k in range(1, len(thunks)):
-        st = streams[k - 1]
-        st.wait_stream(main)
-        with torch.cuda.stream(st):
-            outs[k] = thunks[k]()
-    outs[0] = thunks[0]()
-    for st in streams:
-        main.wait_stream(st)
-    return outs
-
-
 class InceptionA(nn.Module):
     def __init__(self, in_channels, pool_features):
         super().__init__()
@@ -244,9 +207,9 @@ class InceptionA(nn.Module):
 
     def forward(self, x):
         b1, t5, t3 = self._stem(x)
-        b3, b5, bp = _par(self, lambda: _chain(t3, (self.branch3x3dbl_2, self.branch3x3dbl_3)),
-                          lambda: _chain(t5, (self.branch5x5_2,)),
-                          lambda: self.branch_pool(Fn.AvgPool3s1Fn.apply(x)))
+        b5 = _chain(t5, (self.branch5x5_2,))
+        b3 = _chain(t3, (self.branch3x3dbl_2, self.branch3x3dbl_3))
+        bp = self.branch_pool(Fn.AvgPool3s1Fn.apply(x))
         return _cat([b1, b5, b3, bp])
 
 
@@ -259,10 +222,9 @@ class InceptionB(nn.Module):
         self.branch3x3dbl_3 = BasicConv2d(96, 96, 3, stride=2)
 
     def forward(self, x):
-        bd, b3, mp = _par(self, lambda: _chain(x, (self.branch3x3dbl_1, self.branch3x3dbl_2, self.branch3x3dbl_3)),
-                          lambda: self.branch3x3(x),
-                          lambda: Fn.MaxPool3s2Fn.apply(x))
-        return _cat([b3, bd, mp])
+        b3 = self.branch3x3(x)
+        bd = _chain(x, (self.branch3x3dbl_1, self.branch3x3dbl_2, self.branch3x3dbl_3))
+        return _cat([b3, bd, Fn.MaxPool3s2Fn.apply(x)])
 
 
 class InceptionC(nn.Module):
@@ -283,10 +245,9 @@ class InceptionC(nn.Module):
 
     def forward(self, x):
         b1, t7, td = self._stem(x)
-        bd, b7, bp = _par(self, lambda: _chain(td, (self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4,
-                                              self.branch7x7dbl_5)),
-                          lambda: _chain(t7, (self.branch7x7_2, self.branch7x7_3)),
-                          lambda: self.branch_pool(Fn.AvgPool3s1Fn.apply(x)))
+        b7 = _chain(t7, (self.branch7x7_2, self.branch7x7_3))
+        bd = _chain(td, (self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4, self.branch7x7dbl_5))
+        bp = self.branch_pool(Fn.AvgPool3s1Fn.apply(x))
         return _cat([b1, b7, bd, bp])
 
 
@@ -303,10 +264,9 @@ class InceptionD(nn.Module):
 
     def forward(self, x):
         t3, t7 = self._stem(x)
-        b7, b3, mp = _par(self, lambda: _chain(t7, (self.branch7x7x3_2, self.branch7x7x3_3, self.branch7x7x3_4)),
-                          lambda: _chain(t3, (self.branch3x3_2,)),
-                          lambda: Fn.MaxPool3s2Fn.apply(x))
-        return _cat([b3, b7, mp])
+        b3 = _chain(t3, (self.branch3x3_2,))
+        b7 = _chain(t7, (self.branch7x7x3_2, self.branch7x7x3_3, self.branch7x7x3_4))
+        return _cat([b3, b7, Fn.MaxPool3s2Fn.apply(x)])
 
 
 class InceptionE(nn.Module):
@@ -325,12 +285,10 @@ class InceptionE(nn.Module):
 
     def forward(self, x):
         b1, b3, td = self._stem(x)
-
-        def dbl():
-            bd = self.branch3x3dbl_2(td, defer=True)  # both consumers gate
-            return self.branch3x3dbl_3a(bd, in_relu=True), self.branch3x3dbl_3b(bd, in_relu=True)
-        (bda, bdb), b3a, b3b, bp = _par(self, dbl, lambda: self.branch3x3_2a(b3), lambda: self.branch3x3_2b(b3),
-                                        lambda: self.branch_pool(Fn.AvgPool3s1Fn.apply(x)))
+        b3a, b3b = self.branch3x3_2a(b3), self.branch3x3_2b(b3)
+        bd = self.branch3x3dbl_2(td, defer=True)  # both consumers gate
+        bda, bdb = self.branch3x3dbl_3a(bd, in_relu=True), self.branch3x3dbl_3b(bd, in_relu=True)
+        bp = self.branch_pool(Fn.AvgPool3s1Fn.apply(x))
         return _cat([b1, b3a, b3b, bda, bdb, bp])
 
 

@@ -84,82 +84,6 @@ def _grad_sink(ctx, i):
     return g
 
 
-# Parameter gradients written straight into p.grad (sinks) leave the
-# data-gradient chain: a first-order backward launches them on a side stream
-# of the stream it runs on, where they overlap the next layer's data gradient
-# (small-grid convolutions leave most CUs idle), and the side streams are
-# joined back at the end of the backward pass (autograd final callback) --
-# before any optimizer step or .grad read.  Same kernels, same order per
-# parameter: results are bit-identical.  Opt-in (EEGAN_WGRAD_STREAM=1):
-# measured +1.3 % at C2 (558.9 vs 551.6 img/s, one box), inside the run-to-
-# run spread, and a StepGraph captured after two eager warm-ups with it on
-# crashes in the runtime's capture (one warm-up is fine) -- not investigated.
-WGRAD_STREAM = os.environ.get('EEGAN_WGRAD_STREAM', '0') == '1'
-_SIDE = {}      # stream handle -> its weight-gradient side stream
-_PENDING = {}   # stream handle -> (stream, side) to join at the end of this backward
-
-
-def _join_param_grads():
-    for main, side in _PENDING.values():
-        main.wait_stream(side)
-    _PENDING.clear()
-
-
-class _ParamGradStream(object):
-    """`with _ParamGradStream(x, dz):` runs the sink kernels on the side stream
-    (x, dz: tensors they read, kept alive for it)."""
-
-    def __init__(self, *used):
-        self.used = used
-        self.ctx = None
-
-    def __enter__(self):
-        main = torch.cuda.current_stream()
-        if not WGRAD_STREAM or main.device.type != 'cuda':
-            return self
-        key = main.cuda_stream
-        side = _SIDE.get(key)
-        if side is None:
-            if torch.cuda.is_current_stream_capturing():
-                return self   # no stream creation inside a capture: in line (StepGraph warms up on its capture stream)
-            side = _SIDE[key] = T.new_stream(main.device)
-        if key not in _PENDING:
-            _PENDING[key] = (main, side)
-            torch.autograd.Variable._execution_engine.queue_callback(_join_param_grads)
-        side.wait_stream(main)
-        for t in self.used:
-            if t is not None:
-                t.record_stream(side)
-        self.ctx = torch.cuda.stream(side)
-        self.ctx.__enter__()
-        return self
-
-    def __exit__(self, *exc):
-        if self.ctx is not None:
-            self.ctx.__exit__(*exc)
-        return False
-
-
-def _sink_param_grads(ctx, x, dz, g, W_shape, iw, ib):
-    """First-order backward: dW (input iw) and db (input ib, or None) of a
-    convolution accumulated into their p.grad sinks on the side stream.
-    Returns (w_done, b_done)."""
-    wsink = _grad_sink(ctx, iw) if _needed(ctx, iw) else None
-    if wsink is not None and not wsink.is_contiguous(memory_format=CL):
-        wsink = None
-    bsink = None
-    if ib is not None and ctx.needs_input_grad[ib] and _needed(ctx, ib):
-        bsink = _grad_sink(ctx, ib)
-    if wsink is None and bsink is None:
-        return False, False
-    with _ParamGradStream(x, dz):
-        if wsink is not None:
-            conv_bwd_weight_raw(x, dz, g, W_shape, out=wsink)
-        if bsink is not None:
-            chansum_raw(dz, out=bsink)
-    return wsink is not None, bsink is not None
-
-
 # ============================================================== weights ===
 class PackCache:
     """bf16 packed images of one conv weight (forward and bwd-data layouts),
@@ -462,8 +386,6 @@ class Conv2dFn(torch.autograd.Function):
         fused = FUSE_ACT_BWD and not torch.is_grad_enabled()
         dz = ActBwdFn.apply(gy, y, ctx.act, ctx.slope) if ctx.act and not (fused and ctx.defer_act) else gy
         dx = dW = db = None
-        # parameter gradients first: their side stream then overlaps dx below
-        w_done, b_done = _sink_param_grads(ctx, x, dz, g, W.shape, 1, 2) if not g.up2 else (False, False)
         if _needed(ctx, 0):
             if g.up2:
                 dx = conv_bwd_data_raw(dz, W, g, ctx.x_shape, ctx.cache)
@@ -472,13 +394,13 @@ class Conv2dFn(torch.autograd.Function):
                                        gate_slope=ctx.in_slope)
             else:
                 dx = ConvBwdDataFn.apply(dz, W, g, ctx.x_shape, ctx.cache)
-        if _needed(ctx, 1) and not w_done:
+        if _needed(ctx, 1):
             sink = _grad_sink(ctx, 1)
             if sink is not None and sink.is_contiguous(memory_format=CL):
                 conv_bwd_weight_raw(x, dz, g, W.shape, out=sink)
             else:
                 dW = ConvBwdWeightFn.apply(x, dz, g) if not g.up2 else conv_bwd_weight_raw(x, dz, g, W.shape)
-        if ctx.needs_input_grad[2] and _needed(ctx, 2) and not b_done:
+        if ctx.needs_input_grad[2] and _needed(ctx, 2):
             sink = _grad_sink(ctx, 2)
             if sink is not None:
                 chansum_raw(dz, out=sink)
@@ -518,7 +440,6 @@ class PoolConvFn(torch.autograd.Function):
         if gy is not None:
             gy = _as_bf16_grad(gy)
             dz = ActBwdFn.apply(gy, y, ctx.act, ctx.slope) if ctx.act and not (fused and ctx.defer_act) else gy
-        w_done, b_done = _sink_param_grads(ctx, x, dz, g, W.shape, 1, 2) if dz is not None else (False, False)
         if _needed(ctx, 0):
             if fused and gp is not None and dz is not None:
                 dx = conv_bwd_data_raw(dz, W, g, ctx.x_shape, ctx.cache, res=_as_bf16_grad(gp), res_up2=1,
@@ -530,13 +451,13 @@ class PoolConvFn(torch.autograd.Function):
                 if gp is not None:
                     parts.append(AvgPool2AdjFn.apply(_as_bf16_grad(gp)))
                 dx = parts[0] if len(parts) == 1 else parts[0] + parts[1]
-        if dz is not None and _needed(ctx, 1) and not w_done:
+        if dz is not None and _needed(ctx, 1):
             sink = _grad_sink(ctx, 1)
             if sink is not None and sink.is_contiguous(memory_format=CL):
                 conv_bwd_weight_raw(x, dz, g, W.shape, out=sink)
             else:
                 dW = ConvBwdWeightFn.apply(x, dz, g)
-        if dz is not None and ctx.needs_input_grad[2] and _needed(ctx, 2) and not b_done:
+        if dz is not None and ctx.needs_input_grad[2] and _needed(ctx, 2):
             sink = _grad_sink(ctx, 2)
             if sink is not None:
                 chansum_raw(dz, out=sink)
@@ -557,12 +478,9 @@ class ConvBwdDataFn(torch.autograd.Function):
         dz, W = ctx.saved_tensors
         gdx = _as_bf16_grad(gdx)
         g_dz = g_W = None
-        # dW of the second backward: the side stream, overlapping g_dz
-        w_done, _ = _sink_param_grads(ctx, gdx, dz, ctx.g, W.shape, 1, None) if ctx.needs_input_grad[1] \
-            else (False, False)
         if ctx.needs_input_grad[0]:
             g_dz = Conv2dFn.apply(gdx, W, None, ctx.g, 0, 0.0, False, ctx.cache)
-        if ctx.needs_input_grad[1] and _needed(ctx, 1) and not w_done:
+        if ctx.needs_input_grad[1] and _needed(ctx, 1):
             sink = _grad_sink(ctx, 1)
             if sink is not None and sink.is_contiguous(memory_format=CL):
                 # the gradient penalty's second backward: dW straight into p.grad
