@@ -1519,8 +1519,15 @@ __global__ __launch_bounds__(256) void pack_weights_multi_kernel(const long* __r
     for (int k = t * 8; k < Kw; k += 256 * 8) {
       const int tap = k / Cgp, c = k - tap * Cgp;  // Cgp % 8 == 0: the group stays in one tap
       float v[8];
+      const float* sp = src + tap * Cin + c;
+      if (live && tap < RS && c + 8 <= Cin && ((uintptr_t)sp & 15) == 0) {  // two 16-byte loads
+        const float4 a0 = reinterpret_cast<const float4*>(sp)[0], a1 = reinterpret_cast<const float4*>(sp)[1];
+        v[0] = a0.x * sc; v[1] = a0.y * sc; v[2] = a0.z * sc; v[3] = a0.w * sc;
+        v[4] = a1.x * sc; v[5] = a1.y * sc; v[6] = a1.z * sc; v[7] = a1.w * sc;
+      } else {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = (live && tap < RS && c + u < Cin) ? src[tap * Cin + c + u] * sc : 0.f;
+        for (int u = 0; u < 8; ++u) v[u] = (live && tap < RS && c + u < Cin) ? sp[u] * sc : 0.f;
+      }
       *reinterpret_cast<uint4*>(orow + k) =
           make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
     }

@@ -507,7 +507,8 @@ def test_class_onehot_bit_exact(gpu):
 def test_adam_matches_torch(gpu):
     from eegan_hip.optim import FlatAdam
     torch.manual_seed(13)
-    ps = [torch.nn.Parameter(torch.randn(s, device=gpu)) for s in [(7, 3), (5,), (1,), (33, 2, 3)]]
+    # (1000, 3001): several grid-stride groups per thread and a ragged float4 tail
+    ps = [torch.nn.Parameter(torch.randn(s, device=gpu)) for s in [(7, 3), (5,), (1,), (33, 2, 3), (1000, 3001)]]
     qs = [torch.nn.Parameter(p.detach().clone()) for p in ps]
     opt = FlatAdam(ps, lr=4e-4, betas=(0.0, 0.9))
     ref = torch.optim.Adam(qs, lr=4e-4, betas=(0.0, 0.9))
@@ -534,13 +535,17 @@ def test_flat_adam_repacks_conv_weights(gpu):
     m1 = Conv2d(3, 40, 3, 1, 1).to(gpu)
     m2 = Conv2d(40, 136, 4, 2, 1).to(gpu)
     m3 = Conv2d(136, 3, 1, 1, 0).to(gpu)
-    mods = (m1, m2, m3)
+    m4 = Conv2d(3, 192, 1, 1, 0).to(gpu)      # 192 output channels: three 64-wide bwd-image column tiles
+    m5 = Conv2d(256, 160, 4, 2, 1).to(gpu)    # 16-byte forward-image loads, multi-tile bwd image, 16 taps
+    mods = (m1, m2, m3, m4, m5)
     opt = FlatAdam([p for m in mods for p in m.parameters()], lr=1e-2, betas=(0.0, 0.9))
     for _ in range(2):
         opt.zero_grad()
         x = _nhwc(_bf(torch.randn(2, 3, 8, 8)), gpu).requires_grad_()
         y = m3(m2(m1(x, act='lrelu')))
-        y.backward(torch.ones_like(y))
+        z = m5(_nhwc(_bf(torch.randn(2, 256, 8, 8)), gpu))
+        u = m4(x)
+        (y.float().sum() + z.float().sum() + u.float().sum()).backward()
         opt.step()
     for m in mods:
         c = m._cache

@@ -58,7 +58,7 @@ def run(args):
         json.dump({'names': names, 'reps': args.reps}, f)
 
 
-TOP = 14
+TOP = int(os.environ.get("LANE_TOP", "14"))
 
 
 def report(d):
