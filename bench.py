@@ -112,7 +112,11 @@ def cpu_baseline(seconds_budget=30.0):
     import models
     import DAMSM
     affinity = len(os.sched_getaffinity(0))
-    torch.set_num_threads(affinity)
+    # the host cores this process may use: the affinity set, capped by the
+    # scheduler's share when the environment states one (OMP_NUM_THREADS: the
+    # GPU box's affinity mask spans the whole machine, its CPU share is 16)
+    share = int(os.environ.get('OMP_NUM_THREADS') or 0)
+    torch.set_num_threads(min(affinity, share) if share > 0 else affinity)
     B, W, ncls = 4, 32, 200
     spec = lambda m: [(k, tuple(v.shape)) for k, v in m.state_dict().items()]  # noqa: E731
     sd_e = seeded_state(spec(DAMSM.CNN_ENCODER(256)), 9)
@@ -136,14 +140,20 @@ def cpu_baseline(seconds_budget=30.0):
                                                                       models.Dis256(W, True, ncls)][:nd])]
         nets = O.OracleNets(sd_g, sd_a, sd_ds, W, W, True, ncls)
         og, ods = O.make_adams(nets)
-        for _ in range(2):  # warm-ups
+        for k in range(2):  # warm-ups
+            t0 = time.time()
             O.train_step(nets, og, ods, batch, encode_text(), enc, stages=stages)
+            print('bench: cpu baseline (%d stage%s) warm-up %d: %.1f s' % (stages, 's' if stages > 1 else '', k,
+                                                                        time.time() - t0), file=sys.stderr, flush=True)
         times = []
         t_end = time.time() + budget
         while len(times) < 10 and (time.time() < t_end or len(times) < 3):
             t0 = time.time()
             O.train_step(nets, og, ods, batch, encode_text(), enc, stages=stages)
             times.append(time.time() - t0)
+            print('bench: cpu baseline (%d stage%s) step %d: %.1f s' % (stages, 's' if stages > 1 else '',
+                                                                      len(times), times[-1]), file=sys.stderr,
+                  flush=True)
         times.sort()
         return B / times[len(times) // 2], len(times)
 
