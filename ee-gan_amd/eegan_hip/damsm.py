@@ -53,6 +53,9 @@ def global_class_ids(class_ids, device):
     return D.all_gather(ids, differentiable=False)
 
 
+WORDS_PAD = 32   # csrc/damsm.hip NW: the widest caption the words kernel takes
+
+
 def words_block(regions, words_emb, cap_lens, want_att=False):
     """(sim B_global x B_global, att maps of this rank's matching pairs)."""
     dev = regions.device
@@ -60,6 +63,14 @@ def words_block(regions, words_emb, cap_lens, want_att=False):
     off = 0
     if D.collective():
         off = D.rank() * regions.shape[0]
+        # every rank's words padded to the kernel's 32-word width before the
+        # gather: a rank's T is ITS batch's longest caption, so the ranks'
+        # tensors would differ in size; the padding is zeros past each
+        # caption's length -- what the reference's pad_packed_sequence gives
+        # the global batch -- and the kernel masks those positions anyway
+        T = words_emb.shape[2]
+        if T < WORDS_PAD:
+            words_emb = torch.nn.functional.pad(words_emb, (0, WORDS_PAD - T))
         words_emb = gather_texts(words_emb)
         lens = gather_texts(lens)
     sim, att = Fn.WordsSimFn.apply(regions, words_emb, lens, want_att, off)

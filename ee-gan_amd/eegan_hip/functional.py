@@ -71,7 +71,31 @@ def _needed(ctx, i):
 DIRECT_PARAM_GRADS = True
 
 
+_PENDING_SINKS = set()   # FlatAdam objects holding buckets completed by this Function's writes
+
+
+def _commit_sinks():
+    """After a Function's backward has launched its kernels: issue the
+    all-reduces of the buckets its direct gradient writes completed (same
+    stream, so they follow the writes)."""
+    while _PENDING_SINKS:
+        _PENDING_SINKS.pop().flush_ready()
+
+
 def _grad_sink(ctx, i):
+    g = _sink_of(ctx, i)
+    var = getattr(ctx.next_functions[i][0], 'variable', None) if ctx.next_functions[i][0] is not None else None
+    tr = getattr(var, '_eegan_track', None) if var is not None else None
+    if tr is not None:   # FlatAdam's overlapped all-reduce counts the writes
+        if g is not None:
+            if tr.note_grad_write(var):
+                _PENDING_SINKS.add(tr)
+        else:
+            tr.note_autograd_write(var)   # this gradient goes through autograd's accumulation instead
+    return g
+
+
+def _sink_of(ctx, i):
     if not DIRECT_PARAM_GRADS or torch.is_grad_enabled():
         return None
     node = ctx.next_functions[i][0]
@@ -81,6 +105,8 @@ def _grad_sink(ctx, i):
     g = var.grad
     if g is None or g.dtype != F32 or g.shape != var.shape or g.stride() != var.stride():
         return None
+    if g.dim() == 4 and not g.is_contiguous(memory_format=CL):
+        return None   # conv weight gradients are written channels-last only
     return g
 
 
@@ -1640,3 +1666,23 @@ def class_onehot(class_ids, B, ncls, device):
     err = torch.zeros(1, dtype=torch.int32, device=device)
     ops.class_onehot(ids.data_ptr(), B, ncls, out.data_ptr(), err.data_ptr(), stream())
     return out, err
+
+
+def _commit_after_backward(cls):
+    f = cls.backward
+
+    def backward(ctx, *grads):
+        out = f(ctx, *grads)
+        if _PENDING_SINKS:
+            _commit_sinks()
+        return out
+    backward.__doc__ = f.__doc__
+    cls.backward = staticmethod(backward)
+
+
+# every Function of this module: a bucket completed by the direct gradient
+# writes of a backward is reduced once that backward has launched them all
+for _cls in list(globals().values()):
+    if isinstance(_cls, type) and issubclass(_cls, torch.autograd.Function) and _cls.__module__ == __name__ \
+            and 'backward' in _cls.__dict__:
+        _commit_after_backward(_cls)

@@ -10,7 +10,24 @@ gradient reduction).  After each step a generation counter shared by the
 parameters is bumped and every conv weight's bf16 packs (forward and
 backward-data images, eegan_hip.functional.PackCache) are rebuilt in ONE
 batched launch, so no per-layer pack kernel runs in the next forward/backward.
+
+Overlap (world > 1 on the default group): the flat gradient is reduced in
+buckets of parameters taken in REVERSE registration order -- the order a
+backward completes them -- and a bucket's all-reduce is issued during the
+backward, on the stream that wrote its last gradient, as soon as every
+parameter in it has received all of its gradient writes.  The kernels write
+parameter gradients straight into the flat buffer (functional._grad_sink),
+which reports each write here; how many writes a parameter receives in one
+zero_grad..step window (1 in a first-order backward, 2 for a conv weight in
+the gradient penalty's second-order backward) is learned from the first
+window of its kind (keyed by the first parameter written) and then required:
+a window that writes a parameter more often than its plan raises.  Buckets
+holding a parameter whose gradient arrives any other way (autograd's own
+accumulation) are reduced at step(), as are all buckets of an unlearned
+window.  EEGAN_GRAD_OVERLAP=0 reduces everything at step().
 """
+import os
+
 import torch
 
 from ._lib import ops
@@ -21,9 +38,12 @@ def _align(n, a=4):
     return (n + a - 1) // a * a
 
 
+OVERLAP = os.environ.get('EEGAN_GRAD_OVERLAP', '1') != '0'
+
+
 class FlatAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, process_group=None,
-                 bucket_bytes=64 << 20):
+                 bucket_bytes=16 << 20):
         params = [p for p in params]
         seen, uniq = set(), []
         for p in params:
@@ -33,7 +53,6 @@ class FlatAdam(torch.optim.Optimizer):
         super().__init__(uniq, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.process_group = process_group
         self.params = uniq  # the leaves this optimiser updates (backward(inputs=...))
-        self.bucket_elems = max(1, bucket_bytes // 4)
         dev = uniq[0].device
         offs, n = [], 0
         for p in uniq:
@@ -62,36 +81,150 @@ class FlatAdam(torch.optim.Optimizer):
         self._pack_total = 0
         self.step_count = 0   # host mirror (state_dict); the kernels use step_dev
         self.step_dev = torch.zeros(1, dtype=torch.float64, device=dev)
+        self._index = {id(p): i for i, p in enumerate(uniq)}
+        self._offs = offs
+        self.set_bucket_bytes(bucket_bytes)
+        self._plans = {}         # window key -> (writes per param, early-eligible bucket flags)
+        self._late = set()       # params whose gradient went through autograd at least once
+        self._win = None
+
+    # ------------------------------------------------------ overlapped DP --
+    def set_bucket_bytes(self, nbytes):
+        """Reduction buckets: parameter index ranges in reverse registration
+        order, >= nbytes each (the last one may be smaller)."""
+        self.bucket_elems = max(1, nbytes // 4)
+        self.buckets = []       # (lo, hi): params [lo, hi), flat range [offs[lo], end of hi-1)
+        hi, acc = len(self.params), 0
+        for i in range(len(self.params) - 1, -1, -1):
+            acc += _align(self.params[i].numel())
+            if acc >= self.bucket_elems or i == 0:
+                self.buckets.append((i, hi))
+                hi, acc = i, 0
+        self._bucket_of = [0] * len(self.params)
+        for b, (lo, hi) in enumerate(self.buckets):
+            for i in range(lo, hi):
+                self._bucket_of[i] = b
+        self._plans = {}
+
+    def _dp(self):
+        import torch.distributed as dist
+        from . import dist as D
+        if self.process_group is None or not dist.is_initialized():
+            return 0
+        world = dist.get_world_size(self.process_group)
+        if world == 1 and not D.FORCE:
+            return 0
+        return world
+
+    def _flat_range(self, b):
+        lo, hi = self.buckets[b]
+        return self._offs[lo], self._offs[hi - 1] + _align(self._views[hi - 1][2])
+
+    def _reduce_bucket(self, b):
+        import torch.distributed as dist
+        from . import dist as D
+        s, e = self._flat_range(b)
+        if self.process_group is dist.group.WORLD:
+            D.all_reduce(self.gflat[s:e])
+        else:
+            dist.all_reduce(self.gflat[s:e], group=self.process_group)
+        self._win['done'][b] = True
+
+    def flush_ready(self):
+        """Reduce the buckets completed by writes that are launched by now
+        (called by functional once the writing Function's backward returned)."""
+        w = self._win
+        if w is None:
+            return
+        for b in w['ready']:
+            self._reduce_bucket(b)
+        w['ready'] = []
+
+    def note_grad_write(self, p):
+        """A kernel is about to accumulate into p.grad (functional._grad_sink).
+        True when this write completes a bucket (reduced by flush_ready)."""
+        w = self._win
+        if w is None:
+            return False
+        i = self._index[id(p)]
+        if w['key'] is None:
+            w['key'] = i
+            w['plan'] = self._plans.get(i)
+            if w['plan'] is not None:
+                need, early = w['plan']
+                w['left'] = [sum(1 for j in range(lo, hi) if need[j] > 0) if early[b] else -1
+                             for b, (lo, hi) in enumerate(self.buckets)]
+        w['counts'][i] += 1
+        if w['plan'] is None:
+            return False
+        need, early = w['plan']
+        c = w['counts'][i]
+        if c > need[i]:
+            raise RuntimeError('FlatAdam: parameter %d received %d gradient writes in a window planned for %d '
+                               '(overlapped all-reduce would have read it early)' % (i, c, need[i]))
+        b = self._bucket_of[i]
+        if c == need[i] and early[b]:
+            w['left'][b] -= 1
+            if w['left'][b] == 0:
+                w['ready'].append(b)
+                return True
+        return False
 
     def zero_grad(self, set_to_none=False):
         ops.fill_f32(self.gflat.data_ptr(), self.numel, 0.0, stream())
         for p, o, k, g in self._views:
             if p.grad is None or p.grad.data_ptr() != g.data_ptr():
                 p.grad = g
+        if OVERLAP and self._dp() and self.process_group is not None:
+            import torch.distributed as dist
+            if self.process_group is dist.group.WORLD:
+                self._win = {'key': None, 'plan': None, 'counts': [0] * len(self.params), 'ready': [],
+                             'done': [False] * len(self.buckets), 'left': None}
+                for p in self.params:
+                    p._eegan_track = self
+
+    def note_autograd_write(self, p):
+        """A kernel Function hands p's gradient to autograd's accumulation
+        (no direct write): p's bucket is never reduced early."""
+        i = self._index[id(p)]
+        self._late.add(i)
+        w = self._win
+        if w is not None and w['done'][self._bucket_of[i]]:
+            raise RuntimeError('FlatAdam: parameter %d accumulated by autograd after its bucket was reduced' % i)
 
     def _sync_grads(self):
         # gradients that autograd produced out of place (or dropped) are folded back in
-        for p, o, k, g in self._views:
+        for i, (p, o, k, g) in enumerate(self._views):
             if p.grad is None:
                 p.grad = g
                 g.zero_()
             elif p.grad.data_ptr() != g.data_ptr():
                 g.copy_(p.grad)
                 p.grad = g
+                self._late.add(i)
 
     def _allreduce(self):
-        import torch.distributed as dist
-        from . import dist as D
-        if self.process_group is None or not dist.is_initialized() or (
-                dist.get_world_size(self.process_group) == 1 and not D.FORCE):
+        world = self._dp()
+        if not world:
             return
-        world = dist.get_world_size(self.process_group)
-        world_pg = self.process_group is dist.group.WORLD
-        for s in range(0, self.numel, self.bucket_elems):
-            if world_pg:
-                D.all_reduce(self.gflat[s:s + self.bucket_elems])
-            else:
-                dist.all_reduce(self.gflat[s:s + self.bucket_elems], group=self.process_group)
+        w = self._win
+        if w is None:   # no overlap: every bucket now
+            self._win = w = {'key': None, 'plan': None, 'counts': [0] * len(self.params), 'ready': [],
+                             'done': [False] * len(self.buckets), 'left': None}
+        self.flush_ready()
+        late_buckets = {self._bucket_of[i] for i in self._late}
+        if any(w['done'][b] for b in late_buckets):
+            raise RuntimeError('FlatAdam: a bucket with an out-of-place gradient was reduced early')
+        for b in range(len(self.buckets)):   # everything not reduced during the backward, in bucket order
+            if not w['done'][b]:
+                self._reduce_bucket(b)
+        if w['key'] is not None and w['key'] not in self._plans:   # learn this window's write counts
+            need = list(w['counts'])
+            early = [all(need[j] > 0 and j not in self._late for j in range(lo, hi)) for lo, hi in self.buckets]
+            self._plans[w['key']] = (need, early)
+        self._win = None
+        for p in self.params:
+            p._eegan_track = None
         self.gflat.mul_(1.0 / world)
 
     @torch.no_grad()

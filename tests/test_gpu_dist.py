@@ -59,3 +59,29 @@ def test_dropin_train_step_two_ranks(gpu, tmp_path, monkeypatch):
         worst = max(worst, e)
         assert e < 2e-2, (k, e)
     print('DP2 worst post-step parameter rel-L2 vs one process: %.3e' % worst)
+
+
+def test_flat_adam_overlapped_allreduce_two_ranks(gpu, tmp_path):
+    """The trainer path (FlatAdam) at N = 2 on one GPU (gloo): gradient
+    buckets all-reduced during the backward (EEGAN_GRAD_OVERLAP=1, default)
+    give parameters bit-identical to reducing everything at step() (=0), the
+    two ranks agree, and the overlap actually happened (buckets reduced from
+    inside the backward for every optimizer of the second step)."""
+    res = {}
+    for tag, ov in (('ov', '1'), ('seq', '0')):
+        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+               '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
+               os.path.join(HERE, 'dp_trainer_worker.py'), str(tmp_path), tag]
+        env = dict(os.environ, OMP_NUM_THREADS='2', EEGAN_GRAD_OVERLAP=ov)
+        r = subprocess.run(cmd, env=env, timeout=240, capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        res[tag] = [torch.load(os.path.join(tmp_path, 'rank%d_%s.pt' % (i, tag))) for i in range(2)]
+    for tag in res:
+        for a, b in zip(res[tag][0]['params'], res[tag][1]['params']):
+            assert torch.equal(a, b), tag
+    for a, b in zip(res['ov'][0]['params'], res['seq'][0]['params']):
+        assert torch.equal(a, b)
+    print('overlap: buckets reduced inside backward per optimizer', res['ov'][0]['early'],
+          'of', res['ov'][0]['buckets'])
+    assert all(e > 0 for e in res['ov'][0]['early']), res['ov'][0]['early']
+    assert all(e == 0 for e in res['seq'][0]['early'])

@@ -543,7 +543,7 @@ def test_flat_adam_repacks_conv_weights(gpu):
         opt.zero_grad()
         x = _nhwc(_bf(torch.randn(2, 3, 8, 8)), gpu).requires_grad_()
         y = m3(m2(m1(x, act='lrelu')))
-        z = m5(_nhwc(_bf(torch.randn(2, 256, 8, 8)), gpu))
+        z = m5(_nhwc(_bf(torch.randn(2, 256, 8, 8)), gpu).requires_grad_())
         u = m4(x)
         (y.float().sum() + z.float().sum() + u.float().sum()).backward()
         opt.step()
