@@ -89,6 +89,19 @@ def pmc_family(kind):
     return fam, 'profiles/' + os.path.basename(files[-1])
 
 
+def conv_path_hbm_frac():
+    """Whole conv path (fwd + bwd-data + wgrad families): PMC HBM bytes over
+    kernel time over the 8 TB/s peak, from the newest profiles/rNN_families.json."""
+    tot_b = tot_s = 0.0
+    for k in ('conv_fwd', 'conv_bwd_data', 'conv_bwd_weight'):
+        f, _ = pmc_family(k)
+        if not f.get('hbm_bytes_per_call') or not f.get('calls'):
+            return None
+        tot_b += f['hbm_bytes_per_call'] * f['calls']
+        tot_s += f['total_ms'] * 1e-3
+    return round(tot_b / tot_s / 1e9 / HBM_PEAK_GBS, 4) if tot_s else None
+
+
 def _cpu_model():
     try:
         with open('/proc/cpuinfo') as f:
@@ -274,6 +287,11 @@ def main():
             'algorithmic_hbm_GBs': round(nb / tsec / 1e9, 1),
             'mfma_busy': pf.get('mfma_util'),
             'mfma_busy_unit': 'SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE per XCD x 1024 SIMDs), rocprofv3 PMC',
+            # north_star's conv-path HBM figure: PMC FETCH+WRITE bytes over kernel time, / 8 TB/s
+            'pmc_hbm_GBs': round(traffic / pf['avg_call_us'] / 1e3, 1) if traffic and pf.get('avg_call_us') else None,
+            'pmc_hbm_frac': round(traffic / pf['avg_call_us'] / 1e3 / HBM_PEAK_GBS, 4)
+            if traffic and pf.get('avg_call_us') else None,
+            'conv_path_pmc_hbm_frac': conv_path_hbm_frac(),
             'families': {k: {'ms_per_step': round(v[3] / per * 1e3, 3),
                              'TFLOPs': round(v[1] / max(v[3], 1e-12) / 1e12, 1)} for k, v in kern.items()}}
     out = {'metric': 'train images/sec at 256x256 CUB, G+D step', 'value': round(value, 3), 'unit': 'images/sec',

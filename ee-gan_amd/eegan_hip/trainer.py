@@ -36,6 +36,8 @@ def prepare_class_labels(batch_size, class_num, class_ids, device):
 
 
 LANE_PRIO = os.environ.get('EEGAN_LANE_PRIO', '1') != '0'
+# EEGAN_G_EARLY=0: g_update's passes through the three D's wait for all of d_update.
+G_EARLY = os.environ.get('EEGAN_G_EARLY', '1') != '0'
 # EEGAN_DAMSM_EARLY=0: the DAMSM branch runs inside g_update, after d_update (A/B switch).
 DAMSM_EARLY = os.environ.get('EEGAN_DAMSM_EARLY', '1') != '0'
 
@@ -207,15 +209,25 @@ class Trainer(object):
         return (w[0] + w[1]) * lam, (s[0] + s[1]) * lam, (a[0] + a[1]) * lam
 
     # ----------------------------------------------------------- updates --
-    def d_update(self, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec=False):
-        """train.py:437-469: per D a hinge(+class) step, then a GP step (each D on its own stream)."""
+    def d_update(self, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec=False, g_early=None):
+        """train.py:437-469: per D a hinge(+class) step, then a GP step (each D
+        on its own stream).  `g_early` (a list): also run g_update's generator
+        loss term through each D right after that D's update, into the list."""
         streams = self._side_streams(len(self.netsD))
+        g_terms = []
         for i in range(len(self.netsD)):
             with self._on(streams[i]):
                 Fn.stamp('D%d start' % i)
                 self._d_update_one(i, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec)
+                if g_early is not None:
+                    # g_update's pass through this D (train.py:477-489) reads only this D's
+                    # final parameters and the fake images: it runs on the lane as soon as
+                    # the update is done, while the larger D's update still runs
+                    g_terms.append(self._g_term(i, fake_imgs, sent_emb, class_labels, iter_rec))
         self._join(streams)
         Fn.stamp('d_update joined')
+        if g_early is not None:
+            g_early[:] = g_terms
 
     def _d_update_one(self, i, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec):
         """One D of d_update (train.py:439-466)."""
@@ -267,28 +279,34 @@ class Trainer(object):
             Fn.stamp('DAMSM forward')
         return out
 
+    def _g_term(self, i, fake_imgs, sent_emb, class_labels, iter_rec):
+        """The generator's adversarial term through D i (train.py:477-489)."""
+        fake_img, netD = fake_imgs[i], self.netsD[i]
+        Fn.stamp('gD%d start' % i)
+        if self.disc_class and i == 2:
+            errG, errG_class = self.g_loss_class(fake_img, sent_emb, class_labels, netD)
+            term = errG + errG_class * self.g_class_coe
+        else:
+            errG = self.g_loss(fake_img, sent_emb, netD)
+            term = errG
+        Fn.stamp('gD%d forward' % i)
+        if iter_rec:
+            self.records['errG/G_%d_fake_sent' % i] = errG.detach()
+            if self.disc_class and i == 2:
+                self.records['errG/G_%d_fake_class' % i] = errG_class.detach()
+        return term
+
     def g_update(self, fake_imgs, sent_emb, words_emb, attr_emb, class_ids, batch_size, match_labels, cap_lens,
-                 class_labels, iter_rec=False, damsm=None):
-        """train.py:471-502 (`damsm`: the losses from damsm_early, else computed here)."""
+                 class_labels, iter_rec=False, damsm=None, terms=None):
+        """train.py:471-502 (`damsm`: the losses from damsm_early, `terms`: the
+        per-D terms from d_update(g_early=...); else computed here)."""
         nD = len(self.netsD)
         streams = self._side_streams(nD + 1)
-        terms = []
-        for i in range(nD):
-            fake_img, netD = fake_imgs[i], self.netsD[i]
-            with self._on(streams[i]):
-                Fn.stamp('gD%d start' % i)
-                if self.disc_class and i == 2:
-                    errG, errG_class = self.g_loss_class(fake_img, sent_emb, class_labels, netD)
-                    term = errG + errG_class * self.g_class_coe
-                else:
-                    errG = self.g_loss(fake_img, sent_emb, netD)
-                    term = errG
-                Fn.stamp('gD%d forward' % i)
-            terms.append(term)
-            if iter_rec:
-                self.records['errG/G_%d_fake_sent' % i] = errG.detach()
-                if self.disc_class and i == 2:
-                    self.records['errG/G_%d_fake_class' % i] = errG_class.detach()
+        if not terms:
+            terms = []
+            for i in range(nD):
+                with self._on(streams[i]):
+                    terms.append(self._g_term(i, fake_imgs, sent_emb, class_labels, iter_rec))
         if damsm is None:
             with self._on(streams[nD]):
                 Fn.stamp('DAMSM start')
@@ -371,9 +389,10 @@ class Trainer(object):
         if DAMSM_EARLY and self.use_streams:
             damsm = self.damsm_early(fake_imgs, sent, words, attn_attr_emb, cls_ids, B, match_labels,
                                      batch['cap_lens'])
-        self.d_update(batch['imgs'], fake_imgs, sent, unpair, class_labels, iter_rec)
+        terms = [] if (G_EARLY and self.use_streams) else None
+        self.d_update(batch['imgs'], fake_imgs, sent, unpair, class_labels, iter_rec, g_early=terms)
         g = self.g_update(fake_imgs, sent, words, attn_attr_emb, cls_ids, B, match_labels, batch['cap_lens'],
-                          class_labels, iter_rec, damsm=damsm)
+                          class_labels, iter_rec, damsm=damsm, terms=terms)
         Fn.stamp('end')
         return fake_imgs, g
 
