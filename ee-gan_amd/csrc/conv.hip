@@ -80,6 +80,7 @@ struct ConvArgs {
   int gate_vec;  // same for the activation gate
   int red_vec4;  // split-K reduce: 4-channel vector path (host-checked alignment)
   int res_vec;  // res rows 8-byte aligned (ldres % 4 == 0, aligned base): vector residual loads
+  int wide;     // conv_fast_kernel pairs: one 64-channel stage of whole 128-B lines per K-step pair
 };
 
 // K step kt, 8-channel chunk kc -> kernel tap and channel.  Normal mode: the
@@ -645,11 +646,13 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
   const int rsub = tid >> 2;
   const int kc8 = ((tid & 3) ^ swz_b128((tid >> 4) & 3)) * 8;  // swizzled 8-channel chunk of this thread
   const int ld2 = a.lds_src * 2;
-  int pb[B_INS];
-  unsigned vm[B_INS];
-#pragma unroll
-  for (int i = 0; i < B_INS; ++i) {
-    const int p = pix0 + i * 64 + rsub;
+  // wide pair stages: 128-B rows (8 chunks), this thread's row tid / 8 (+ 32 i) and
+  // physical chunk tid & 7 holding logical chunk (tid & 7) ^ ((row >> 1) & 7)
+  constexpr bool WIDE_OK = VAR == 2 && KS == 2 && TCO >= 64;
+  const bool wide = WIDE_OK && a.wide;
+  const int wrow = tid >> 3;
+  const int wkc8 = ((tid & 7) ^ ((wrow >> 1) & 7)) * 8;
+  auto pix_state = [&](int p, int kcb, int& pbo, unsigned& vmo) {
     const bool ok = p < Pc;
     const int pp = ok ? p : 0;
     const int hw = CH * CW;
@@ -674,12 +677,26 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
         if ((unsigned)ix < (unsigned)a.IW) m |= 1u << (ta * TS + tb);
       }
     }
-    vm[i] = ok ? m : 0u;
-    pb[i] = ((n * a.IH + y0) * a.IW + x0) * ld2 + kc8 * 2;
-  }
+    vmo = ok ? m : 0u;
+    pbo = ((n * a.IH + y0) * a.IW + x0) * ld2 + kcb * 2;
+  };
+  int pb[B_INS];
+  unsigned vm[B_INS];
   unsigned aoff[A_INS];
+  constexpr int B_INW = WIDE_OK ? TPIX / 32 : 1, A_INW = WIDE_OK ? TCO / 32 : 1;  // 16-B chunks / 256 threads
+  int pbw[B_INW];
+  unsigned vmw[B_INW], aoffw[A_INW];
+  if (!wide) {
 #pragma unroll
-  for (int i = 0; i < A_INS; ++i) aoff[i] = (unsigned)(((co0 + i * 64 + rsub) * a.Kw + kc8) * 2);
+    for (int i = 0; i < B_INS; ++i) pix_state(pix0 + i * 64 + rsub, kc8, pb[i], vm[i]);
+#pragma unroll
+    for (int i = 0; i < A_INS; ++i) aoff[i] = (unsigned)(((co0 + i * 64 + rsub) * a.Kw + kc8) * 2);
+  } else {
+#pragma unroll
+    for (int i = 0; i < B_INW; ++i) pix_state(pix0 + i * 32 + wrow, wkc8, pbw[i], vmw[i]);
+#pragma unroll
+    for (int i = 0; i < A_INW; ++i) aoffw[i] = (unsigned)(((co0 + i * 32 + wrow) * a.Kw + wkc8) * 2);
+  }
 
   const rsrc_t rs_src = make_rsrc(a.src, src_bytes);
   const rsrc_t rs_w = make_rsrc(a.wp, w_bytes);
@@ -723,6 +740,38 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
     }
   };
 
+  // one wide stage = ring slots (sp, sp + 1): A rows then B rows of 128 B, the
+  // pair's two 32-channel slices side by side
+  auto issue_wide = [&](int sp) {
+    const int t = w_ta * TS + w_tb;
+    const int c = w_cs * BK;
+    int toff, kw;
+    if (MODE == MODE_FWD) {
+      toff = (w_ta * IW + w_tb) * ld2 + c * 2;
+      kw = (w_ta * a.S + w_tb) * a.Cgp + c;
+    } else {
+      toff = c * 2 - (w_ta * IW + w_tb) * ld2;
+      kw = ((r0 + a.st * w_ta) * a.S + s0 + a.st * w_tb) * a.Cgp + c;
+    }
+    const int cv = a.Cvalid - c;
+    const int base = lds0 + sp * (STAGE * 2);
+#pragma unroll
+    for (int i = 0; i < A_INW; ++i) lds_dma16s(rs_w, base + (i * 256 + wave * 64) * 16, aoffw[i], kw * 2);
+#pragma unroll
+    for (int i = 0; i < B_INW; ++i) {
+      const bool ok = ((vmw[i] >> t) & 1u) && wkc8 < cv;
+      const unsigned off = ok ? (unsigned)(pbw[i] + toff) : OOB;
+      lds_dma16s(rs_src, base + TCO * 2 * BK * 2 + (i * 256 + wave * 64) * 16, off, 0);
+    }
+    w_cs += 2;  // both slices of this tap (even slice count per tap)
+    if (w_cs == nc) {
+      w_cs = 0;
+      if (++w_tb == TS) {
+        w_tb = 0;
+        ++w_ta;
+      }
+    }
+  };
   f32x4_t acc[FI][FJ];
 #pragma unroll
   for (int i = 0; i < FI; ++i)
@@ -735,9 +784,28 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
   // slots multiplied in the previous iteration
   constexpr int YNG = S - 2 * KS;  // stages allowed in flight at the wait
   static_assert(YNG >= 0, "stages");
+  if (wide) {
+    if (nk > 0) issue_wide(0);   // stages 0 and 1 (S - KS == 2)
+  } else {
 #pragma unroll
-  for (int st = 0; st < S - KS; ++st)
-    if (st < nk) issue(st);
+    for (int st = 0; st < S - KS; ++st)
+      if (st < nk) issue(st);
+  }
+  auto rd_frags_wide = [&](int sp, int half, bf16x8_t (&fa_)[FI], bf16x8_t (&fb_)[FJ]) {
+    const bf16_t* base = lds + sp * STAGE;
+    const int q = 4 * half + fq;
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const int row = wi * WT_CO + i * 16 + fr;
+      fa_[i] = as_frag(*reinterpret_cast<const uint4*>(base + row * 2 * BK + ((q ^ ((row >> 1) & 7)) * 8)));
+    }
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const int row = wj * WT_PIX + j * 16 + fr;
+      fb_[j] = as_frag(*reinterpret_cast<const uint4*>(base + TCO * 2 * BK + row * 2 * BK +
+                                                        ((q ^ ((row >> 1) & 7)) * 8)));
+    }
+  };
   auto rd_frags = [&](int stage, bf16x8_t (&fa_)[FI], bf16x8_t (&fb_)[FJ]) {
     const bf16_t* base = lds + stage * STAGE;
 #pragma unroll
@@ -763,11 +831,17 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
       } else {
         wait_vmcnt_barrier<0>();
       }
-      if (it0 + S - 2 < nk) issue((it0 + S - 2) % S);
-      if (it0 + S - 1 < nk) issue((it0 + S - 1) % S);
       bf16x8_t fa0[FI], fb0[FJ], fa1[FI], fb1[FJ];
-      rd_frags(it0 % S, fa0, fb0);
-      rd_frags((it0 + 1) % S, fa1, fb1);
+      if (wide) {
+        if (it0 + S - 2 < nk) issue_wide((it0 + S - 2) % S);
+        rd_frags_wide(it0 % S, 0, fa0, fb0);
+        rd_frags_wide(it0 % S, 1, fa1, fb1);
+      } else {
+        if (it0 + S - 2 < nk) issue((it0 + S - 2) % S);
+        if (it0 + S - 1 < nk) issue((it0 + S - 1) % S);
+        rd_frags(it0 % S, fa0, fb0);
+        rd_frags((it0 + 1) % S, fa1, fb1);
+      }
 #pragma unroll
       for (int i = 0; i < FI; ++i)
 #pragma unroll
@@ -2023,6 +2097,16 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   const int ksv = env_int("EEGAN_CONV_KS", 22);  // 22: pairs, interleaved reads; 2: pairs; 1: single steps
   a.nsplit = p.nsplit;
   a.part = p.nsplit > 1 ? part_ws : nullptr;
+  {
+    // wide pair stages (whole 128-B lines: 64 channels per pixel / weight row): an
+    // even number of 32-channel slices per tap and every split starting on a pair
+    const int nc = a.Cgp / BK;
+    int taps_max = a.R * a.S;
+    if (MODE == MODE_BWDD && a.st > 1) taps_max = ee_cdiv(a.R, a.st) * ee_cdiv(a.S, a.st);
+    const int nk_max = taps_max * nc;
+    const int kchunk = ee_cdiv(nk_max, p.nsplit);
+    a.wide = p.tco >= 64 && nc % 2 == 0 && kchunk % 2 == 0 && env_int("EEGAN_CONV_WIDE", 1);
+  }
   if (p.nsplit > 1 && !part_ws) {
     ee_set_error("conv: split-K workspace missing");
     return -22;

@@ -185,6 +185,47 @@ def test_splitk_reduce_vector_path_bit_identical(gpu, monkeypatch):
             assert torch.equal(a, c)
 
 
+@pytest.mark.parametrize('target', ['512', '4096'])
+def test_conv_wide_stages_bit_identical(gpu, monkeypatch, target):
+    """Wide pair stages (one 64-channel stage of whole 128-B lines per K-step
+    pair, EEGAN_CONV_WIDE=1, default) against two 32-channel stages (=0): same
+    K order and MFMA sequence, so torch.equal -- forward with bias / act /
+    residual + gain and fp32 out, backward-data with gate, the
+    half-resolution residual and stride-2 parity classes, channel counts with
+    padded 64-channel pairs (72, 200), with and without split-K."""
+    Fn, T, _ = _mods()
+    monkeypatch.setenv('EEGAN_CONV_TARGET', target)
+    monkeypatch.setenv('EEGAN_CONV_MINK', '2')
+    lrelu = Fn.ACT_CODES['lrelu']
+    for N, Cin, H, W, Cout, k, st, pad in [(2, 64, 16, 16, 128, 3, 1, 1), (3, 128, 9, 11, 64, 3, 1, 1),
+                                            (2, 96, 16, 16, 256, 4, 2, 1), (2, 64, 12, 12, 200, 1, 1, 0),
+                                            (4, 256, 8, 8, 72, 3, 1, 1), (2, 128, 16, 16, 96, 4, 2, 1),
+                                            (2, 72, 10, 10, 128, 3, 1, 1), (2, 200, 8, 8, 64, 3, 1, 1)]:
+        torch.manual_seed(N * Cin + Cout + H)
+        g = Fn.Geom(Cout, k, k, st, pad, pad, 0)
+        x = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        Wt = (torch.randn(Cout, Cin, k, k) * 0.05).to(gpu)
+        b = torch.randn(Cout).to(gpu)
+        gam = torch.tensor([0.7]).to(gpu)
+        Ho, Wo = g.out_hw(H, W)
+        res = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
+        dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
+        gate = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        halfres = _nhwc(torch.randn(N, Cin, H // 2, W // 2), gpu) if H % 2 == 0 and W % 2 == 0 else None
+        outs = []
+        for wide in ('0', '1'):
+            monkeypatch.setenv('EEGAN_CONV_WIDE', wide)
+            o = [Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, res=res, gamma=gam).float().cpu(),
+                 Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, out_f32=True).cpu(),
+                 Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), gate=gate, gate_act=lrelu).float().cpu()]
+            if halfres is not None:
+                o.append(Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), res=halfres, res_up2=1,
+                                              res_scale=0.25).float().cpu())
+            outs.append(o)
+        for a, c in zip(*outs):
+            assert torch.equal(a, c), (N, Cin, H, W, Cout, k, st)
+
+
 def test_cat_channels(gpu):
     """Inception branch concat (one launch when every part has C % 8 == 0,
     else the per-part path) against torch.cat, with strided (sliced) parts."""
