@@ -3,7 +3,10 @@
 trainer, settings alternated R times, each setting captured into its own
 StepGraph and timed over K replays.  Comparing within one process removes
 the per-process spread (~541 vs ~575 img/s between processes
-of one build).  Knobs must be read at launch time (the conv planner's are).
+of one build).  Knobs must be read at launch time (the conv planner's are;
+module constants such as EEGAN_DAMSM_EARLY are read at import and cannot be
+switched this way).  The order of the settings rotates every repetition (the
+clock drifts over a run: a fixed order biases the comparison).
 
     python tools/ab_inproc.py "EEGAN_CONV_MINK=32" ["EEGAN_CONV_MINK=8" ...] [--reps 3] [--steps 20]
 """
@@ -38,7 +41,7 @@ def main():
     res = {s: [] for s in settings}
     base_env = dict(os.environ)
     for rep in range(args.reps):
-        for s in settings:
+        for s in settings[rep % len(settings):] + settings[:rep % len(settings)]:
             os.environ.clear()
             os.environ.update(base_env)
             if s != 'base':
