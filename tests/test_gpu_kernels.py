@@ -200,7 +200,8 @@ def test_conv_wide_stages_bit_identical(gpu, monkeypatch, target):
     for N, Cin, H, W, Cout, k, st, pad in [(2, 64, 16, 16, 128, 3, 1, 1), (3, 128, 9, 11, 64, 3, 1, 1),
                                             (2, 96, 16, 16, 256, 4, 2, 1), (2, 64, 12, 12, 200, 1, 1, 0),
                                             (4, 256, 8, 8, 72, 3, 1, 1), (2, 128, 16, 16, 96, 4, 2, 1),
-                                            (2, 72, 10, 10, 128, 3, 1, 1), (2, 200, 8, 8, 64, 3, 1, 1)]:
+                                            (2, 72, 10, 10, 128, 3, 1, 1), (2, 200, 8, 8, 64, 3, 1, 1),
+                                            (2, 32, 32, 32, 64, 4, 2, 1), (2, 24, 16, 16, 64, 3, 1, 1)]:
         torch.manual_seed(N * Cin + Cout + H)
         g = Fn.Geom(Cout, k, k, st, pad, pad, 0)
         x = _nhwc(torch.randn(N, Cin, H, W), gpu)
