@@ -1905,6 +1905,230 @@ __global__ __launch_bounds__(256, 3) void conv_thin_lds_kernel(ConvArgs a, int s
   }
 }
 
+// ------------------------------------------------------------ 1x1 convs --
+// Pointwise convs (and their data gradients, again pointwise) with <= 256
+// padded input channels: resD's learned shortcut conv_s (models.py:274) at
+// every resolution, get_mask's 100 -> 1 projection (models.py:39).  A plain
+// streaming GEMM over pixels: the tile kernels spend one LDS ring fill, one
+// barrier-paced K-step or two and an epilogue per 64..256-pixel tile on these
+// 1..8-K-step shapes (35 TFLOP/s, 1.6 TB/s at C32 -> K64).  Here a wave keeps
+// its 16 NT output rows' weights (NT x NKS A fragments) in VGPRs and streams
+// 16-pixel groups, each B fragment (8 channels of one pixel, 16 B) loaded
+// straight into the lane that feeds it to the MFMA, the next groups' loads in
+// flight during this group's MFMAs and stores; blockIdx.y picks the 16 NT-row
+// slice of the output channels.  K order = the packed row (32-channel steps),
+// as the tile kernels: bit-identical to their unsplit result.  Epilogue = theirs.
+template <int MODE, int NT, int NKS, int GPI>
+__global__ __launch_bounds__(256) void conv_1x1_kernel(ConvArgs a, int iters_per_block, int src_bytes) {
+  const int lane = threadIdx.x & 63, kg = lane >> 4, col = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (b & 7) * (nb >> 3) + (b >> 3);  // XCD-contiguous logical block (nb % 8 == 0)
+  const int co0 = blockIdx.y * 16 * NT;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, src_bytes, 0x00020000);
+  bf16x8_t fa[NT][NKS];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      fa[t][ks] = as_frag(*reinterpret_cast<const uint4*>(a.wp + (long)(co0 + 16 * t + col) * a.Kw + 32 * ks + 8 * kg));
+  // chunks at or past the valid channels read zeros (OOB offset); the one
+  // straddling Cvalid is masked after the loads were issued
+  const int ld2 = a.lds_src * 2;
+  int c_off[NKS];
+  uint4 cm[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int c = 32 * ks + 8 * kg;
+    c_off[ks] = c < a.Cvalid ? c * 2 : -1;
+    cm[ks] = mask_chunk(make_uint4(~0u, ~0u, ~0u, ~0u), c, a.Cvalid);
+  }
+  const int it0 = lb * iters_per_block, it_end = it0 + iters_per_block;
+  auto load = [&](uint4 (&bv)[GPI][NKS], int it) {
+#pragma unroll
+    for (int g = 0; g < GPI; ++g) {
+      const int p = (it * GPI + g) * 16 + col;
+      const bool pok = it < it_end && p < a.P;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const int off = (pok && c_off[ks] >= 0) ? p * ld2 + c_off[ks] : (int)0x80000000;
+        bv[g][ks] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      }
+    }
+  };
+  auto compute = [&](uint4 (&bv)[GPI][NKS], int it) {
+#pragma unroll
+    for (int g = 0; g < GPI; ++g) {
+      f32x4_t acc[NT][1];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t][0] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        uint4 v = bv[g][ks];
+        v.x &= cm[ks].x;
+        v.y &= cm[ks].y;
+        v.z &= cm[ks].z;
+        v.w &= cm[ks].w;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t][ks], as_frag(v), acc[t][0], 0, 0, 0);
+      }
+      const int pix0 = (it * GPI + g) * 16;
+      if (it < it_end && pix0 < a.P)
+        igemm_epilogue<MODE, NT, 1, 16 * NT, 16>(a, acc, pix0, co0, 0, 0, lane, 0, a.P, a.OH, a.OW, 0, 0, 1);
+    }
+  };
+  uint4 b0[GPI][NKS], b1[GPI][NKS];
+  int it = it0 + wv;
+  load(b0, it);
+  for (; it < it_end; it += 8) {
+    load(b1, it + 4);
+    compute(b0, it);
+    if (it + 4 >= it_end) break;
+    load(b0, it + 8);
+    compute(b1, it + 4);
+  }
+}
+
+// ------------------------------------------ stride-2 backward-data, halo --
+// Data gradient of the 4x4 / stride-2 / pad-1 convs with <= 32 input channels:
+// resD.conv_r[0] of every discriminator's first block (models.py:267, fin =
+// ndf, at the D's full resolution).  The tile kernels run it as four parity
+// classes, each re-gathering its 2x2 taps of dy through L2 (16 gathers of every
+// dy pixel over the classes; 0.74 TB/s).  Here one workgroup owns a TH x TW tile
+// of the class grid for ALL four classes: the (TH + 2) x (TW + 2) dy halo they
+// share is staged once in LDS by LDS-DMA, and wave w computes class
+// (w >> 1, w & 1) from it, its 2x2-tap weight slab (NT x 4 NC A fragments)
+// held in VGPRs.  K order = the tile kernels' (tap-major, 32-channel slices),
+// so the fp32 sums are bit-identical to the unsplit tile kernel's.
+// Epilogue: a class's pixels are every other dx pixel, so storing straight
+// from the MFMA layout writes 32-B pieces at a 128-B stride (measured: the
+// stores took 60 % of the kernel).  Instead each class row pair lands as fp32
+// in an LDS staging image of two dx rows x 2 TW pixels, and the workgroup
+// writes it out as whole 16-B runs of 8 channels (gate and residual applied
+// there, in fp32, then rounded once -- as the tile kernels' epilogue).
+// Class (qy, qx) with pad 1: first tap r0 = (qy + 1) & 1, dy row = i + qy - ta.
+constexpr int S2B_TH = 4, S2B_TW = 32;
+
+template <int NT, int NC>
+__global__ __launch_bounds__(256, 2) void conv_s2bwd_lds_kernel(ConvArgs a, int src_bytes, int tiles_per_block) {
+  constexpr int NCH = NC * 4;  // 16-B chunks per staged dy pixel
+  constexpr int TH = S2B_TH, TW = S2B_TW, PWT = TW + 2, NPIX = (TH + 2) * PWT, NCHUNK = NPIX * NCH;
+  constexpr int NDMA = (NCHUNK + 255) / 256;
+  constexpr int NKS = 4 * NC;  // 2 x 2 taps x NC 32-channel slices
+  constexpr int SPX = 2 * 2 * TW;  // staged dx pixels per class row (2 dx rows x 2 TW columns)
+  __shared__ uint4 tile[NDMA * 256];
+  __shared__ float4 stage[2][SPX * 8];  // [buffer][pixel][8 fp32 chunks of 4 channels], chunk-swizzled
+  const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4, col = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int qy = wv >> 1, qx = wv & 1;
+  const int r0 = (qy + 1) & 1, s0 = (qx + 1) & 1;
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (b & 7) * (nb >> 3) + (b >> 3);  // XCD-contiguous logical block (nb % 8 == 0)
+  const rsrc_t rsv = make_rsrc(a.src, src_bytes);
+  auto swz = [](int pix, int c) { return NCH == 8 ? c ^ ((pix >> 1) & 7) : c ^ ((pix >> 1) & 2); };
+  bf16x8_t fa[NT][NKS];
+  int t_off[NKS], t_ch[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int tap = ks / NC, cs = ks - tap * NC, ta = tap >> 1, tb = tap & 1;
+    const int r = r0 + 2 * ta, s = s0 + 2 * tb;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      fa[t][ks] = as_frag(*reinterpret_cast<const uint4*>(a.wp + (long)(16 * t + col) * a.Kw + (r * 4 + s) * a.Cgp +
+                                                          32 * cs + 8 * kg));
+    t_off[ks] = (qy - ta + 1) * PWT + (qx - tb + 1);
+    t_ch[ks] = cs * 4 + kg;
+  }
+  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
+  const int C8 = a.Mrows >> 3;  // 8-channel output runs per pixel (Mrows % 8 == 0, host-checked)
+  const int CH = a.OH >> 1, CW = a.OW >> 1;
+  const int tiles_x = CW / TW, tiles_y = CH / TH, tiles = a.N * tiles_x * tiles_y;
+  const int t0 = lb * tiles_per_block, t1 = min(t0 + tiles_per_block, tiles);
+  int sb = 0;
+  for (int tt = t0; tt < t1; ++tt) {
+    const int n = tt / (tiles_x * tiles_y), rem = tt - n * tiles_x * tiles_y;
+    const int i0 = (rem / tiles_x) * TH, j0 = (rem - (rem / tiles_x) * tiles_x) * TW;
+    __syncthreads();  // the previous tile's fragment reads are done
+#pragma unroll
+    for (int i = 0; i < NDMA; ++i) {
+      const int sl = i * 256 + wv * 64 + lane;  // LDS slot this lane's piece lands in
+      const int pix = sl / NCH, phys = sl - pix * NCH;
+      const int pr = pix / PWT, pq = pix - pr * PWT;
+      const int iy = i0 - 1 + pr, ix = j0 - 1 + pq;
+      const bool ok = sl < NCHUNK && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
+      const int off = (((n * a.IH + iy) * a.IW + ix) * a.lds_src + swz(pix, phys) * 8) * 2;
+      if (!(a.noload & 1)) lds_dma16(rsv, &tile[i * 256 + wv * 64], ok ? (unsigned)off : 0x80000000u);
+    }
+    wait_vmcnt_barrier<0>();
+#pragma unroll 1
+    for (int rr = 0; rr < TH; ++rr) {
+      f32x4_t acc[TW / 16][NT];
+#pragma unroll
+      for (int g = 0; g < TW / 16; ++g) {
+        const int q = 16 * g + col;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[g][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          const int pix = rr * PWT + q + t_off[ks];
+          const bf16x8_t v = as_frag(tile[pix * NCH + swz(pix, t_ch[ks])]);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t][ks], v, acc[g][t], 0, 0, 0);
+        }
+      }
+      // stage: lane (col, kg) of tile t holds channels 16 t + 4 kg .. + 3 of dx pixel
+      // (row qy, column 2 (16 g + col) + qx); 4-channel chunk index 4 t + kg
+#pragma unroll
+      for (int g = 0; g < TW / 16; ++g)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int sp = qy * 2 * TW + 2 * (16 * g + col) + qx;
+          stage[sb][sp * 8 + ((4 * t + kg) ^ ((sp >> 1) & 7))] =
+              make_float4(acc[g][t][0], acc[g][t][1], acc[g][t][2], acc[g][t][3]);
+        }
+      __syncthreads();
+      if (a.noload & 2) {  // diagnostics: skip the global stores
+        sb ^= 1;
+        continue;
+      }
+      const int y0 = 2 * (i0 + rr), x0 = 2 * j0;
+#pragma unroll
+      for (int k = 0; k < (SPX * 4 + 255) / 256; ++k) {
+        const int item = tid + 256 * k, sp = item >> 2, e = item & 3;
+        if (sp >= SPX || e >= C8) continue;
+        const float4 lo = stage[sb][sp * 8 + ((2 * e) ^ ((sp >> 1) & 7))];
+        const float4 hi = stage[sb][sp * 8 + ((2 * e + 1) ^ ((sp >> 1) & 7))];
+        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        const int y = y0 + sp / (2 * TW), x = x0 + sp % (2 * TW);
+        const long p = ((long)n * a.OH + y) * a.OW + x;
+        if (a.gate) {
+          const uint4 gv = *reinterpret_cast<const uint4*>(a.gate + p * a.ldgate + 8 * e);
+          const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[2 * j] *= act_dgrad_from_y(lo_f(gw[j]), a.gate_act, a.gate_slope);
+            v[2 * j + 1] *= act_dgrad_from_y(hi_f(gw[j]), a.gate_act, a.gate_slope);
+          }
+        }
+        if (a.res) {
+          const long rp = a.res_up2 ? ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1) : p;
+          const uint4 rv = *reinterpret_cast<const uint4*>(a.res + rp * a.ldres + 8 * e);
+          const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[2 * j] = a.res_scale * lo_f(rw[j]) + gam * v[2 * j];
+            v[2 * j + 1] = a.res_scale * hi_f(rw[j]) + gam * v[2 * j + 1];
+          }
+        }
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + p * a.ldo + 8 * e) =
+            make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+      }
+      sb ^= 1;  // the next row pair stages into the other buffer (one barrier per row pair)
+    }
+  }
+}
+
 // ---------------------------------------------------- thin weight gradient --
 // dW of 3x3 stride-1 pad-1 convs with <= 8 output channels and 32 or 64
 // (padded) input channels: get_image (ngf * {1, 2} -> 3, models.py:25-32),
@@ -2089,9 +2313,79 @@ int try_thin(const ConvArgs& a, hipStream_t s, long src_bytes) {
   return rc ? rc : 1;
 }
 
+// 4x4 / stride-2 / pad-1 data gradients with <= 32 input channels take
+// conv_s2bwd_lds_kernel (0: not eligible, else the launch rc as try_thin)
+int try_s2bwd(const ConvArgs& a, hipStream_t s, long src_bytes) {
+  if (!env_int("EEGAN_CONV_S2B", 1) || src_bytes >= 0x7fffffffL) return 0;
+  if (a.R != 4 || a.S != 4 || a.st != 2 || a.ph != 1 || a.pw != 1 || a.ncls != 4 || a.up2 || a.Mrows > 32) return 0;
+  if ((a.Cgp != 32 && a.Cgp != 64) || a.Cvalid != a.Cgp || (a.lds_src & 7) || ((uintptr_t)a.src & 15)) return 0;
+  // LDS-staged epilogue: bf16 output, 16-B runs of 8 channels (output / gate / residual rows 16-B aligned)
+  if (a.out_f32 || a.bias || a.act != ACT_NONE || (a.Mrows & 7) || (a.ldo & 7) || ((uintptr_t)a.out & 15)) return 0;
+  if (a.gate && ((a.ldgate & 7) || ((uintptr_t)a.gate & 15))) return 0;
+  if (a.res && ((a.ldres & 7) || ((uintptr_t)a.res & 15))) return 0;
+  if ((a.OH & 1) || (a.OW & 1) || (a.OW / 2) % S2B_TW || (a.OH / 2) % S2B_TH) return 0;
+  if ((long)a.N * a.OH * a.OW >= 0x7fffffffL) return 0;
+  const int tiles = a.N * (a.OW / 2 / S2B_TW) * (a.OH / 2 / S2B_TH);
+  const int nbl = ee_round_up(std::min(tiles, env_int("EEGAN_CONV_S2B_BLOCKS", 512)), 8);
+  const int tpb = (tiles + nbl - 1) / nbl;
+  const int nt = a.Mrows > 16 ? 2 : 1;
+  ConvArgs a2 = a;
+  a2.noload = env_int("EEGAN_CONV_NOLOAD", 0);  // diagnostics: 1 no halo DMA, 2 no epilogue
+#define SB(NT, NC) ee_launch(conv_s2bwd_lds_kernel<NT, NC>, dim3(nbl), dim3(256), 0, s, a2, (int)src_bytes, tpb)
+  if (a.Cgp == 64) { if (nt == 2) SB(2, 2); else SB(1, 2); }
+  else { if (nt == 2) SB(2, 1); else SB(1, 1); }
+#undef SB
+  const int rc = ee_check_launch("conv_bwd_data(s2-halo)");
+  return rc ? rc : 1;
+}
+
+// 1x1 stride-1 convs with <= 256 packed K columns take conv_1x1_kernel
+// (0: not eligible, else the launch rc as try_thin)
+template <int MODE>
+int try_1x1(const ConvArgs& a, hipStream_t s, long src_bytes) {
+  if (!env_int("EEGAN_CONV_1X1", 1) || src_bytes >= 0x7fffffffL) return 0;
+  if (a.R != 1 || a.S != 1 || a.st != 1 || a.ph || a.pw || a.ncls != 1 || a.up2 || a.Kw > 256) return 0;
+  if ((a.lds_src & 7) || ((uintptr_t)a.src & 15)) return 0;
+  const int nks = a.Kw / BK;
+  const int nt_max = nks <= 2 ? 8 : nks == 4 ? 4 : 2;
+  int nt = 1;
+  while (nt < nt_max && 16 * nt < a.Mrows) nt *= 2;
+  const int rowblocks = ee_cdiv(a.Mrows, 16 * nt);
+  constexpr int G1 = 1;  // groups per wave iteration (larger: more loads in flight, but the
+  const int gpi = G1;    // epilogue unrolled per group costs VGPRs: 247 at NT = 4, GPI = 4)
+  const long iters = ((a.P + 15L) / 16 + gpi - 1) / gpi;
+  const int cap = std::max(64, env_int("EEGAN_CONV_1X1_BLOCKS", 1024) / rowblocks);
+  const int nb = ee_round_up((int)std::min<long>((iters + 3) / 4, cap), 8);
+  const int ipb = (int)((iters + nb - 1) / nb);
+  const dim3 grid(nb, rowblocks);
+#define P1(NT, NKS, G) ee_launch(conv_1x1_kernel<MODE, NT, NKS, G>, grid, dim3(256), 0, s, a, ipb, (int)src_bytes)
+  switch (nks * 16 + nt) {
+    case 16 + 1: P1(1, 1, G1); break;
+    case 16 + 2: P1(2, 1, G1); break;
+    case 16 + 4: P1(4, 1, G1); break;
+    case 16 + 8: P1(8, 1, G1); break;
+    case 32 + 1: P1(1, 2, G1); break;
+    case 32 + 2: P1(2, 2, G1); break;
+    case 32 + 4: P1(4, 2, G1); break;
+    case 32 + 8: P1(8, 2, G1); break;
+    case 64 + 1: P1(1, 4, 1); break;
+    case 64 + 2: P1(2, 4, 1); break;
+    case 64 + 4: P1(4, 4, 1); break;
+    case 128 + 1: P1(1, 8, 1); break;
+    case 128 + 2: P1(2, 8, 1); break;
+    default: return 0;
+  }
+#undef P1
+  const int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd(1x1)" : "conv_bwd_data(1x1)");
+  return rc ? rc : 1;
+}
+
 template <int MODE>
 int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src_bytes) {
   if (const int th = try_thin<MODE>(a, s, src_bytes)) return th > 0 ? 0 : th;
+  if (const int pw = try_1x1<MODE>(a, s, src_bytes)) return pw > 0 ? 0 : pw;
+  if (MODE == MODE_BWDD)
+    if (const int sb = try_s2bwd(a, s, src_bytes)) return sb > 0 ? 0 : sb;
   Plan p = plan_igemm(a, Pc_max);
   a.noload = env_int("EEGAN_CONV_NOLOAD", 0);
   const int ksv = env_int("EEGAN_CONV_KS", 22);  // 22: pairs, interleaved reads; 2: pairs; 1: single steps

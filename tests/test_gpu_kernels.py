@@ -227,6 +227,89 @@ def test_conv_wide_stages_bit_identical(gpu, monkeypatch, target):
             assert torch.equal(a, c), (N, Cin, H, W, Cout, k, st)
 
 
+def test_conv_s2bwd_halo_bit_identical(gpu, monkeypatch):
+    """4x4 / stride-2 / pad-1 data gradients with <= 32 input channels (resD
+    block0's conv_r[0]) take the shared-halo parity-class kernel
+    (EEGAN_CONV_S2B=1, default): same K order as the unsplit tile kernel
+    (EEGAN_CONV_TARGET=1 keeps it unsplit), so torch.equal -- plain, gated and
+    with the half-resolution pooled-shortcut residual; 16/20/32 input and
+    32/64 output channels, one- and multi-tile grids; also against torch fp32."""
+    Fn, T, _ = _mods()
+    monkeypatch.setenv('EEGAN_CONV_TARGET', '1')
+    lrelu = Fn.ACT_CODES['lrelu']
+    for N, Cin, H, W, Cout in [(2, 32, 64, 64, 64), (3, 16, 8, 64, 32), (1, 24, 16, 128, 64),
+                               (2, 32, 24, 192, 32), (5, 32, 8, 64, 64)]:
+        torch.manual_seed(N * Cin + Cout + H)
+        g = Fn.Geom(Cout, 4, 4, 2, 1, 1, 0)
+        Wt = _bf(torch.randn(Cout, Cin, 4, 4) * 0.05)
+        Ho, Wo = g.out_hw(H, W)
+        dzl = _bf(torch.randn(N, Cout, Ho, Wo))
+        dz = _nhwc(dzl, gpu)
+        gate = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        halfres = _nhwc(torch.randn(N, Cin, H // 2, W // 2), gpu)
+        outs = []
+        for s2b in ('0', '1'):
+            monkeypatch.setenv('EEGAN_CONV_S2B', s2b)
+            outs.append([Fn.conv_bwd_data_raw(dz, Wt.to(gpu), g, (N, Cin, H, W)).float().cpu(),
+                         Fn.conv_bwd_data_raw(dz, Wt.to(gpu), g, (N, Cin, H, W), gate=gate,
+                                              gate_act=lrelu).float().cpu(),
+                         Fn.conv_bwd_data_raw(dz, Wt.to(gpu), g, (N, Cin, H, W), res=halfres, res_up2=1,
+                                              res_scale=0.25).float().cpu()])
+        for a, c in zip(*outs):
+            assert torch.equal(a, c), (N, Cin, H, W, Cout)
+        xr = torch.zeros(N, Cin, H, W, requires_grad=True)
+        F.conv2d(xr, Wt, None, 2, 1).backward(dzl)
+        assert rel_l2(outs[1][0], xr.grad) < 1e-2
+
+
+def test_conv_1x1_stream_bit_identical(gpu, monkeypatch):
+    """1x1 convs with <= 256 packed K columns (resD's conv_s, get_mask's
+    100 -> 1 projection) and their data gradients take the streaming pointwise
+    kernel (EEGAN_CONV_1X1=1, default): same K order as the unsplit tile kernel
+    (EEGAN_CONV_TARGET=1), so torch.equal -- forward with bias / act / residual
+    + gain and fp32 out, backward-data plain, gated and with the
+    half-resolution residual; channel counts that straddle a 16-B chunk (100),
+    one-channel operands (the packed 8-channel K row) and several output-row
+    slices per pixel group; also against torch fp32."""
+    Fn, T, _ = _mods()
+    monkeypatch.setenv('EEGAN_CONV_TARGET', '1')
+    lrelu = Fn.ACT_CODES['lrelu']
+    for N, Cin, H, W, Cout in [(2, 32, 16, 24, 64), (3, 64, 8, 8, 128), (2, 100, 12, 10, 1), (2, 1, 8, 8, 100),
+                               (2, 256, 4, 4, 512), (1, 128, 6, 6, 256), (2, 24, 5, 7, 40), (2, 200, 4, 4, 72)]:
+        torch.manual_seed(N * Cin + Cout + H)
+        g = Fn.Geom(Cout, 1, 1, 1, 0, 0, 0)
+        xl = _bf(torch.randn(N, Cin, H, W))
+        x = _nhwc(xl, gpu)
+        Wt = _bf(torch.randn(Cout, Cin, 1, 1) * 0.1)
+        b = torch.randn(Cout).to(gpu)
+        gam = torch.tensor([0.7]).to(gpu)
+        res = _nhwc(torch.randn(N, Cout, H, W), gpu)
+        dzl = _bf(torch.randn(N, Cout, H, W))
+        dz = _nhwc(dzl, gpu)
+        gate = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        even = H % 2 == 0 and W % 2 == 0
+        halfres = _nhwc(torch.randn(N, Cin, H // 2, W // 2), gpu) if even else None
+        Wd = Wt.to(gpu)
+        outs = []
+        for on in ('0', '1'):
+            monkeypatch.setenv('EEGAN_CONV_1X1', on)
+            o = [Fn.conv_fwd_raw(x, Wd, b, g, act=lrelu, res=res, gamma=gam).float().cpu(),
+                 Fn.conv_fwd_raw(x, Wd, b, g, act=lrelu, out_f32=True).cpu(),
+                 Fn.conv_fwd_raw(x, Wd, None, g).float().cpu(),
+                 Fn.conv_bwd_data_raw(dz, Wd, g, (N, Cin, H, W)).float().cpu(),
+                 Fn.conv_bwd_data_raw(dz, Wd, g, (N, Cin, H, W), gate=gate, gate_act=lrelu).float().cpu()]
+            if halfres is not None:
+                o.append(Fn.conv_bwd_data_raw(dz, Wd, g, (N, Cin, H, W), res=halfres, res_up2=1,
+                                              res_scale=0.25).float().cpu())
+            outs.append(o)
+        for a, c in zip(*outs):
+            assert torch.equal(a, c), (N, Cin, H, W, Cout)
+        assert rel_l2(outs[1][2], F.conv2d(xl, Wt)) < 1e-2
+        xr = xl.clone().requires_grad_()
+        F.conv2d(xr, Wt).backward(dzl)
+        assert rel_l2(outs[1][3], xr.grad) < 1e-2
+
+
 def test_cat_channels(gpu):
     """Inception branch concat (one launch when every part has C % 8 == 0,
     else the per-part path) against torch.cat, with strided (sliced) parts."""

@@ -37,6 +37,11 @@ SHAPES = {
     'stem_3_256x32': (32, 3, 256, 256, 32, 3, 1, 1),
     'img_32_256': (16, 32, 256, 256, 3, 3, 1, 1),
     'c3x3_32_128': (16, 32, 128, 128, 32, 3, 1, 1),
+    'c1x1_32_128': (16, 32, 128, 128, 64, 1, 1, 0),
+    'c1x1_64_64': (16, 64, 64, 64, 128, 1, 1, 0),
+    'c1x1_128_32': (16, 128, 32, 32, 256, 1, 1, 0),
+    'c1x1_256_4': (16, 256, 4, 4, 512, 1, 1, 0),
+    'c1x1_100_128': (16, 100, 128, 128, 1, 1, 1, 0),
 }
 
 
