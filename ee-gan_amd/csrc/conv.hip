@@ -48,6 +48,11 @@ EE_DEV uint4 mask_chunk(uint4 v, int c, int cvalid) {
   return v;
 }
 
+// out = res_scale * res + gamma * v with one explicit rounding order, so the
+// direct, LDS-staged and split-K epilogues agree bit for bit (left to
+// -ffp-contract the compiler fuses either product, differently per site)
+EE_DEV float res_combine(float rs, float r, float g, float v) { return __builtin_fmaf(g, v, rs * r); }
+
 struct ConvArgs {
   const bf16_t* src;   // FWD: x ; BWDD: dy
   const bf16_t* wp;    // packed weights [rows_pad][Kw], K = (tap, channel padded to Cgp)
@@ -81,6 +86,7 @@ struct ConvArgs {
   int red_vec4;  // split-K reduce: 4-channel vector path (host-checked alignment)
   int res_vec;  // res rows 8-byte aligned (ldres % 4 == 0, aligned base): vector residual loads
   int wide;     // conv_fast_kernel pairs: one 64-channel stage of whole 128-B lines per K-step pair
+  int stage_epi;  // conv_fast_kernel: LDS-staged epilogue (unsplit bf16 output, 16-B aligned rows; host-checked)
 };
 
 // K step kt, 8-channel chunk kc -> kernel tap and channel.  Normal mode: the
@@ -180,11 +186,11 @@ EE_DEV void igemm_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], int 
           const uint2 rv = *reinterpret_cast<const uint2*>(rp);
           const float rr[4] = {lo_f(rv.x), hi_f(rv.x), lo_f(rv.y), hi_f(rv.y)};
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = a.res_scale * rr[r] + gam * v[r];
+          for (int r = 0; r < 4; ++r) v[r] = res_combine(a.res_scale, rr[r], gam, v[r]);
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (co + r < a.Mrows) v[r] = a.res_scale * bf2f(rp[r]) + gam * v[r];
+            if (co + r < a.Mrows) v[r] = res_combine(a.res_scale, bf2f(rp[r]), gam, v[r]);
         }
       }
       if (a.out_f32) {
@@ -203,6 +209,83 @@ EE_DEV void igemm_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], int 
         }
       }
     }
+  }
+}
+
+// LDS-staged form of igemm_epilogue for conv_fast_kernel (unsplit, bf16 out,
+// Mrows % 8 == 0, output / gate / residual rows 16-B aligned: host-checked).
+// Straight from the MFMA layout every store writes 16 pixels x 32 B, a quarter
+// or half of each pixel's line, the rest coming from other stores and waves
+// (stride-2 classes: from other workgroups) -- measured 30-47 % of the tile
+// kernels' time on 64..128-channel shapes.  Here the fp32 tile goes through
+// the (then idle) LDS ring and every thread finishes 8 channels of one pixel:
+// 16-B loads of the gate / residual runs, one 16-B store, consecutive threads
+// along the pixel's row.  Same arithmetic and order as igemm_epilogue, so
+// bit-identical.  The staged image is [pixel][TCO / 4 fp32 chunks], chunk index
+// XOR (pixel & 7): conflict-free ds_write_b128 (8 pixels per lane group) and
+// ds_read_b128 at 8-channel runs.
+template <int MODE, int TCO, int TPIX, int FI, int FJ, int WT_CO, int WT_PIX>
+EE_DEV void staged_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], float4* st, int pix0, int co0, int wi,
+                            int wj, int lane, int tid, int Pc, int CH, int CW, int qy, int qx, int stc) {
+  constexpr int NCK = TCO / 4, SWM = NCK >= 8 ? 7 : NCK - 1, E = TCO / 8, ITEMS = TPIX * E;
+  const int fr = lane & 15, fq = lane >> 4;
+  __syncthreads();  // every wave's last ring reads are done
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const int pix = wj * WT_PIX + j * 16 + fr;
+      const int c = (wi * WT_CO + i * 16) / 4 + fq;
+      st[pix * NCK + (c ^ (pix & SWM))] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+  __syncthreads();
+  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
+#pragma unroll
+  for (int k = 0; k < (ITEMS + 255) / 256; ++k) {
+    const int item = k * 256 + tid;
+    if (ITEMS % 256 && item >= ITEMS) break;
+    const int pix = item / E, e = item % E;
+    const int pc = pix0 + pix, co = co0 + 8 * e;
+    if (pc >= Pc || co >= a.Mrows) continue;
+    const float4 lo = st[pix * NCK + ((2 * e) ^ (pix & SWM))];
+    const float4 hi = st[pix * NCK + ((2 * e + 1) ^ (pix & SWM))];
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    long p = pc, rpix = pc;
+    if (MODE == MODE_BWDD && a.ncls > 1) {
+      const int hw = CH * CW;
+      const int n = pc / hw, rem = pc - n * hw;
+      const int yy = rem / CW, xx = rem - yy * CW;
+      const int y = qy + stc * yy, x = qx + stc * xx;
+      p = ((long)n * a.OH + y) * a.OW + x;
+      if (a.res_up2) rpix = ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
+    } else if (a.res_up2) {
+      const unsigned hw = (unsigned)a.OH * (unsigned)a.OW;
+      const unsigned n = (unsigned)pc / hw, rem = (unsigned)pc - n * hw;
+      const unsigned y = rem / (unsigned)a.OW, x = rem - y * (unsigned)a.OW;
+      rpix = ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = act_fwd(v[r] + (a.bias ? a.bias[co + r] : 0.f), a.act, a.slope);
+    if (MODE == MODE_BWDD && a.gate) {
+      const uint4 gv = *reinterpret_cast<const uint4*>(a.gate + p * a.ldgate + co);
+      const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[2 * r] *= act_dgrad_from_y(lo_f(gw[r]), a.gate_act, a.gate_slope);
+        v[2 * r + 1] *= act_dgrad_from_y(hi_f(gw[r]), a.gate_act, a.gate_slope);
+      }
+    }
+    if (a.res) {
+      const uint4 rv = *reinterpret_cast<const uint4*>(a.res + (a.res_up2 ? rpix : p) * a.ldres + co);
+      const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[2 * r] = res_combine(a.res_scale, lo_f(rw[r]), gam, v[2 * r]);
+        v[2 * r + 1] = res_combine(a.res_scale, hi_f(rw[r]), gam, v[2 * r + 1]);
+      }
+    }
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + p * a.ldo + co) =
+        make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
   }
 }
 
@@ -869,7 +952,7 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
     }
 #pragma unroll
     for (int k = 0; k < KS; ++k)
-      if (it + S - KS + k < nk && !a.noload) issue((it + S - KS + k) % S);
+      if (it + S - KS + k < nk && !(a.noload & 1)) issue((it + S - KS + k) % S);
     bf16x8_t fa[KS][FI], fb[KS][FJ];
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
@@ -896,6 +979,16 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
         for (int j = 0; j < FJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[k][i], fb[k][j], acc[i][j], 0, 0, 0);
     }
+  }
+  if (a.noload & 4) {  // diagnostics (EEGAN_CONV_NOLOAD=4): keep the MFMAs alive, skip the epilogue
+    if (acc[0][0][0] == 123.f) reinterpret_cast<float*>(a.out)[0] = acc[FI - 1][FJ - 1][1];
+    return;
+  }
+  static_assert(TPIX * TCO * 4 <= S * STAGE * 2, "staged epilogue tile exceeds the LDS ring");
+  if (a.stage_epi) {
+    staged_epilogue<MODE, TCO, TPIX, FI, FJ, WT_CO, WT_PIX>(a, acc, reinterpret_cast<float4*>(lds), pix0, co0, wi, wj,
+                                                            lane, tid, Pc, CH, CW, qy, qx, stc);
+    return;
   }
   igemm_epilogue<MODE, FI, FJ, WT_CO, WT_PIX>(a, acc, pix0, co0, wi, wj, lane, split, Pc, CH, CW, qy, qx, stc);
 }
@@ -944,7 +1037,7 @@ __global__ void conv_splitk_reduce_kernel(ConvArgs a) {
         const uint2 rv = *reinterpret_cast<const uint2*>(a.res + rpix * a.ldres + co);
         const float rr[4] = {lo_f(rv.x), hi_f(rv.x), lo_f(rv.y), hi_f(rv.y)};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = a.res_scale * rr[r] + gam * v[r];
+        for (int r = 0; r < 4; ++r) v[r] = res_combine(a.res_scale, rr[r], gam, v[r]);
       }
       if (a.out_f32) {
         *reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(a.out) + (long)p * a.ldo + co) = {v[0], v[1], v[2], v[3]};
@@ -970,7 +1063,7 @@ __global__ void conv_splitk_reduce_kernel(ConvArgs a) {
         const unsigned y = rem / (unsigned)a.OW, x = rem - y * (unsigned)a.OW;
         rpix = ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
       }
-      v = a.res_scale * bf2f(a.res[rpix * a.ldres + co]) + gam * v;
+      v = res_combine(a.res_scale, bf2f(a.res[rpix * a.ldres + co]), gam, v);
     }
     if (a.out_f32) reinterpret_cast<float*>(a.out)[p * a.ldo + co] = v;
     else reinterpret_cast<bf16_t*>(a.out)[p * a.ldo + co] = f2bf(v);
@@ -2117,8 +2210,8 @@ __global__ __launch_bounds__(256, 2) void conv_s2bwd_lds_kernel(ConvArgs a, int 
           const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            v[2 * j] = a.res_scale * lo_f(rw[j]) + gam * v[2 * j];
-            v[2 * j + 1] = a.res_scale * hi_f(rw[j]) + gam * v[2 * j + 1];
+            v[2 * j] = res_combine(a.res_scale, lo_f(rw[j]), gam, v[2 * j]);
+            v[2 * j + 1] = res_combine(a.res_scale, hi_f(rw[j]), gam, v[2 * j + 1]);
           }
         }
         *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + p * a.ldo + 8 * e) =
@@ -2347,6 +2440,11 @@ int try_1x1(const ConvArgs& a, hipStream_t s, long src_bytes) {
   if (a.R != 1 || a.S != 1 || a.st != 1 || a.ph || a.pw || a.ncls != 1 || a.up2 || a.Kw > 256) return 0;
   if ((a.lds_src & 7) || ((uintptr_t)a.src & 15)) return 0;
   const int nks = a.Kw / BK;
+  // measured (tools/conv_bench.py): ahead of the tile kernels for one K-step
+  // (<= 128 rows), two K-steps at <= 64 rows and single-tile rows (<= 16);
+  // behind them from 64 -> 128 channels up (one B fragment per 8 MFMAs, 2
+  // waves per SIMD at NT = 8; or the input re-read per 64-row slice)
+  if (!(nks == 1 || (nks == 2 && a.Mrows <= 64) || a.Mrows <= 16)) return 0;
   const int nt_max = nks <= 2 ? 8 : nks == 4 ? 4 : 2;
   int nt = 1;
   while (nt < nt_max && 16 * nt < a.Mrows) nt *= 2;
@@ -2401,6 +2499,10 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
     const int kchunk = ee_cdiv(nk_max, p.nsplit);
     a.wide = p.tco >= 64 && nc % 2 == 0 && kchunk % 2 == 0 && env_int("EEGAN_CONV_WIDE", 1);
   }
+  // LDS-staged epilogue (conv_fast_kernel): unsplit bf16 output with 16-B aligned rows
+  a.stage_epi = p.nsplit == 1 && !a.out_f32 && a.Mrows % 8 == 0 && a.ldo % 8 == 0 && ((uintptr_t)a.out & 15) == 0 &&
+                (!a.gate || (a.ldgate % 8 == 0 && ((uintptr_t)a.gate & 15) == 0)) &&
+                (!a.res || (a.ldres % 8 == 0 && ((uintptr_t)a.res & 15) == 0)) && env_int("EEGAN_CONV_STAGE_EPI", 1);
   if (p.nsplit > 1 && !part_ws) {
     ee_set_error("conv: split-K workspace missing");
     return -22;

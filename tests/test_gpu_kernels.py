@@ -310,6 +310,50 @@ def test_conv_1x1_stream_bit_identical(gpu, monkeypatch):
         assert rel_l2(outs[1][3], xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize('target', ['1', '512'])
+def test_conv_staged_epilogue_bit_identical(gpu, monkeypatch, target):
+    """The tile kernel's LDS-staged epilogue (EEGAN_CONV_STAGE_EPI=1, default:
+    whole 16-B runs of 8 channels per thread) against the direct MFMA-layout
+    epilogue (=0): same arithmetic in the same order, so torch.equal --
+    forward with bias / act / residual + gain, backward-data with the gate,
+    the half-resolution residual and stride-2 parity classes, every tile
+    shape (16..128 rows x 64..256 pixels), ragged pixel tails; split-K and
+    unaligned cases keep the direct epilogue in both runs."""
+    Fn, T, _ = _mods()
+    monkeypatch.setenv('EEGAN_CONV_TARGET', target)
+    lrelu = Fn.ACT_CODES['lrelu']
+    for N, Cin, H, W, Cout, k, st, pad in [(2, 64, 16, 16, 128, 3, 1, 1), (3, 128, 9, 11, 64, 3, 1, 1),
+                                            (2, 96, 16, 16, 256, 4, 2, 1), (2, 64, 12, 12, 200, 1, 1, 0),
+                                            (4, 256, 8, 8, 72, 3, 1, 1), (2, 128, 16, 16, 96, 4, 2, 1),
+                                            (2, 48, 32, 32, 32, 3, 1, 1), (2, 32, 33, 31, 16, 3, 1, 1),
+                                            (2, 64, 32, 32, 64, 4, 2, 1), (2, 24, 16, 16, 40, 3, 1, 1),
+                                            (1, 512, 4, 4, 512, 3, 1, 1), (2, 40, 16, 16, 24, 4, 2, 1)]:
+        torch.manual_seed(N * Cin + Cout + H)
+        g = Fn.Geom(Cout, k, k, st, pad, pad, 0)
+        x = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        Wt = (torch.randn(Cout, Cin, k, k) * 0.05).to(gpu)
+        b = torch.randn(Cout).to(gpu)
+        gam = torch.tensor([0.7]).to(gpu)
+        Ho, Wo = g.out_hw(H, W)
+        res = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
+        dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
+        gate = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        halfres = _nhwc(torch.randn(N, Cin, H // 2, W // 2), gpu) if H % 2 == 0 and W % 2 == 0 else None
+        outs = []
+        for on in ('0', '1'):
+            monkeypatch.setenv('EEGAN_CONV_STAGE_EPI', on)
+            o = [Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, res=res, gamma=gam).float().cpu(),
+                 Fn.conv_fwd_raw(x, Wt, None, g).float().cpu(),
+                 Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape)).float().cpu(),
+                 Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), gate=gate, gate_act=lrelu).float().cpu()]
+            if halfres is not None:
+                o.append(Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), res=halfres, res_up2=1,
+                                              res_scale=0.25).float().cpu())
+            outs.append(o)
+        for a, c in zip(*outs):
+            assert torch.equal(a, c), (N, Cin, H, W, Cout, k, st)
+
+
 def test_cat_channels(gpu):
     """Inception branch concat (one launch when every part has C % 8 == 0,
     else the per-part path) against torch.cat, with strided (sliced) parts."""
