@@ -45,6 +45,9 @@ _FAMILIES = [
     (re.compile(r'conv_thin(_lds)?_kernel<0,'), 'conv_fwd', True),
     (re.compile(r'conv_thin(_lds)?_kernel<1,'), 'conv_bwd_data', True),
     (re.compile(r'conv_wgrad_thin_kernel<'), 'conv_bwd_weight', True),
+    (re.compile(r'conv_1x1_kernel<0,'), 'conv_fwd', True),
+    (re.compile(r'conv_1x1_kernel<1,'), 'conv_bwd_data', True),
+    (re.compile(r'conv_s2bwd_lds_kernel<'), 'conv_bwd_data', True),
     (re.compile(r'colsum_rows_kernel<.*WgradMap'), 'conv_bwd_weight', False),
 ]
 
