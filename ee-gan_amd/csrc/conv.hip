@@ -623,6 +623,10 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a, long src_
       m[j] = (2 * j < a.Cvalid ? 0xffffu : 0u) | (2 * j + 1 < a.Cvalid ? 0xffff0000u : 0u);
   }
 
+  // C % 8 != 0 (get_mask's 100-channel gradients): the chunk straddling Cvalid
+  // carries the tensor's padding channels (never written, may hold any bits);
+  // its lanes AND them away per K-step (block-uniform switch)
+  const bool rag = (a.Cvalid & 7) && a.Cgp != 8;
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
   for (int st = 0; st < S - 1; ++st)
@@ -650,6 +654,7 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(ConvArgs a, long src_
       v.y &= bmask.y;
       v.z &= bmask.z;
       v.w &= bmask.w;
+      if (rag) v = mask_chunk(v, ((kt0 + it) % nc) * BK + 8 * fq, a.Cvalid);
       fb[j] = as_frag(v);
     }
 #pragma unroll
@@ -874,7 +879,15 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
     for (int st = 0; st < S - KS; ++st)
       if (st < nk) issue(st);
   }
-  auto rd_frags_wide = [&](int sp, int half, bf16x8_t (&fa_)[FI], bf16x8_t (&fb_)[FJ]) {
+  // C % 8 != 0: the 16-B chunk straddling Cvalid carries the row's padding
+  // channels (never written, any bits): ANDed away in the B fragments of the
+  // K-step's slice (block-uniform switch; chunks past the row read the next
+  // pixel's finite channels against zero weights, as for any Cvalid < Cgp)
+  const bool rag = (a.Cvalid & 7) != 0;
+  auto rag_mask = [&](uint4 v, int kt) {
+    return rag ? mask_chunk(v, (kt % nc) * BK + 8 * fq, a.Cvalid) : v;
+  };
+  auto rd_frags_wide = [&](int sp, int half, bf16x8_t (&fa_)[FI], bf16x8_t (&fb_)[FJ], int kt) {
     const bf16_t* base = lds + sp * STAGE;
     const int q = 4 * half + fq;
 #pragma unroll
@@ -885,11 +898,11 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
       const int row = wj * WT_PIX + j * 16 + fr;
-      fb_[j] = as_frag(*reinterpret_cast<const uint4*>(base + TCO * 2 * BK + row * 2 * BK +
-                                                        ((q ^ ((row >> 1) & 7)) * 8)));
+      fb_[j] = as_frag(rag_mask(*reinterpret_cast<const uint4*>(base + TCO * 2 * BK + row * 2 * BK +
+                                                        ((q ^ ((row >> 1) & 7)) * 8)), kt));
     }
   };
-  auto rd_frags = [&](int stage, bf16x8_t (&fa_)[FI], bf16x8_t (&fb_)[FJ]) {
+  auto rd_frags = [&](int stage, bf16x8_t (&fa_)[FI], bf16x8_t (&fb_)[FJ], int kt) {
     const bf16_t* base = lds + stage * STAGE;
 #pragma unroll
     for (int i = 0; i < FI; ++i) {
@@ -899,8 +912,8 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
       const int row = wj * WT_PIX + j * 16 + fr;
-      fb_[j] = as_frag(
-          *reinterpret_cast<const uint4*>(base + TCO * BK + row * BK + ((fq ^ swz_b128((row >> 2) & 3)) * 8)));
+      fb_[j] = as_frag(rag_mask(
+          *reinterpret_cast<const uint4*>(base + TCO * BK + row * BK + ((fq ^ swz_b128((row >> 2) & 3)) * 8)), kt));
     }
   };
   int it0 = 0;
@@ -917,13 +930,13 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
       bf16x8_t fa0[FI], fb0[FJ], fa1[FI], fb1[FJ];
       if (wide) {
         if (it0 + S - 2 < nk) issue_wide((it0 + S - 2) % S);
-        rd_frags_wide(it0 % S, 0, fa0, fb0);
-        rd_frags_wide(it0 % S, 1, fa1, fb1);
+        rd_frags_wide(it0 % S, 0, fa0, fb0, kt0 + it0);
+        rd_frags_wide(it0 % S, 1, fa1, fb1, kt0 + it0 + 1);
       } else {
         if (it0 + S - 2 < nk) issue((it0 + S - 2) % S);
         if (it0 + S - 1 < nk) issue((it0 + S - 1) % S);
-        rd_frags(it0 % S, fa0, fb0);
-        rd_frags((it0 + 1) % S, fa1, fb1);
+        rd_frags(it0 % S, fa0, fb0, kt0 + it0);
+        rd_frags((it0 + 1) % S, fa1, fb1, kt0 + it0 + 1);
       }
 #pragma unroll
       for (int i = 0; i < FI; ++i)
@@ -966,8 +979,8 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
 #pragma unroll
       for (int j = 0; j < FJ; ++j) {
         const int row = wj * WT_PIX + j * 16 + fr;
-        fb[k][j] = as_frag(
-            *reinterpret_cast<const uint4*>(base + TCO * BK + row * BK + ((fq ^ swz_b128((row >> 2) & 3)) * 8)));
+        fb[k][j] = as_frag(rag_mask(
+            *reinterpret_cast<const uint4*>(base + TCO * BK + row * BK + ((fq ^ swz_b128((row >> 2) & 3)) * 8)), kt0 + it + k));
       }
     }
 #pragma unroll
@@ -2517,7 +2530,10 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
     else ee_launch(conv_fast_kernel<MODE, TC, TP, 1, 4>, grid, dim3(256), 0, s, a, src_bytes, w_bytes);                     \
   } while (0)
 #define IG(TC, TP, WC) ee_launch(conv_igemm_kernel<MODE, TC, TP, WC>, grid, dim3(256), 0, s, a)
-  const bool glds = ((a.Cvalid % 8) == 0 || a.Cgp == 8) && src_bytes < 0x7fffffffL && w_bytes < 0x7fffffffL;
+  // glds: channel chunks fetched whole (C % 8 != 0 masked in the fragments; the
+  // fast kernel needs whole valid chunks)
+  const bool glds = ((a.Cvalid % 8) == 0 || a.Cgp == 8 || env_int("EEGAN_CONV_GLDS_RAGGED", 1)) &&
+                    src_bytes < 0x7fffffffL && w_bytes < 0x7fffffffL;
   int tr_ = a.R, ts_ = a.S;
   if (MODE == MODE_BWDD && a.st > 1) tr_ = ee_cdiv(a.R, a.st), ts_ = ee_cdiv(a.S, a.st);
   const bool fast = glds && a.Cgp % BK == 0 && !a.up2 && tr_ * ts_ <= 32 && env_int("EEGAN_CONV_FAST", 1);

@@ -354,6 +354,53 @@ def test_conv_staged_epilogue_bit_identical(gpu, monkeypatch, target):
             assert torch.equal(a, c), (N, Cin, H, W, Cout, k, st)
 
 
+def _nhwc_nan_padded(x, dev):
+    """As _nhwc, with every padding channel of the row (ld > C) holding NaN bits."""
+    Fn, T, _ = _mods()
+    N, C, H, W = x.shape
+    t = T.empty_nhwc(N, C, H, W, dev)
+    torch.empty(0, dtype=torch.uint8, device=dev).set_(t.untyped_storage()).fill_(255)
+    t.copy_(x.to(dev).to(torch.bfloat16))
+    return t
+
+
+def test_conv_ragged_channels_lds_path(gpu, monkeypatch):
+    """Operands whose channel count is not a multiple of 8 (get_mask's 100
+    channels, models.py:35-41) take the LDS-DMA kernels (hoisted-gather fast
+    kernel, or conv_glds_kernel with EEGAN_CONV_FAST=0) with the straddling
+    16-B chunk masked per K-step (EEGAN_CONV_GLDS_RAGGED=1, default) instead of
+    the register-staged kernel (=0): same K order, so torch.equal -- even with
+    NaN bits in the padding channels -- and against torch fp32."""
+    Fn, T, _ = _mods()
+    monkeypatch.setenv('EEGAN_CONV_TARGET', '1')
+    for N, Cin, H, W, Cout, k, st, pad in [(2, 64, 16, 16, 100, 3, 1, 1), (2, 100, 12, 12, 64, 3, 1, 1),
+                                            (2, 20, 16, 16, 36, 4, 2, 1), (1, 128, 8, 8, 100, 3, 1, 1),
+                                            (2, 44, 9, 11, 52, 3, 1, 1)]:
+        torch.manual_seed(N * Cin + Cout + H)
+        g = Fn.Geom(Cout, k, k, st, pad, pad, 0)
+        xl = _bf(torch.randn(N, Cin, H, W))
+        x = _nhwc_nan_padded(xl, gpu)
+        Wt = _bf(torch.randn(Cout, Cin, k, k) * 0.05)
+        Wd = Wt.to(gpu)
+        Ho, Wo = g.out_hw(H, W)
+        dzl = _bf(torch.randn(N, Cout, Ho, Wo))
+        dz = _nhwc_nan_padded(dzl, gpu)
+        outs = []
+        for rag, fast in (('0', '1'), ('1', '0'), ('1', '1')):
+            monkeypatch.setenv('EEGAN_CONV_GLDS_RAGGED', rag)
+            monkeypatch.setenv('EEGAN_CONV_FAST', fast)
+            outs.append([Fn.conv_fwd_raw(x, Wd, None, g).float().cpu(),
+                         Fn.conv_bwd_data_raw(dz, Wd, g, (N, Cin, H, W)).float().cpu()])
+        for other in outs[1:]:
+            for a, c in zip(outs[0], other):
+                assert torch.isfinite(c).all()
+                assert torch.equal(a, c), (N, Cin, H, W, Cout, k, st)
+        assert rel_l2(outs[1][0], F.conv2d(xl, Wt, None, st, pad)) < 1e-2
+        xr = xl.clone().requires_grad_()
+        F.conv2d(xr, Wt, None, st, pad).backward(dzl)
+        assert rel_l2(outs[1][1], xr.grad) < 1e-2
+
+
 def test_cat_channels(gpu):
     """Inception branch concat (one launch when every part has C % 8 == 0,
     else the per-part path) against torch.cat, with strided (sliced) parts."""

@@ -42,6 +42,8 @@ SHAPES = {
     'c1x1_128_32': (16, 128, 32, 32, 256, 1, 1, 0),
     'c1x1_256_4': (16, 256, 4, 4, 512, 1, 1, 0),
     'c1x1_100_128': (16, 100, 128, 128, 1, 1, 1, 0),
+    'c3x3_64_100_128': (16, 64, 128, 128, 100, 3, 1, 1),
+    'c3x3_128_100_64': (16, 128, 64, 64, 100, 3, 1, 1),
 }
 
 
