@@ -2123,8 +2123,9 @@ __global__ __launch_bounds__(256, 2) void conv_s2bwd_lds_kernel(ConvArgs a, int 
   constexpr int NDMA = (NCHUNK + 255) / 256;
   constexpr int NKS = 4 * NC;  // 2 x 2 taps x NC 32-channel slices
   constexpr int SPX = 2 * 2 * TW;  // staged dx pixels per class row (2 dx rows x 2 TW columns)
+  constexpr int NSB = NC >= 4 ? 1 : 2;  // staging buffers (one at 128 K channels: 2 workgroups per CU)
   __shared__ uint4 tile[NDMA * 256];
-  __shared__ float4 stage[2][SPX * 8];  // [buffer][pixel][8 fp32 chunks of 4 channels], chunk-swizzled
+  __shared__ float4 stage[NSB][SPX * 8];  // [buffer][pixel][8 fp32 chunks of 4 channels], chunk-swizzled
   const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4, col = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int qy = wv >> 1, qx = wv & 1;
@@ -2132,7 +2133,10 @@ __global__ __launch_bounds__(256, 2) void conv_s2bwd_lds_kernel(ConvArgs a, int 
   const int nb = gridDim.x, b = blockIdx.x;
   const int lb = (b & 7) * (nb >> 3) + (b >> 3);  // XCD-contiguous logical block (nb % 8 == 0)
   const rsrc_t rsv = make_rsrc(a.src, src_bytes);
-  auto swz = [](int pix, int c) { return NCH == 8 ? c ^ ((pix >> 1) & 7) : c ^ ((pix >> 1) & 2); };
+  auto swz = [](int pix, int c) {
+    return NCH == 16 ? c ^ (pix & 15) : NCH == 8 ? c ^ ((pix >> 1) & 7) : c ^ ((pix >> 1) & 2);
+  };
+  const int co0 = blockIdx.y * 32;  // this workgroup's 32-row slice of the input channels
   bf16x8_t fa[NT][NKS];
   int t_off[NKS], t_ch[NKS];
 #pragma unroll
@@ -2141,13 +2145,13 @@ __global__ __launch_bounds__(256, 2) void conv_s2bwd_lds_kernel(ConvArgs a, int 
     const int r = r0 + 2 * ta, s = s0 + 2 * tb;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
-      fa[t][ks] = as_frag(*reinterpret_cast<const uint4*>(a.wp + (long)(16 * t + col) * a.Kw + (r * 4 + s) * a.Cgp +
-                                                          32 * cs + 8 * kg));
+      fa[t][ks] = as_frag(*reinterpret_cast<const uint4*>(a.wp + (long)(co0 + 16 * t + col) * a.Kw +
+                                                          (r * 4 + s) * a.Cgp + 32 * cs + 8 * kg));
     t_off[ks] = (qy - ta + 1) * PWT + (qx - tb + 1);
     t_ch[ks] = cs * 4 + kg;
   }
   const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
-  const int C8 = a.Mrows >> 3;  // 8-channel output runs per pixel (Mrows % 8 == 0, host-checked)
+  const int C8 = min(32, a.Mrows - co0) >> 3;  // 8-channel output runs of the slice (Mrows % 8 == 0, host-checked)
   const int CH = a.OH >> 1, CW = a.OW >> 1;
   const int tiles_x = CW / TW, tiles_y = CH / TH, tiles = a.N * tiles_x * tiles_y;
   const int t0 = lb * tiles_per_block, t1 = min(t0 + tiles_per_block, tiles);
@@ -2195,7 +2199,7 @@ __global__ __launch_bounds__(256, 2) void conv_s2bwd_lds_kernel(ConvArgs a, int 
         }
       __syncthreads();
       if (a.noload & 2) {  // diagnostics: skip the global stores
-        sb ^= 1;
+        if (NSB == 2) sb ^= 1;
         continue;
       }
       const int y0 = 2 * (i0 + rr), x0 = 2 * j0;
@@ -2209,7 +2213,7 @@ __global__ __launch_bounds__(256, 2) void conv_s2bwd_lds_kernel(ConvArgs a, int 
         const int y = y0 + sp / (2 * TW), x = x0 + sp % (2 * TW);
         const long p = ((long)n * a.OH + y) * a.OW + x;
         if (a.gate) {
-          const uint4 gv = *reinterpret_cast<const uint4*>(a.gate + p * a.ldgate + 8 * e);
+          const uint4 gv = *reinterpret_cast<const uint4*>(a.gate + p * a.ldgate + co0 + 8 * e);
           const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -2219,7 +2223,7 @@ __global__ __launch_bounds__(256, 2) void conv_s2bwd_lds_kernel(ConvArgs a, int 
         }
         if (a.res) {
           const long rp = a.res_up2 ? ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1) : p;
-          const uint4 rv = *reinterpret_cast<const uint4*>(a.res + rp * a.ldres + 8 * e);
+          const uint4 rv = *reinterpret_cast<const uint4*>(a.res + rp * a.ldres + co0 + 8 * e);
           const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -2227,10 +2231,13 @@ __global__ __launch_bounds__(256, 2) void conv_s2bwd_lds_kernel(ConvArgs a, int 
             v[2 * j + 1] = res_combine(a.res_scale, hi_f(rw[j]), gam, v[2 * j + 1]);
           }
         }
-        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + p * a.ldo + 8 * e) =
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + p * a.ldo + co0 + 8 * e) =
             make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
       }
-      sb ^= 1;  // the next row pair stages into the other buffer (one barrier per row pair)
+      // the next row pair stages into the other buffer (one barrier per row pair), or
+      // waits until this copy-out has read the single one
+      if (NSB == 2) sb ^= 1;
+      else __syncthreads();
     }
   }
 }
@@ -2393,7 +2400,7 @@ int try_thin(const ConvArgs& a, hipStream_t s, long src_bytes) {
   if (!env_int("EEGAN_CONV_THIN", 1) || src_bytes >= 0x7fffffffL) return 0;
   if (a.R != 3 || a.S != 3 || a.st != 1 || a.ncls != 1 || a.res || a.gate || a.out_f32 || a.Mrows > 32) return 0;
   if ((a.ldo & 3) || ((uintptr_t)a.out & 7) || (a.lds_src & 7) || ((uintptr_t)a.src & 15)) return 0;
-  const int nt = a.Mrows > 16 ? 2 : 1;
+  const int nt = a.Mrows > 16 ? 2 : 1, slices = ee_cdiv(a.Mrows, 32);
   const int nks = a.Cgp == 8 ? 3 : a.Cgp == 32 ? 9 : (a.Cgp == 64 && nt == 1) ? 18 : 0;
   if (!nks || (nks > 3 && (a.Cvalid & 7))) return 0;
   const int gpi = nks == 3 ? 2 : 1;
@@ -2423,8 +2430,11 @@ int try_thin(const ConvArgs& a, hipStream_t s, long src_bytes) {
 // conv_s2bwd_lds_kernel (0: not eligible, else the launch rc as try_thin)
 int try_s2bwd(const ConvArgs& a, hipStream_t s, long src_bytes) {
   if (!env_int("EEGAN_CONV_S2B", 1) || src_bytes >= 0x7fffffffL) return 0;
-  if (a.R != 4 || a.S != 4 || a.st != 2 || a.ph != 1 || a.pw != 1 || a.ncls != 4 || a.up2 || a.Mrows > 32) return 0;
-  if ((a.Cgp != 32 && a.Cgp != 64) || a.Cvalid != a.Cgp || (a.lds_src & 7) || ((uintptr_t)a.src & 15)) return 0;
+  if (a.R != 4 || a.S != 4 || a.st != 2 || a.ph != 1 || a.pw != 1 || a.ncls != 4 || a.up2 || a.Mrows > 64) return 0;
+  if ((a.Cgp != 32 && a.Cgp != 64 && a.Cgp != 128) || a.Cvalid != a.Cgp || (a.lds_src & 7) ||
+      ((uintptr_t)a.src & 15))
+    return 0;
+  if (a.Mrows > 32 && !env_int("EEGAN_CONV_S2B64", 1)) return 0;
   // LDS-staged epilogue: bf16 output, 16-B runs of 8 channels (output / gate / residual rows 16-B aligned)
   if (a.out_f32 || a.bias || a.act != ACT_NONE || (a.Mrows & 7) || (a.ldo & 7) || ((uintptr_t)a.out & 15)) return 0;
   if (a.gate && ((a.ldgate & 7) || ((uintptr_t)a.gate & 15))) return 0;
@@ -2434,11 +2444,13 @@ int try_s2bwd(const ConvArgs& a, hipStream_t s, long src_bytes) {
   const int tiles = a.N * (a.OW / 2 / S2B_TW) * (a.OH / 2 / S2B_TH);
   const int nbl = ee_round_up(std::min(tiles, env_int("EEGAN_CONV_S2B_BLOCKS", 512)), 8);
   const int tpb = (tiles + nbl - 1) / nbl;
-  const int nt = a.Mrows > 16 ? 2 : 1;
+  const int nt = a.Mrows > 16 ? 2 : 1, slices = ee_cdiv(a.Mrows, 32);
   ConvArgs a2 = a;
   a2.noload = env_int("EEGAN_CONV_NOLOAD", 0);  // diagnostics: 1 no halo DMA, 2 no epilogue
-#define SB(NT, NC) ee_launch(conv_s2bwd_lds_kernel<NT, NC>, dim3(nbl), dim3(256), 0, s, a2, (int)src_bytes, tpb)
-  if (a.Cgp == 64) { if (nt == 2) SB(2, 2); else SB(1, 2); }
+#define SB(NT, NC) \
+  ee_launch(conv_s2bwd_lds_kernel<NT, NC>, dim3(nbl, slices), dim3(256), 0, s, a2, (int)src_bytes, tpb)
+  if (a.Cgp == 128) { if (nt == 2) SB(2, 4); else SB(1, 4); }
+  else if (a.Cgp == 64) { if (nt == 2) SB(2, 2); else SB(1, 2); }
   else { if (nt == 2) SB(2, 1); else SB(1, 1); }
 #undef SB
   const int rc = ee_check_launch("conv_bwd_data(s2-halo)");

@@ -228,17 +228,20 @@ def test_conv_wide_stages_bit_identical(gpu, monkeypatch, target):
 
 
 def test_conv_s2bwd_halo_bit_identical(gpu, monkeypatch):
-    """4x4 / stride-2 / pad-1 data gradients with <= 32 input channels (resD
-    block0's conv_r[0]) take the shared-halo parity-class kernel
+    """4x4 / stride-2 / pad-1 data gradients with <= 64 input channels (resD
+    block0's and block1's conv_r[0]) take the shared-halo parity-class kernel
     (EEGAN_CONV_S2B=1, default): same K order as the unsplit tile kernel
     (EEGAN_CONV_TARGET=1 keeps it unsplit), so torch.equal -- plain, gated and
-    with the half-resolution pooled-shortcut residual; 16/20/32 input and
-    32/64 output channels, one- and multi-tile grids; also against torch fp32."""
+    with the half-resolution pooled-shortcut residual; 16..64 input (one or two
+    32-row slices) and 32/64/128 output channels, one- and multi-tile grids;
+    also against torch fp32."""
     Fn, T, _ = _mods()
     monkeypatch.setenv('EEGAN_CONV_TARGET', '1')
     lrelu = Fn.ACT_CODES['lrelu']
     for N, Cin, H, W, Cout in [(2, 32, 64, 64, 64), (3, 16, 8, 64, 32), (1, 24, 16, 128, 64),
-                               (2, 32, 24, 192, 32), (5, 32, 8, 64, 64)]:
+                               (2, 32, 24, 192, 32), (5, 32, 8, 64, 64),
+                               # two 32-row slices of the input channels, 128-channel K runs (block1)
+                               (2, 64, 16, 64, 128), (1, 48, 8, 128, 128), (2, 64, 8, 64, 64), (1, 40, 8, 64, 32)]:
         torch.manual_seed(N * Cin + Cout + H)
         g = Fn.Geom(Cout, 4, 4, 2, 1, 1, 0)
         Wt = _bf(torch.randn(Cout, Cin, 4, 4) * 0.05)

@@ -24,6 +24,7 @@ SHAPES = {
     'c3x3_32_256': (16, 32, 256, 256, 32, 3, 1, 1),
     'c4x4s2_32_256': (16, 32, 256, 256, 64, 4, 2, 1),
     'c4x4s2_128_64': (16, 128, 64, 64, 256, 4, 2, 1),
+    'c4x4s2_64_128': (16, 64, 128, 128, 128, 4, 2, 1),
     'c3x3_768_4': (16, 768, 4, 4, 1024, 3, 1, 1),
     'c3x3_512_4': (16, 512, 4, 4, 512, 3, 1, 1),
     'c4x4s4_1024_4': (16, 1024, 4, 4, 1024, 4, 4, 0),
