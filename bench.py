@@ -12,8 +12,10 @@ initialised weights (no datasets/checkpoints offline).
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
 Prints ONE JSON line on rank 0 (see the repo README / task contract), with a
-`roofline` object for the dominant kernel family (conv forward implicit GEMM,
-bf16 MFMA) measured with HIP events over the timed region, and a
+`roofline` object for the dominant conv kernel family (by summed dispatch
+time: forward, backward-data or weight-gradient implicit GEMM, bf16 MFMA),
+timed per dispatch with HIP events, its PMC traffic and MFMA-busy figures
+from the committed rocprofv3 summary of the same config, and a
 `cpu_baseline` object: the CPU oracle (oracle/, a PyTorch-CPU restatement of
 the reference step) timed on the host on a bounded sample.
 """
@@ -74,32 +76,61 @@ def build(cfg_name, device, sim_coe=0.05):
     return T, B, ncls
 
 
-def pmc_family(kind):
-    """PMC figures of kernel family `kind` from the newest committed rocprofv3
-    summary (profiles/rNN_families.json, written by tools/rocprof_families.py,
-    one counter pass each): HBM bytes per launch (FETCH_SIZE x2 -- the gfx950
-    wide-read correction -- + WRITE_SIZE) and the MFMA-busy fraction
-    (SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE x SIMDs)."""
+def _lib_sha():
+    import hashlib
+    h = hashlib.sha256()
+    with open(os.path.join(REPO, 'ee-gan_amd', 'eegan_hip', 'libeegan_hip.so'), 'rb') as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_summary(config):
+    """The newest committed rocprofv3 summary of workload `config`
+    (profiles/rNN_<config>_families.json, tools/gpu_profile.sh +
+    tools/rocprof_families.py: kernel-trace pass plus one PMC pass per
+    counter).  Returns (summary dict, path, current) where current says the
+    summary was taken with the libeegan_hip.so this run loaded (its sha256);
+    (None, None, False) when no summary of this config exists."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_families.json')))
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_%s_families.json' % config)))
     if not files:
-        return {}, None
+        return None, None, False
     with open(files[-1]) as f:
-        fam = json.load(f).get('families', {}).get(kind, {})
-    return fam, 'profiles/' + os.path.basename(files[-1])
+        summ = json.load(f)
+    try:
+        current = summ.get('lib_sha256_16') == _lib_sha()
+    except OSError:
+        current = False
+    return summ, 'profiles/' + os.path.basename(files[-1]), current
 
 
-def conv_path_hbm_frac():
+def conv_path_hbm_frac(fams):
     """Whole conv path (fwd + bwd-data + wgrad families): PMC HBM bytes over
-    kernel time over the 8 TB/s peak, from the newest profiles/rNN_families.json."""
+    kernel time over the 8 TB/s peak (north_star's definition).
+    Counts every byte the counters saw, wasted re-reads included."""
     tot_b = tot_s = 0.0
     for k in ('conv_fwd', 'conv_bwd_data', 'conv_bwd_weight'):
-        f, _ = pmc_family(k)
+        f = fams.get(k, {})
         if not f.get('hbm_bytes_per_call') or not f.get('calls'):
             return None
         tot_b += f['hbm_bytes_per_call'] * f['calls']
         tot_s += f['total_ms'] * 1e-3
     return round(tot_b / tot_s / 1e9 / HBM_PEAK_GBS, 4) if tot_s else None
+
+
+def host_submit_ms(step, reps=3):
+    """Host time of submitting one step (graph replay) while the GPU is held
+    by a ~0.3 s spin kernel: the pure submission cost, without the queue
+    back-pressure that makes the host wait during back-to-back replays."""
+    ts = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        torch.cuda._sleep(int(2.4e9 * 0.3))
+        t0 = time.perf_counter()
+        step()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    torch.cuda.synchronize()
+    return round(sorted(ts)[len(ts) // 2], 3)
 
 
 def _cpu_model():
@@ -213,8 +244,8 @@ def main():
     use_graph = args.graph == 'on' or (args.graph == 'auto' and (
         world == 1 or (bool(D.COMMS) and os.environ.get('EEGAN_GRAPH_DIST', '1') == '1')))
     graph_error = None
+    from eegan_hip.trainer import StepGraph
     if use_graph:
-        from eegan_hip.trainer import StepGraph
         # the eager timing pass after the capture re-enters AccumulateGrad nodes first seen on the
         # capture stream; torch warns about the stream change, which is harmless here
         torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
@@ -252,6 +283,9 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = t.item()
 
+    # host cost of submitting one step with the GPU held busy (no queue back-pressure)
+    submit_ms = host_submit_ms(step) if use_graph else None
+
     # roofline timing pass: the same step run eagerly right after the timed
     # region, every conv / GEMM dispatch stamped by its own HIP start/stop
     # events (hipExtLaunchKernel), so host launch gaps are excluded
@@ -274,26 +308,49 @@ def main():
     dom = max(((k, v) for k, v in kern.items() if k.startswith('conv')), key=lambda kv: kv[1][3])
     kind, (n, fl, nb, tsec) = dom
     achieved = fl / tsec / 1e12
-    pf, traffic_src = pmc_family(kind)
+    summ, traffic_src, current = pmc_summary(args.config)
+    pfams = (summ or {}).get('families', {})
+    pf = pfams.get(kind, {})
     traffic = pf.get('hbm_bytes_per_call')
+    fam_out = {}
+    for k, v in kern.items():
+        e = {'ms_per_step': round(v[3] / per * 1e3, 3), 'TFLOPs': round(v[1] / max(v[3], 1e-12) / 1e12, 1)}
+        if k.startswith('conv'):
+            n_k = max(v[0], 1)
+            e['launches_per_step'] = v[0] // per
+            e['algorithmic_bytes_per_launch'] = round(v[2] / n_k)
+            e['algorithmic_flops_per_launch'] = round(v[1] / n_k)
+            e['frac_of_mfma_peak'] = round(v[1] / max(v[3], 1e-12) / 1e12 / MFMA_PEAK_TFLOPS, 4)
+            q = pfams.get(k, {})
+            if q.get('hbm_bytes_per_call'):
+                e['pmc_bytes_per_launch'] = q['hbm_bytes_per_call']
+                e['pmc_over_algorithmic'] = round(q['hbm_bytes_per_call'] / max(v[2] / n_k, 1), 3)
+            if q.get('mfma_util') is not None:
+                e['mfma_busy'] = q['mfma_util']
+        fam_out[k] = e
     roof = {'kernel': kind, 'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': MFMA_PEAK_TFLOPS,
             'unit': 'TFLOP/s', 'frac': round(achieved / MFMA_PEAK_TFLOPS, 4), 'traffic': traffic,
-            'traffic_unit': 'HBM bytes per launch (rocprofv3 PMC)', 'traffic_source': traffic_src,
+            'traffic_unit': 'HBM bytes per launch (rocprofv3 PMC: FETCH_SIZE x2 + WRITE_SIZE, one pass each)',
+            'traffic_source': traffic_src,
+            # False: the PMC summary was taken with another build of libeegan_hip.so (stale figures)
+            'traffic_matches_this_build': current if traffic_src else None,
+            'traffic_git_head': (summ or {}).get('git_head'),
             'algorithmic_bytes_per_launch': round(nb / n),
             'algorithmic_flops_per_launch': round(fl / n),
+            'pmc_over_algorithmic': round(traffic / (nb / n), 3) if traffic else None,
             'launches_per_step': n // per, 'avg_launch_us': round(tsec / n * 1e6, 2),
             'timing': 'HIP start/stop events per dispatch (hipExtLaunchKernel) over %d eager step(s) of the same '
                       'workload right after the timed region' % per,
             'algorithmic_hbm_GBs': round(nb / tsec / 1e9, 1),
-            'mfma_busy': pf.get('mfma_util'),
-            'mfma_busy_unit': 'SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE per XCD x 1024 SIMDs), rocprofv3 PMC',
+            'mfma_busy': pf.get('mfma_util') if pf.get('mfma_util_unit') else None,
+            'mfma_busy_unit': pf.get('mfma_util_unit'),
             # north_star's conv-path HBM figure: PMC FETCH+WRITE bytes over kernel time, / 8 TB/s
+            # (wasted re-reads count as achieved bandwidth here; pmc_over_algorithmic says how many)
             'pmc_hbm_GBs': round(traffic / pf['avg_call_us'] / 1e3, 1) if traffic and pf.get('avg_call_us') else None,
             'pmc_hbm_frac': round(traffic / pf['avg_call_us'] / 1e3 / HBM_PEAK_GBS, 4)
             if traffic and pf.get('avg_call_us') else None,
-            'conv_path_pmc_hbm_frac': conv_path_hbm_frac(),
-            'families': {k: {'ms_per_step': round(v[3] / per * 1e3, 3),
-                             'TFLOPs': round(v[1] / max(v[3], 1e-12) / 1e12, 1)} for k, v in kern.items()}}
+            'conv_path_pmc_hbm_frac': conv_path_hbm_frac(pfams),
+            'families': fam_out}
     out = {'metric': 'train images/sec at 256x256 CUB, G+D step', 'value': round(value, 3), 'unit': 'images/sec',
            'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16',
@@ -303,6 +360,10 @@ def main():
                'model': 'EE-GAN Gen+ATTR_Enhance+Dis64/128/256+DAMSM(Inception-v3, biLSTM)',
                'global_batch': B * world, 'seq_len': 20, 'parallelism': 'dp%d' % world},
            'host_issue_ms_per_step': round(t_issue / args.steps * 1e3, 3),
+           # host_issue: host time inside the timed loop (with replay pacing it includes the waits for the
+           # previous replay); host_submit: one replay submitted with the GPU held busy (pure submission cost)
+           'host_submit_ms_per_step': submit_ms,
+           'replay_depth': StepGraph.DEPTH if use_graph else None,
            'execution': 'hip-graph replay of the captured step' if use_graph else 'eager',
            'roofline': roof}
     if args.config in CEILINGS:

@@ -253,5 +253,12 @@ def ensure_grad_hooks(module):
     (called from the drop-in models' forward, so reference code that wraps D
     and ATTR_Enhance in torch's own nn.DataParallel gets them too)."""
     if getattr(module, '_eegan_grad_hooks', None) is None and collective():
+        if any(p.requires_grad and not p.is_leaf for p in module.parameters()):
+            # torch's nn.DataParallel replicated the module over several visible
+            # GPUs: its parameters are non-leaf copies (no post-accumulate hook
+            # possible) and the original parameters would never be averaged
+            raise RuntimeError('eegan_hip: %s runs as an nn.DataParallel replica (non-leaf parameters); the '
+                               'data-parallel drop-in needs ONE visible GPU per rank (CUDA_VISIBLE_DEVICES / '
+                               'HIP_VISIBLE_DEVICES set per rank, see INTEGRATION.md)' % type(module).__name__)
         module._eegan_grad_hooks = GradHooks(module)
     return getattr(module, '_eegan_grad_hooks', None)

@@ -88,7 +88,7 @@ def _grad_sink(ctx, i):
     tr = getattr(var, '_eegan_track', None) if var is not None else None
     if tr is not None:   # FlatAdam's overlapped all-reduce counts the writes
         if g is not None:
-            if tr.note_grad_write(var):
+            if tr.note_grad_write(var, type(ctx).__name__):
                 _PENDING_SINKS.add(tr)
         else:
             tr.note_autograd_write(var)   # this gradient goes through autograd's accumulation instead

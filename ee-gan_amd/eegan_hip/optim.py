@@ -20,11 +20,21 @@ parameter gradients straight into the flat buffer (functional._grad_sink),
 which reports each write here; how many writes a parameter receives in one
 zero_grad..step window (1 in a first-order backward, 2 for a conv weight in
 the gradient penalty's second-order backward) is learned from the first
-window of its kind (keyed by the first parameter written) and then required:
-a window that writes a parameter more often than its plan raises.  Buckets
-holding a parameter whose gradient arrives any other way (autograd's own
-accumulation) are reduced at step(), as are all buckets of an unlearned
-window.  EEGAN_GRAD_OVERLAP=0 reduces everything at step().
+window of its kind and then required.  Windows are keyed by the first
+parameter written and the backward Function writing it (a first-order
+backward and the gradient penalty's double backward write from different
+Functions); windows of different kinds can still share a key,
+so a key holds every write-count plan learned under it (its first two
+windows only learn), and a bucket is
+reduced early only when ALL plans still consistent with the writes seen so
+far agree it is complete (a plan drops out as soon as a parameter receives
+more writes than it allows).  A window that matches no plan raises if it
+writes into an already reduced bucket, and its counts are learned at step().
+A bucket is reduced early only if all its writes came from the stream that
+completes it (the all-reduce is issued there); buckets written from several
+streams, or holding a parameter whose gradient arrives any other way
+(autograd's own accumulation), are reduced at step(), as are all buckets of
+an unlearned window.  EEGAN_GRAD_OVERLAP=0 reduces everything at step().
 """
 import os
 
@@ -84,7 +94,8 @@ class FlatAdam(torch.optim.Optimizer):
         self._index = {id(p): i for i, p in enumerate(uniq)}
         self._offs = offs
         self.set_bucket_bytes(bucket_bytes)
-        self._plans = {}         # window key -> (writes per param, early-eligible bucket flags)
+        self._plans = {}         # window key -> [(writes per param, early-eligible bucket flags, writing stream per bucket)]
+        self._key_seen = {}      # window key -> windows opened under it
         self._late = set()       # params whose gradient went through autograd at least once
         self._win = None
 
@@ -105,6 +116,7 @@ class FlatAdam(torch.optim.Optimizer):
             for i in range(lo, hi):
                 self._bucket_of[i] = b
         self._plans = {}
+        self._key_seen = {}
 
     def _dp(self):
         import torch.distributed as dist
@@ -130,45 +142,59 @@ class FlatAdam(torch.optim.Optimizer):
             dist.all_reduce(self.gflat[s:e], group=self.process_group)
         self._win['done'][b] = True
 
+    def _new_window(self):
+        return {'key': None, 'cands': [], 'counts': [0] * len(self.params), 'ready': [],
+                'done': [False] * len(self.buckets), 'streams': [None] * len(self.buckets)}
+
     def flush_ready(self):
         """Reduce the buckets completed by writes that are launched by now
         (called by functional once the writing Function's backward returned)."""
         w = self._win
         if w is None:
             return
+        cur = torch.cuda.current_stream().cuda_stream if self.gflat.is_cuda else 0
         for b in w['ready']:
-            self._reduce_bucket(b)
+            if w['streams'][b] == cur:   # issued behind every write of the bucket
+                self._reduce_bucket(b)
         w['ready'] = []
 
-    def note_grad_write(self, p):
-        """A kernel is about to accumulate into p.grad (functional._grad_sink).
-        True when this write completes a bucket (reduced by flush_ready)."""
+    def note_grad_write(self, p, site=None):
+        """A kernel is about to accumulate into p.grad (functional._grad_sink),
+        on the current stream, from backward Function `site`.  True when this
+        write completes a bucket (reduced by flush_ready)."""
         w = self._win
         if w is None:
             return False
         i = self._index[id(p)]
-        if w['key'] is None:
-            w['key'] = i
-            w['plan'] = self._plans.get(i)
-            if w['plan'] is not None:
-                need, early = w['plan']
-                w['left'] = [sum(1 for j in range(lo, hi) if need[j] > 0) if early[b] else -1
-                             for b, (lo, hi) in enumerate(self.buckets)]
-        w['counts'][i] += 1
-        if w['plan'] is None:
-            return False
-        need, early = w['plan']
-        c = w['counts'][i]
-        if c > need[i]:
-            raise RuntimeError('FlatAdam: parameter %d received %d gradient writes in a window planned for %d '
-                               '(overlapped all-reduce would have read it early)' % (i, c, need[i]))
         b = self._bucket_of[i]
-        if c == need[i] and early[b]:
-            w['left'][b] -= 1
-            if w['left'][b] == 0:
-                w['ready'].append(b)
-                return True
-        return False
+        if w['key'] is None:
+            w['key'] = key = (i, site)
+            seen = self._key_seen.get(key, 0)
+            self._key_seen[key] = seen + 1
+            # a key's plans steer early reductions from its third window on, so
+            # two kinds of window sharing a key are both learned first
+            w['cands'] = list(self._plans.get(key, ())) if seen >= 2 else []
+        w['counts'][i] += 1
+        c = w['counts'][i]
+        st = torch.cuda.current_stream().cuda_stream if p.is_cuda else 0
+        ws = w['streams'][b]
+        if ws is None:
+            w['streams'][b] = st
+        elif ws != st:
+            w['streams'][b] = -1     # written from several streams: reduce at step()
+        if w['done'][b]:
+            raise RuntimeError('FlatAdam: parameter %d received gradient write %d after its bucket was reduced '
+                               '(no learned write plan matches this window)' % (i, c))
+        # plans that allow fewer writes of p than seen are not this window's
+        w['cands'] = [pl for pl in w['cands'] if pl[0][i] >= c]
+        if not w['cands'] or w['streams'][b] == -1 or b in w['ready']:
+            return False
+        lo, hi = self.buckets[b]
+        for need, early, _ in w['cands']:
+            if not early[b] or any(w['counts'][j] != need[j] for j in range(lo, hi)):
+                return False
+        w['ready'].append(b)
+        return True
 
     def zero_grad(self, set_to_none=False):
         ops.fill_f32(self.gflat.data_ptr(), self.numel, 0.0, stream())
@@ -178,8 +204,7 @@ class FlatAdam(torch.optim.Optimizer):
         if OVERLAP and self._dp() and self.process_group is not None:
             import torch.distributed as dist
             if self.process_group is dist.group.WORLD:
-                self._win = {'key': None, 'plan': None, 'counts': [0] * len(self.params), 'ready': [],
-                             'done': [False] * len(self.buckets), 'left': None}
+                self._win = self._new_window()
                 for p in self.params:
                     p._eegan_track = self
 
@@ -209,8 +234,7 @@ class FlatAdam(torch.optim.Optimizer):
             return
         w = self._win
         if w is None:   # no overlap: every bucket now
-            self._win = w = {'key': None, 'plan': None, 'counts': [0] * len(self.params), 'ready': [],
-                             'done': [False] * len(self.buckets), 'left': None}
+            self._win = w = self._new_window()
         self.flush_ready()
         late_buckets = {self._bucket_of[i] for i in self._late}
         if any(w['done'][b] for b in late_buckets):
@@ -218,10 +242,13 @@ class FlatAdam(torch.optim.Optimizer):
         for b in range(len(self.buckets)):   # everything not reduced during the backward, in bucket order
             if not w['done'][b]:
                 self._reduce_bucket(b)
-        if w['key'] is not None and w['key'] not in self._plans:   # learn this window's write counts
-            need = list(w['counts'])
-            early = [all(need[j] > 0 and j not in self._late for j in range(lo, hi)) for lo, hi in self.buckets]
-            self._plans[w['key']] = (need, early)
+        if w['key'] is not None:   # learn this window's write counts (a new kind of window under this key)
+            need = tuple(w['counts'])
+            plans = self._plans.setdefault(w['key'], [])
+            if not any(pl[0] == need for pl in plans):
+                early = [all(need[j] > 0 and j not in self._late for j in range(lo, hi)) and w['streams'][b] != -1
+                         for b, (lo, hi) in enumerate(self.buckets)]
+                plans.append((need, early, w['streams'][:]))
         self._win = None
         for p in self.params:
             p._eegan_track = None

@@ -410,7 +410,7 @@ class StepGraph(object):
     kernels that are part of the graph.  Learning rates are baked in.
     """
 
-    def __init__(self, trainer, batch, warmup=2, timer=None, **step_kw):
+    def __init__(self, trainer, batch, warmup=2, timer=None, keep_graph=False, **step_kw):
         from . import functional as Fn
         side = new_stream(torch.cuda.current_device())
         side.wait_stream(torch.cuda.current_stream())
@@ -418,7 +418,8 @@ class StepGraph(object):
             for _ in range(warmup):
                 trainer.train_step(batch, **step_kw)
         torch.cuda.current_stream().wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
+        # keep_graph: the hipGraph stays inspectable after instantiation (node counts, tools/probe)
+        self.graph = torch.cuda.CUDAGraph(keep_graph=keep_graph)
         prev, Fn.TIMER = Fn.TIMER, timer
         # with a process group the RCCL collectives (SyncBN statistics, DAMSM
         # gathers, gradient buckets) are captured too; thread-local capture
@@ -458,6 +459,29 @@ class StepGraph(object):
         finally:
             Fn.TIMER = prev
 
+    # Replays kept in flight.  Back-to-back graph launches fill the HW queues
+    # (the host then blocks inside hipGraphLaunch, `host_issue_ms_per_step` ~
+    # the GPU time) and the next replay's packets queue up beside the running
+    # one's: the step's stream lanes then run slower.  Measured on the C2 step
+    # (tools/probe/graph_submit.py, profiles/r03_graph_submit.json): 27.4-27.8
+    # ms per step unpaced or with 2-3 replays in flight, 25.8-26.0 ms when each
+    # replay is submitted after the previous one finished (one replay from an
+    # idle GPU: 25.6 ms); submitting one replay costs 6.3 ms of host time
+    # (GPU blocked, 2,390 nodes / 2,417 edges), so it overlaps the replay it
+    # launches.  With depth d the host waits for replay k-d before launching
+    # replay k.  EEGAN_REPLAY_DEPTH=0: unpaced.
+    DEPTH = int(os.environ.get('EEGAN_REPLAY_DEPTH', '1'))
+
     def replay(self):
+        if self.DEPTH > 0:
+            q = getattr(self, '_inflight', None)
+            if q is None:
+                q = self._inflight = []
+            while len(q) >= self.DEPTH:
+                q.pop(0).synchronize()
         self.graph.replay()
+        if self.DEPTH > 0:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._inflight.append(ev)
         return self.out

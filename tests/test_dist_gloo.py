@@ -81,6 +81,69 @@ def _case_flat_adam_allreduce(rank):
         assert p.grad.data_ptr() >= opt.gflat.data_ptr()
 
 
+def _case_flat_adam_overlap_plans(rank):
+    """FlatAdam's overlapped all-reduce over learned write plans (the kernels'
+    direct gradient writes simulated on CPU): two kinds of window share one
+    key (same first parameter, same writing Function) but write parameters
+    different numbers of times -- a first-order backward (one write each) and
+    a double backward (two writes to some).  Each key's first two windows only
+    learn; from then on a bucket is reduced during the backward only when
+    every plan still consistent with the writes agrees it is complete; every
+    window's result equals the mean over ranks, and buckets written from two
+    streams wait for step()."""
+    import types
+    from eegan_hip import optim as OP
+    torch.manual_seed(7)
+    ps = [torch.nn.Parameter(torch.randn(8)) for _ in range(4)]
+    opt = OP.FlatAdam(ps, lr=1e-3, betas=(0.0, 0.9), process_group=dist.group.WORLD, bucket_bytes=32)
+    assert len(opt.buckets) == 4   # one parameter per bucket
+    OP.ops = types.SimpleNamespace(fill_f32=lambda ptr, n, v, st: opt.gflat.fill_(v))
+    OP.stream = lambda: 0
+    early = []
+    orig = opt._reduce_bucket
+    opt._reduce_bucket = lambda b: (early.append((opt._in_bwd, b)), orig(b))[1]
+    kinds = {'first': [3, 2, 1, 0], 'double': [3, 2, 2, 1, 1, 0]}
+    g = torch.Generator().manual_seed(100 + rank)
+    for it, kind in enumerate(['first', 'double'] * 3 + ['double', 'first']):
+        early.clear()
+        opt.zero_grad()
+        local = torch.zeros(opt.numel)
+        opt._in_bwd = True
+        for i in kinds[kind]:
+            v = torch.randn(8, generator=g)
+            ps[i].grad.add_(v)
+            local[opt._offs[i]:opt._offs[i] + 8] += v
+            if opt.note_grad_write(ps[i], 'ConvFnBackward'):
+                opt.flush_ready()
+        opt._in_bwd = False
+        opt._allreduce()
+        allg = [torch.empty(opt.numel) for _ in range(WORLD)]
+        dist.all_gather(allg, local)
+        assert torch.allclose(opt.gflat, sum(allg) / WORLD, atol=1e-6), (it, kind)
+        during = sorted(b for d, b in early if d)
+        if it < 2:
+            assert during == [], (it, during)    # learning windows
+        elif kind == 'first':
+            # bucket of parameter 3 (bucket 0): one write in both plans -> early;
+            # parameters 2 and 1 were written once: the double plan wants two
+            assert opt._bucket_of[3] in during and opt._bucket_of[2] not in during
+        else:
+            assert opt._bucket_of[3] in during and opt._bucket_of[2] in during, (it, during)
+    # a bucket written from two streams is never reduced before step()
+    opt.zero_grad()
+    w = opt._win
+    opt._in_bwd = True
+    early.clear()
+    for i in kinds['first']:
+        if i == 3:
+            w['streams'][opt._bucket_of[3]] = 12345   # an earlier write from another lane
+        if opt.note_grad_write(ps[i], 'ConvFnBackward'):
+            opt.flush_ready()
+    opt._in_bwd = False
+    assert opt._bucket_of[3] not in [b for d, b in early if d]
+    opt._allreduce()
+
+
 def _case_grad_reducer(rank):
     from eegan_hip.dist import GradReducer
     m = torch.nn.Linear(4, 3)
@@ -174,6 +237,6 @@ def _case_syncbn_stats(rank):
     assert torch.allclose(rv.float(), sd['bn.running_var'], atol=1e-5)
 
 
-@pytest.mark.parametrize('case', ['all_gather', 'flat_adam_allreduce', 'grad_reducer', 'grad_hooks_adam', 'syncbn_stats'])
+@pytest.mark.parametrize('case', ['all_gather', 'flat_adam_allreduce', 'flat_adam_overlap_plans', 'grad_reducer', 'grad_hooks_adam', 'syncbn_stats'])
 def test_gloo_world2(case):
     _run(globals()['_case_' + case])

@@ -492,7 +492,8 @@ def test_damsm_losses(gpu):
     _check('damsm/w1_nocls', w1n.reshape(1), g['damsm/w1_nocls'].reshape(1), TOL_DAMSM_LOSS)
 
 
-@pytest.mark.parametrize('n_img,n_txt,T,off', [(3, 7, 20, 2), (16, 16, 18, 0), (2, 5, 32, 3)])
+@pytest.mark.parametrize('n_img,n_txt,T,off', [(3, 7, 20, 2), (16, 16, 18, 0), (2, 5, 32, 3),
+                                               (32, 256, 18, 5)])   # C5's rank: 32 local x 256 global
 def test_words_block_rectangular(gpu, n_img, n_txt, T, off):
     """The B_local x B_global block a data-parallel rank computes: rows for
     n_img images against n_txt captions (lengths 1..T, > 16 words use both
@@ -839,12 +840,15 @@ def test_step_graph_matches_eager(gpu):
     assert torch.equal(state['graph'], state['eager'])
 
 
-@pytest.mark.parametrize('cfg', ['C3', 'C4'])
+@pytest.mark.parametrize('cfg', ['C2', 'C3', 'C4', 'C5'])
 def test_config_step_graph_matches_eager(gpu, cfg):
-    """Full-size steps of the configs the bench line does not time: C3
+    """Full-size steps of every BASELINE configuration that runs on one GPU:
+    C2 (the bench line's workload: CUB, GF=DF=32, batch 16, 200 classes), C3
     (Oxford-102 Flowers, GF=DF=48 -> 48/96/192/384/768 channels on the padded-K
     conv paths, batch 32, 102 classes) and C4's per-GPU shard (MS-COCO,
-    GF=DF=64, batch 8, USE_CLASS=False: Dis256 with the DiscSent head).  Size-
+    GF=DF=64, batch 8, USE_CLASS=False: Dis256 with the DiscSent head) and
+    C5's per-GPU shard (CUB, GF=DF=32, 32 images per GPU; its 32 x 256
+    global-batch DAMSM block is test_words_block_rectangular's last case).  Size-
     independent properties (the golden fixtures pin the arithmetic at small
     width): finite parameters / moments, images in [-1, 1], and the captured
     step graph equal to the eager step bit for bit."""

@@ -4,20 +4,21 @@
 # with sys/runtime tracing).  Outputs under gpurun_out/prof_<tag>/.
 TAG=${1:-r01}
 STEPS=${2:-6}
+CFG=${3:-C2}
 source "$(dirname "$0")/../run_gpu_steps.sh"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/prof_$TAG
 mkdir -p $O
 step 900 prof_trace rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
-  python3 bench.py --steps $STEPS --warmup 2 --no-cpu-baseline
+  python3 bench.py --config $CFG --steps $STEPS --warmup 2 --no-cpu-baseline
 step 900 prof_fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- \
-  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --graph off --no-timer
+  python3 bench.py --config $CFG --steps 1 --warmup 1 --no-cpu-baseline --graph off --no-timer
 step 900 prof_write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- \
-  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --graph off --no-timer
+  python3 bench.py --config $CFG --steps 1 --warmup 1 --no-cpu-baseline --graph off --no-timer
 step 900 prof_mfma rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $O/mfma -o run -- \
-  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --graph off --no-timer
+  python3 bench.py --config $CFG --steps 1 --warmup 1 --no-cpu-baseline --graph off --no-timer
 python3 tools/rocprof_families.py --trace $O/trace --fetch $O/fetch --write $O/write --mfma $O/mfma \
-  --steps $((STEPS + 4)) --out $O/families.json > /dev/null
+  --steps $((STEPS + 4)) --config $CFG --out $O/families.json > /dev/null
 python3 tools/dispatch_groups.py $O/trace --steps $((STEPS + 4)) --filter conv --top 60 > $O/conv_groups.txt
 python3 tools/dispatch_groups.py $O/trace --steps $((STEPS + 4)) --top 60 > $O/all_groups.txt
 for d in trace fetch write mfma; do find $O/$d -name '*.csv' -size +20M -delete; done

@@ -12,11 +12,18 @@ used, its reduce kernel -- the same bracket bench.py's HIP events time).
 section) FETCH_SIZE on gfx950 counts half the bytes of wide coalesced reads,
 so it is doubled; WRITE_SIZE is taken as is.  Both are in KB.
 --mfma: directory of a `rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES
-GRBM_GUI_ACTIVE` run: MFMA-busy SIMD cycles and GPU-active cycles (summed
-over the 8 XCDs, so /8 per XCD) per call; mfma_util = busy / (active/8 x 1024
-SIMDs), the fraction of the dense bf16 MFMA peak at the clock the kernel ran
-(a 16x16x32 bf16 MFMA is 16 busy cycles for 16384 FLOP: 1024 FLOP per busy
-cycle per SIMD -- MI355X_MICROARCH.md, matrix cores).
+GRBM_GUI_ACTIVE` run: MFMA-busy SIMD cycles per call (summed over the
+1024 SIMDs; a 16x16x32 bf16 MFMA is 16 busy cycles for 16384 FLOP, 1024
+FLOP per busy cycle per SIMD -- MI355X_MICROARCH.md, matrix cores).
+mfma_util = busy cycles / (the call's duration in the kernel-trace pass x
+2.4 GHz x 1024 SIMDs): the fraction of the dense bf16 MFMA peak, on the
+same time base as bench.py's FLOP-derived fraction (which it can only exceed
+by the MFMAs spent on padding).  GRBM_GUI_ACTIVE (summed over the 8 XCDs)
+is kept as gpu_active_cycles_per_call for reference only: on dispatches
+shorter than ~0.3 ms it reads well above duration x clock (MI355X_MICROARCH.md,
+DVFS give-back), so it is not used as the denominator.
+The summary records the git commit and the sha256 of libeegan_hip.so it was
+taken with, so bench.py can flag a summary taken with other kernels.
 Output JSON: {family: {calls, avg_call_us, total_ms, hbm_bytes_per_call,
 mfma_util}} plus totals (GPU busy time per step), read by bench.py for
 `traffic` and `mfma_busy`.
@@ -50,6 +57,31 @@ _FAMILIES = [
     (re.compile(r'conv_s2bwd_lds_kernel<'), 'conv_bwd_data', True),
     (re.compile(r'colsum_rows_kernel<.*WgradMap'), 'conv_bwd_weight', False),
 ]
+
+
+CLOCK_HZ = 2.4e9   # MI355X max clock (MI355X_MICROARCH.md): a lower bound on the busy fraction under DVFS
+SIMDS = 1024
+
+
+def _provenance():
+    import hashlib
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    so = os.path.join(repo, 'ee-gan_amd', 'eegan_hip', 'libeegan_hip.so')
+    h = hashlib.sha256()
+    try:
+        with open(so, 'rb') as f:
+            h.update(f.read())
+        sha = h.hexdigest()[:16]
+    except OSError:
+        sha = None
+    try:
+        head = subprocess.run(['git', 'rev-parse', '--short=12', 'HEAD'], cwd=repo, capture_output=True,
+                              text=True).stdout.strip() or None
+    except OSError:
+        head = None
+    head = head or os.environ.get('EEGAN_GIT_HEAD')   # the GPU box's copy of the tree has no .git
+    return {'lib_sha256_16': sha, 'git_head': head}
 
 
 def family(name):
@@ -102,6 +134,7 @@ def main():
     ap.add_argument('--mfma')
     ap.add_argument('--steps', type=int, default=0, help='steps in the traced run (warmup+timed) for per-step totals')
     ap.add_argument('--out')
+    ap.add_argument('--config', default='C2', help='bench.py workload the runs were taken on')
     a = ap.parse_args()
     fams = kernel_trace(a.trace)
     fetch = pmc(a.fetch, 'FETCH_SIZE') if a.fetch else None
@@ -120,15 +153,19 @@ def main():
             e['hbm_read_bytes_per_call'] = round(rd)
             e['hbm_write_bytes_per_call'] = round(wr)
             e['hbm_bytes_per_call'] = round(rd + wr)
-        if busy and gui and gui[0].get(fam):
-            b, gcy = busy[0][fam], gui[0][fam]
+        if busy and busy[0].get(fam):
+            b = busy[0][fam]
             n = max(busy[1][fam], 1)
             e['mfma_busy_cycles_per_call'] = round(b / n)
-            e['gpu_active_cycles_per_call'] = round(gcy / 8 / n)
-            e['mfma_util'] = round(b / (gcy / 8 * 1024), 4)
+            e['mfma_util'] = round(b / n / (e['avg_call_us'] * 1e-6 * CLOCK_HZ * SIMDS), 4)
+            e['mfma_util_unit'] = ('SQ_VALU_MFMA_BUSY_CYCLES per call / (kernel-trace call duration x 2.4 GHz x '
+                                   '1024 SIMDs)')
+            if gui and gui[0].get(fam):
+                e['gpu_active_cycles_per_call'] = round(gui[0][fam] / 8 / n)
         out[fam] = e
     total_ns = sum(o['ns'] for o in fams.values())
-    res = {'families': out, 'gpu_busy_ms_total': round(total_ns * 1e-6, 3)}
+    res = {'families': out, 'gpu_busy_ms_total': round(total_ns * 1e-6, 3), 'config': a.config}
+    res.update(_provenance())
     if a.steps:
         res['gpu_busy_ms_per_step'] = round(total_ns * 1e-6 / a.steps, 3)
     txt = json.dumps(res, indent=1)
