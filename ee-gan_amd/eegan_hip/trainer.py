@@ -40,6 +40,10 @@ LANE_PRIO = os.environ.get('EEGAN_LANE_PRIO', '1') != '0'
 G_EARLY = os.environ.get('EEGAN_G_EARLY', '1') != '0'
 # EEGAN_DAMSM_EARLY=0: the DAMSM branch runs inside g_update, after d_update (A/B switch).
 DAMSM_EARLY = os.environ.get('EEGAN_DAMSM_EARLY', '1') != '0'
+# EEGAN_DAMSM_GRAD_EARLY=0: the DAMSM branch's backward waits for g_update's backward (A/B switch).
+DAMSM_GRAD_EARLY = os.environ.get('EEGAN_DAMSM_GRAD_EARLY', '1') != '0'
+# EEGAN_LANE_ORDER=rev: the discriminator lanes are issued largest first, the DAMSM lane after them
+LANE_ORDER = os.environ.get('EEGAN_LANE_ORDER', 'fwd')
 
 
 class Trainer(object):
@@ -209,13 +213,17 @@ class Trainer(object):
         return (w[0] + w[1]) * lam, (s[0] + s[1]) * lam, (a[0] + a[1]) * lam
 
     # ----------------------------------------------------------- updates --
-    def d_update(self, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec=False, g_early=None):
+    def d_update(self, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec=False, g_early=None,
+                 before_join=None):
         """train.py:437-469: per D a hinge(+class) step, then a GP step (each D
         on its own stream).  `g_early` (a list): also run g_update's generator
         loss term through each D right after that D's update, into the list."""
         streams = self._side_streams(len(self.netsD))
-        g_terms = []
-        for i in range(len(self.netsD)):
+        g_terms = [None] * len(self.netsD)
+        order = range(len(self.netsD))
+        if LANE_ORDER == 'rev':
+            order = reversed(order)
+        for i in order:
             with self._on(streams[i]):
                 Fn.stamp('D%d start' % i)
                 self._d_update_one(i, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec)
@@ -223,7 +231,9 @@ class Trainer(object):
                     # g_update's pass through this D (train.py:477-489) reads only this D's
                     # final parameters and the fake images: it runs on the lane as soon as
                     # the update is done, while the larger D's update still runs
-                    g_terms.append(self._g_term(i, fake_imgs, sent_emb, class_labels, iter_rec))
+                    g_terms[i] = self._g_term(i, fake_imgs, sent_emb, class_labels, iter_rec)
+        if before_join is not None:
+            before_join()
         self._join(streams)
         Fn.stamp('d_update joined')
         if g_early is not None:
@@ -270,14 +280,37 @@ class Trainer(object):
         only the fake images, the text embeddings and the frozen encoder --
         nothing d_update changes -- so its values are exactly the ones g_update
         would compute after d_update (train.py:490); the lane is joined in
-        g_update and the losses enter g_loss there."""
+        g_update and the losses enter g_loss there.
+
+        Its backward is issued here too (DAMSM_GRAD_EARLY): g_loss is linear in
+        the DAMSM terms (train.py:493, g_loss += DAMSM_coe * (s + w + a)), so
+        their gradient w.r.t. the 256-px fake image -- the losses' backward and
+        the Inception-v3 input-gradient pass -- depends on nothing d_update
+        computes.  It runs on this lane beside the discriminator updates and
+        g_update's backward only adds it at the image (the same sum, one
+        accumulation order apart), instead of running it behind the D passes
+        on the step's critical path.  Returns (w, s, a, dfake or None)."""
         streams = self._side_streams(len(self.netsD) + 1)
         with self._on(streams[-1]):
             Fn.stamp('DAMSM start')
-            out = self.DAMSM_loss(fake_imgs[-1], sent_emb, words_emb, attr_emb, class_ids, batch_size,
-                                  match_labels, cap_lens, self.image_encoder)
+            img = fake_imgs[-1]
+            grad_early = DAMSM_GRAD_EARLY and img.requires_grad
+            if grad_early:
+                # an alias whose autograd node lives on this lane: autograd.grad stops at
+                # it, so the gradient it captures makes no stream of the generator's
+                # (main) wait for this lane -- only g_update's backward, through the
+                # alias, joins them
+                img = img.view_as(img)
+            w, s, a = self.DAMSM_loss(img, sent_emb, words_emb, attr_emb, class_ids, batch_size,
+                                      match_labels, cap_lens, self.image_encoder)
             Fn.stamp('DAMSM forward')
-        return out
+            dfake = None
+            if grad_early:
+                (dfake,) = torch.autograd.grad(self.DAMSM_coe * (s + w + a), img)
+                w, s, a = w.detach(), s.detach(), a.detach()
+                Fn.stamp('DAMSM backward')
+                dfake = (img, dfake)
+        return w, s, a, dfake
 
     def _g_term(self, i, fake_imgs, sent_emb, class_labels, iter_rec):
         """The generator's adversarial term through D i (train.py:477-489)."""
@@ -313,12 +346,14 @@ class Trainer(object):
                 damsm = self.DAMSM_loss(fake_imgs[-1], sent_emb, words_emb, attr_emb, class_ids,
                                         batch_size, match_labels, cap_lens, self.image_encoder)
                 Fn.stamp('DAMSM forward')
-        w_loss, s_loss, a_loss = damsm
+        w_loss, s_loss, a_loss = damsm[:3]
+        dfake = damsm[3] if len(damsm) > 3 else None
         self._join(streams)
         Fn.stamp('g_update forwards joined')
         g_loss = terms[0]
         for t in terms[1:]:
             g_loss = g_loss + t
+        g_adv = g_loss
         g_loss = g_loss + self.DAMSM_coe * (s_loss + w_loss + a_loss)
         if iter_rec:
             self.records['errG/s_loss'] = s_loss.detach()
@@ -333,7 +368,11 @@ class Trainer(object):
         # zeroes those before every use (train.py:451,457), and the GP's
         # interpolated-image gradient is never read -- skipping them changes no
         # parameter and saves the D weight-gradient passes
-        g_loss.backward(inputs=self.optimizerG.params)
+        if dfake is not None:
+            # the DAMSM terms' share, computed by damsm_early, enters at (its alias of) the 256-px image
+            torch.autograd.backward([g_adv, dfake[0]], [None, dfake[1]], inputs=self.optimizerG.params)
+        else:
+            g_loss.backward(inputs=self.optimizerG.params)
         Fn.stamp('G backward (D, DAMSM, G)')
         self.optimizerG.step()
         Fn.stamp('G adam')
@@ -385,12 +424,18 @@ class Trainer(object):
         Fn.stamp('ATTR + G forward')
         _, _, match_labels = prepare_labels(B, dev)
         cls_ids = batch.get('cls_ids')  # train.py:490 passes class ids to DAMSM_loss even without USE_CLASS
-        damsm = None
-        if DAMSM_EARLY and self.use_streams:
-            damsm = self.damsm_early(fake_imgs, sent, words, attn_attr_emb, cls_ids, B, match_labels,
-                                     batch['cap_lens'])
+        damsm = []
+        early = DAMSM_EARLY and self.use_streams
+
+        def issue_damsm():
+            damsm[:] = self.damsm_early(fake_imgs, sent, words, attn_attr_emb, cls_ids, B, match_labels,
+                                        batch['cap_lens'])
+        if early and LANE_ORDER != 'rev':
+            issue_damsm()
         terms = [] if (G_EARLY and self.use_streams) else None
-        self.d_update(batch['imgs'], fake_imgs, sent, unpair, class_labels, iter_rec, g_early=terms)
+        self.d_update(batch['imgs'], fake_imgs, sent, unpair, class_labels, iter_rec, g_early=terms,
+                      before_join=issue_damsm if early and LANE_ORDER == 'rev' else None)
+        damsm = damsm or None
         g = self.g_update(fake_imgs, sent, words, attn_attr_emb, cls_ids, B, match_labels, batch['cap_lens'],
                           class_labels, iter_rec, damsm=damsm, terms=terms)
         Fn.stamp('end')

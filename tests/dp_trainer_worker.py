@@ -32,7 +32,7 @@ def main(out, tag):
 
     def counted(self, b):   # reductions issued from inside a backward (a window still open with its plan)
         w = self._win
-        if w is not None and w['plan'] is not None and not getattr(self, '_in_step', False):
+        if w is not None and w['cands'] and not getattr(self, '_in_step', False):
             early[id(self)] = early.get(id(self), 0) + 1
         return orig(self, b)
     O.FlatAdam._reduce_bucket = counted
@@ -51,7 +51,7 @@ def main(out, tag):
         o.set_bucket_bytes(16384)   # many small buckets at this test size
     batch = make_batch(B, dev, seed=11 + rank, class_num=ncls, with_class=True, id_offset=rank * B)
     noise = torch.randn(B, 100, device=dev, generator=torch.Generator(device=dev).manual_seed(5 + rank))
-    for _ in range(2):
+    for _ in range(3):   # a write plan steers early reductions from its key's third window on
         T.train_step(batch, noise=noise)
     torch.cuda.synchronize()
     opts = [T.optimizerG] + list(T.optimizerDs)
@@ -59,7 +59,8 @@ def main(out, tag):
         for o in opts:
             print('DBG opt params %d buckets %d late %d plans %s' % (
                 len(o.params), len(o.buckets), len(o._late),
-                [(k, sum(e), sum(1 for n in need if n == 0), sorted(set(need))) for k, (need, e) in o._plans.items()]),
+                [(k, sum(e), sum(1 for n in need if n == 0), sorted(set(need))) for k, pl in o._plans.items()
+                 for need, e, _ in pl]),
                 flush=True)
     torch.save({'params': [o.flat.cpu() for o in opts], 'early': [early.get(id(o), 0) for o in opts],
                 'buckets': [len(o.buckets) for o in opts]}, os.path.join(out, 'rank%d_%s.pt' % (rank, tag)))

@@ -66,7 +66,7 @@ def test_flat_adam_overlapped_allreduce_two_ranks(gpu, tmp_path):
     buckets all-reduced during the backward (EEGAN_GRAD_OVERLAP=1, default)
     give parameters bit-identical to reducing everything at step() (=0), the
     two ranks agree, and the overlap actually happened (buckets reduced from
-    inside the backward for every optimizer of the second step)."""
+    inside the backward for every optimizer of the third step)."""
     res = {}
     for tag, ov in (('ov', '1'), ('seq', '0')):
         cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
