@@ -32,6 +32,17 @@ class GemmDesc(C.Structure):
                [(n, C.c_int) for n in ['M', 'N', 'K', 'act', 'gate_act']] + [('alpha', C.c_float), ('beta', C.c_float)]
 
 
+class ImgJob(C.Structure):
+    _fields_ = [('src_off', C.c_long)] + [(n, C.c_int) for n in ['src_stride', 'row0', 'nrows', 'flip', 'hcoef_off',
+                                                                  'hbound_off', 'hksize', 'vcoef_off', 'vbound_off',
+                                                                  'vksize']]
+
+
+class ScaleTable(C.Structure):
+    _fields_ = [('size', C.c_int), ('ksize', C.c_int), ('hcoef', C.c_void_p), ('hbounds', C.c_void_p),
+                ('vcoef', C.c_void_p), ('vbounds', C.c_void_p)]
+
+
 P, I, L, F, D = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_double
 CD, BD = C.POINTER(ConvDesc), C.POINTER(BnModDesc)
 
@@ -120,6 +131,8 @@ _SIGS = {
     'eegan_adam': ([P, P, P, P, L, F, F, F, F, F, P, P], I),
     'eegan_embedding': ([P, L, P, I, P, P], I),
     'eegan_lstm_bidir': ([P, P, P, I, I, I, I, P, P, P], I),
+    'eegan_pipe_workspace': ([I, I, I, I, P], L),
+    'eegan_pipe_transform': ([P, P, I, I, I, P, P, I, P, P, P, I, P, P, P], I),
 }
 
 
@@ -137,7 +150,7 @@ def _load():
 
 LIB = _load()
 ABI_VERSION = LIB.eegan_abi_version()
-EXPECTED_ABI = 5
+EXPECTED_ABI = 6
 if ABI_VERSION != EXPECTED_ABI:
     raise ImportError('%s has ABI %d, these bindings need %d: rebuild (make -C ee-gan_amd/csrc)'
                       % (LIB_PATH, ABI_VERSION, EXPECTED_ABI))

@@ -42,8 +42,10 @@ G_EARLY = os.environ.get('EEGAN_G_EARLY', '1') != '0'
 DAMSM_EARLY = os.environ.get('EEGAN_DAMSM_EARLY', '1') != '0'
 # EEGAN_DAMSM_GRAD_EARLY=0: the DAMSM branch's backward waits for g_update's backward (A/B switch).
 DAMSM_GRAD_EARLY = os.environ.get('EEGAN_DAMSM_GRAD_EARLY', '1') != '0'
-# EEGAN_LANE_ORDER=rev: the discriminator lanes are issued largest first, the DAMSM lane after them
-LANE_ORDER = os.environ.get('EEGAN_LANE_ORDER', 'fwd')
+# the discriminator lanes are issued largest (critical) first and the DAMSM lane after them: the
+# first packets of the critical lane then do not queue behind the others' (C2: 678 vs 656 img/s,
+# tools/gpu_lane_ab.sh); EEGAN_LANE_ORDER=fwd: D64, D128, D256 after the DAMSM lane
+LANE_ORDER = os.environ.get('EEGAN_LANE_ORDER', 'rev')
 
 
 class Trainer(object):

@@ -26,9 +26,10 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 5  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
+#define EEGAN_ABI_VERSION 6  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
                                 4: rectangular (local x global) DAMSM words / sentence blocks on MFMA;
-                                5: GlobalAttentionGeneral (eegan_gag_*), words backward reuses the forward's prep */
+                                5: GlobalAttentionGeneral (eegan_gag_*), words backward reuses the forward's prep;
+                                6: device input pipeline (eegan_pipe_*) */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
@@ -289,6 +290,44 @@ int eegan_embedding(const long* ids, long n, const float* table, int E, float* o
  * words [B][2H][Tout] (zero padded past each length), sent [B][2H] = [h_fwd(last), h_bwd(first)] */
 int eegan_lstm_bidir(const float* xproj, const float* whhT, const long* lens, int B, int T, int H, int Tout,
                      float* words, float* sent, hipStream_t s);
+
+/* ---------------------------------------------------------- input pipeline --
+ * replaces: the per-image PIL work of TextDataset.get_imgs (datasets.py:391-424) under train.py's
+ * transform (train.py:269-272): Resize(304) -> RandomCrop(256) -> RandomHorizontalFlip -> Resize(64) /
+ * Resize(128) -> ToTensor + Normalize(0.5, 0.5), for a batch of decoded RGB uint8 images (3 bytes per
+ * pixel, bounding-box crop applied through src_off / the coefficient tables).  PIL's bilinear resample
+ * bit for bit: the host supplies PIL's 22-bit fixed-point weights (eegan_hip/pipeline.py), the kernels
+ * sum from 2^21, clip (>> 22) to uint8 and store the horizontal pass as uint8 before the vertical pass.
+ *
+ * One job per image (device memory, B entries): the horizontal pass reads source rows
+ * [row0, row0 + nrows) of the bbox crop (relative to src_off) for the `crop` crop columns; hbounds
+ * (xmin, count) and hcoef (hksize per column) give each crop column's support in bbox-crop columns;
+ * vbounds / vcoef (vksize per row) each crop row's support in bbox-crop rows.  flip mirrors the crop.
+ * scales[]: the output sizes, ascending, the last equal to `crop` (its tables unused); every smaller
+ * scale is PIL's Resize of the uint8 crop with the given tables (device pointers, same for all images).
+ * Outputs per scale (either may be NULL): out_f32[i] NCHW fp32 [B][3][s][s]; out_bf16[i] NHWC bf16
+ * [B][s][s][ld_bf16] (channels 3.. zeroed).  crop_u8_out (optional) receives the uint8 crops
+ * [B][crop][crop][3].  ws: eegan_pipe_workspace bytes. */
+typedef struct {
+  long src_off;   /* byte offset of the bbox crop's pixel (0, 0) in src */
+  int src_stride; /* bytes per source row */
+  int row0, nrows;
+  int flip;
+  int hcoef_off, hbound_off, hksize;
+  int vcoef_off, vbound_off, vksize;
+} eegan_img_job;
+typedef struct {
+  int size, ksize;
+  const int* hcoef;
+  const int* hbounds;
+  const int* vcoef;
+  const int* vbounds;
+} eegan_scale_table;
+long eegan_pipe_workspace(int B, int crop, int max_rows, int nscales, const int* scales);
+int eegan_pipe_transform(const uint8_t* src, const eegan_img_job* jobs, int B, int max_rows, int crop,
+                         const int* coef, const int* bounds, int nscales, const eegan_scale_table* scales,
+                         float* const* out_f32, uint16_t* const* out_bf16, int ld_bf16, uint8_t* crop_u8_out,
+                         void* ws, hipStream_t s);
 
 /* -------------------------------------------------------------------- adam --
  * replaces: torch.optim.Adam(betas=(0.0, 0.9)) of train.py:252-263 on one flat buffer.
