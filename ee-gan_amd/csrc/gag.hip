@@ -11,22 +11,26 @@
 //   att = softmax over s                                            [B][S][Lq]
 //   wc[b][c][q] = sum_s value[b][c][s] att[b][s][q]                 [B][cdf][Lq]
 //
-// Forward: one workgroup per (64 queries, b), 4 waves x 16 queries.  Both
-// contractions are split-bf16 MFMAs (hi*hi + lo*hi + hi*lo, ~fp32 accuracy):
-// the logits over idf in K-steps of 32 (input / key tiles staged in LDS), the
-// softmax in registers (16-lane shuffles), the weighted context over s with
-// att kept in LDS.  S <= 64.
-// Backward (fp32 SIMT; the op is cold): per query tile, g = datt + value^T dwc,
-// dlogits = att (g - <att, g>), dinput = key dlogits, and per-tile partials of
-// dkey = input dlogits^T and dvalue = dwc att^T, reduced over tiles in a
-// fixed order (deterministic, no atomics).
+// Any source length: the source is processed in chunks of 64.  Forward, two
+// kernels, one workgroup per (64 queries, b), 4 waves x 16 queries:
+//   stats: the logits of each chunk (split-bf16 MFMA over idf in K-steps of
+//          32: hi*hi + lo*hi + hi*lo, ~fp32 accuracy), the row max and the
+//          rescaled row sum carried across chunks (online softmax);
+//   ctx:   per 64 output channels (blockIdx.z), each chunk's logits again,
+//          normalised with the final max / sum into att (written once, by
+//          channel group 0), and wc accumulated over the chunks in registers
+//          (split-bf16 MFMA, att staged in LDS).
+// Backward (fp32 SIMT; the op is cold), deterministic (fixed-order sums, no
+// atomics): per query tile g = datt + value^T dwc, <att, g> over all chunks,
+// dlogits = att (g - <att, g>) into the workspace; then dinput = key dlogits,
+// dkey = input dlogits^T and dvalue = dwc att^T, one output element per thread.
 #include "common.h"
 #include "../../include/eegan_hip.h"
 
 namespace {
 
 constexpr int GQ = 64;  // queries per workgroup
-constexpr int GS = 64;  // max source length
+constexpr int GS = 64;  // sources per chunk
 constexpr int GK = 32;  // idf per K-step
 constexpr int KLD = GK + 8;
 constexpr int ALD = GS + 8;
@@ -50,17 +54,18 @@ EE_DEV float xsum16(float v) {
   return v;
 }
 
-__global__ __launch_bounds__(256) void gag_fwd_kernel(const float* __restrict__ in, const float* __restrict__ key,
-                                                      const float* __restrict__ val, const uint8_t* __restrict__ mask,
-                                                      int B, int idf, int cdf, int Lq, int S, float* __restrict__ wc,
-                                                      float* __restrict__ att) {
-  __shared__ __attribute__((aligned(16))) bf16_t inh[GQ][KLD], inl[GQ][KLD];  // query x k
-  __shared__ __attribute__((aligned(16))) bf16_t kh[GS][KLD], kl[GS][KLD];    // source x k
-  __shared__ __attribute__((aligned(16))) bf16_t ah[GQ][ALD], al[GQ][ALD];    // att: query x source
-  __shared__ float af[GS][GQ + 1];                                            // att fp32: source x query
+struct GagSmem {
+  bf16_t inh[GQ][KLD], inl[GQ][KLD];  // query x k
+  bf16_t kh[GS][KLD], kl[GS][KLD];    // source x k
+};
+
+// logits of queries q0.. (this wave: 16 rows) x sources s0..s0+63 into acc[4]
+// (row q = 16 wv + 4 fq + r, column s0 + 16 n + fr); masked / out-of-range
+// columns are -inf
+EE_DEV void chunk_logits(GagSmem& sm, const float* __restrict__ in, const float* __restrict__ key,
+                         const uint8_t* __restrict__ mask, int B, int idf, int Lq, int S, int b, int q0, int s0,
+                         f32x4_t acc[4]) {
   const int t = threadIdx.x, l = t & 63, wv = t >> 6, fr = l & 15, fq = l >> 4;
-  const int b = blockIdx.y, q0 = blockIdx.x * GQ;
-  f32x4_t acc[4];
 #pragma unroll
   for (int n = 0; n < 4; ++n) acc[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   for (int k0 = 0; k0 < idf; k0 += GK) {
@@ -69,77 +74,133 @@ __global__ __launch_bounds__(256) void gag_fwd_kernel(const float* __restrict__ 
       const int k = e / GQ, q = e % GQ;
       const float v = (k0 + k < idf && q0 + q < Lq) ? in[((long)b * idf + k0 + k) * Lq + q0 + q] : 0.f;
       const bf16_t h = f2bf(v);
-      inh[q][k] = h;
-      inl[q][k] = f2bf(v - bf2f(h));
+      sm.inh[q][k] = h;
+      sm.inl[q][k] = f2bf(v - bf2f(h));
     }
     for (int e = t; e < GK * GS; e += 256) {
       const int k = e / GS, s = e % GS;
-      const float v = (k0 + k < idf && s < S) ? key[((long)b * idf + k0 + k) * S + s] : 0.f;
+      const float v = (k0 + k < idf && s0 + s < S) ? key[((long)b * idf + k0 + k) * S + s0 + s] : 0.f;
       const bf16_t h = f2bf(v);
-      kh[s][k] = h;
-      kl[s][k] = f2bf(v - bf2f(h));
+      sm.kh[s][k] = h;
+      sm.kl[s][k] = f2bf(v - bf2f(h));
     }
     __syncthreads();
-    const bf16x8_t a_h = lds_frag(&inh[wv * 16 + fr][fq * 8]), a_l = lds_frag(&inl[wv * 16 + fr][fq * 8]);
+    const bf16x8_t a_h = lds_frag(&sm.inh[wv * 16 + fr][fq * 8]), a_l = lds_frag(&sm.inl[wv * 16 + fr][fq * 8]);
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
-      const bf16x8_t b_h = lds_frag(&kh[n * 16 + fr][fq * 8]), b_l = lds_frag(&kl[n * 16 + fr][fq * 8]);
+      const bf16x8_t b_h = lds_frag(&sm.kh[n * 16 + fr][fq * 8]), b_l = lds_frag(&sm.kl[n * 16 + fr][fq * 8]);
       acc[n] = mfma(a_h, b_h, acc[n]);
       acc[n] = mfma(a_l, b_h, acc[n]);
       acc[n] = mfma(a_h, b_l, acc[n]);
     }
   }
-  // softmax over the source: row q = 16 wv + 4 fq + r, column s = 16 n + fr
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int s = s0 + n * 16 + fr;
+    f32x4_t v = acc[n];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long mrow = ((long)b * Lq + q0 + wv * 16 + fq * 4 + r) % B;
+      const bool off = s >= S || (mask != nullptr && mask[mrow * S + s] != 0);
+      v[r] = off ? -INFINITY : v[r];
+    }
+    acc[n] = v;
+  }
+}
+
+// row max / sum of exp over all sources -> stats[b][q] = (max, sum)
+__global__ __launch_bounds__(256) void gag_stats_kernel(const float* __restrict__ in, const float* __restrict__ key,
+                                                        const uint8_t* __restrict__ mask, int B, int idf, int Lq,
+                                                        int S, float2* __restrict__ stats) {
+  __shared__ __attribute__((aligned(16))) GagSmem sm;
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, fr = l & 15, fq = l >> 4;
+  const int b = blockIdx.y, q0 = blockIdx.x * GQ;
+  float m[4], z[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) m[r] = -INFINITY, z[r] = 0.f;
+  for (int s0 = 0; s0 < S; s0 += GS) {
+    f32x4_t acc[4];
+    chunk_logits(sm, in, key, mask, B, idf, Lq, S, b, q0, s0, acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float cm = fmaxf(fmaxf(acc[0][r], acc[1][r]), fmaxf(acc[2][r], acc[3][r]));
+      cm = xmax16(cm);
+      const float nm = fmaxf(m[r], cm);
+      float e = 0.f;
+      if (nm != -INFINITY) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n) e += expf(acc[n][r] - nm);
+      }
+      e = xsum16(e);
+      z[r] = (m[r] == -INFINITY ? 0.f : z[r] * expf(m[r] - nm)) + e;
+      m[r] = nm;
+    }
+  }
+  if (fr == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = q0 + wv * 16 + fq * 4 + r;
+      if (q < Lq) stats[(long)b * Lq + q] = make_float2(m[r], z[r]);
+    }
+  }
+}
+
+// att (channel group 0 writes it) and wc for 64 output channels (blockIdx.z)
+__global__ __launch_bounds__(256) void gag_ctx_kernel(const float* __restrict__ in, const float* __restrict__ key,
+                                                      const float* __restrict__ val, const uint8_t* __restrict__ mask,
+                                                      const float2* __restrict__ stats, int B, int idf, int cdf,
+                                                      int Lq, int S, float* __restrict__ wc, float* __restrict__ att) {
+  __shared__ __attribute__((aligned(16))) GagSmem sm;
+  __shared__ __attribute__((aligned(16))) bf16_t ah[GQ][ALD], al[GQ][ALD];  // att chunk: query x source
+  __shared__ float af[GS][GQ + 1];                                          // att chunk fp32: source x query
+  const int t = threadIdx.x, l = t & 63, wv = t >> 6, fr = l & 15, fq = l >> 4;
+  const int b = blockIdx.y, q0 = blockIdx.x * GQ, cg = blockIdx.z;
+  float rm[4], rinv[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int q = wv * 16 + fq * 4 + r;
-    const long mrow = ((long)b * Lq + q0 + q) % B;
-    float x[4], m = -INFINITY;
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int s = n * 16 + fr;
-      const bool off = s >= S || (mask != nullptr && mask[mrow * S + s]);
-      x[n] = off ? -INFINITY : acc[n][r];
-      m = fmaxf(m, x[n]);
-    }
-    m = xmax16(m);
-    float sum = 0.f;
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      x[n] = n * 16 + fr < S ? expf(x[n] - m) : 0.f;
-      sum += x[n];
-    }
-    const float inv = 1.f / xsum16(sum);
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int s = n * 16 + fr;
-      const float p = x[n] * inv;
-      const bf16_t h = f2bf(p);
-      ah[q][s] = h;
-      al[q][s] = f2bf(p - bf2f(h));
-      af[s][q] = p;
-    }
+    const int q = q0 + wv * 16 + fq * 4 + r;
+    const float2 st = q < Lq ? stats[(long)b * Lq + q] : make_float2(0.f, 1.f);
+    rm[r] = st.x;
+    rinv[r] = 1.f / st.y;
   }
-  __syncthreads();
-  for (int e = t; e < S * GQ; e += 256) {
-    const int s = e / GQ, q = e % GQ;
-    if (q0 + q < Lq) att[((long)b * S + s) * Lq + q0 + q] = af[s][q];
-  }
-  // wc[c][q] = sum_s value[c][s] att[q][s]: rows c (A from global), columns q (B from LDS)
-  const int nks = (S + 31) / 32;
-  for (int ct = wv; ct * 16 < cdf; ct += 4) {
-    f32x4_t o[4];
+  const int c = cg * 64 + wv * 16 + fr;  // this lane's A-operand row (output channel)
+  f32x4_t o[4];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) o[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    const int c = ct * 16 + fr;
-    for (int ks = 0; ks < nks; ++ks) {
+  for (int n = 0; n < 4; ++n) o[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int s0 = 0; s0 < S; s0 += GS) {
+    f32x4_t acc[4];
+    chunk_logits(sm, in, key, mask, B, idf, Lq, S, b, q0, s0, acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = wv * 16 + fq * 4 + r;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int s = n * 16 + fr;
+        const float p = s0 + s < S ? expf(acc[n][r] - rm[r]) * rinv[r] : 0.f;
+        const bf16_t h = f2bf(p);
+        ah[q][s] = h;
+        al[q][s] = f2bf(p - bf2f(h));
+        af[s][q] = p;
+      }
+    }
+    __syncthreads();
+    if (cg == 0) {
+      const int sn = min(GS, S - s0);
+      for (int e = t; e < sn * GQ; e += 256) {
+        const int s = e / GQ, q = e % GQ;
+        if (q0 + q < Lq) att[((long)b * S + s0 + s) * Lq + q0 + q] = af[s][q];
+      }
+    }
+    // o[c][q] += sum_{s in chunk} value[c][s] att[q][s]: rows c (A from global), columns q (B from LDS)
+#pragma unroll
+    for (int ks = 0; ks < GS / 32; ++ks) {
       uint32_t vh[4], vl[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float v2[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          const int s = ks * 32 + fq * 8 + 2 * j + u;
+          const int s = s0 + ks * 32 + fq * 8 + 2 * j + u;
           v2[u] = (c < cdf && s < S) ? val[((long)b * cdf + c) * S + s] : 0.f;
         }
         const bf16_t h0 = f2bf(v2[0]), h1 = f2bf(v2[1]);
@@ -157,110 +218,103 @@ __global__ __launch_bounds__(256) void gag_fwd_kernel(const float* __restrict__ 
         o[n] = mfma(a_h, b_l, o[n]);
       }
     }
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int cc = ct * 16 + fq * 4 + r, q = q0 + n * 16 + fr;
-        if (cc < cdf && q < Lq) wc[((long)b * cdf + cc) * Lq + q] = o[n][r];
-      }
+    // the next chunk's logits re-stage sm behind a barrier; ah / al / af are
+    // rewritten only after it, by which point every wave has consumed them
   }
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int cc = cg * 64 + wv * 16 + fq * 4 + r, q = q0 + n * 16 + fr;
+      if (cc < cdf && q < Lq) wc[((long)b * cdf + cc) * Lq + q] = o[n][r];
+    }
 }
 
-// backward of one query tile; partial dkey / dvalue of the tile into ws
-__global__ __launch_bounds__(256) void gag_bwd_tile_kernel(const float* __restrict__ in, const float* __restrict__ key,
-                                                           const float* __restrict__ val,
-                                                           const float* __restrict__ att,
-                                                           const float* __restrict__ dwc,
-                                                           const float* __restrict__ datt, int B, int idf, int cdf,
-                                                           int Lq, int S, float* __restrict__ din,
-                                                           float* __restrict__ pkey, float* __restrict__ pval) {
-  __shared__ float pa[GS][GQ + 1];  // att (source x query)
-  __shared__ float dl[GS][GQ + 1];  // dlogits
+// dlogits of one query tile over all sources (two passes: <att, g>, then
+// att (g - <att, g>)), written to dl[b][s][q]
+__global__ __launch_bounds__(256) void gag_bwd_dl_kernel(const float* __restrict__ val, const float* __restrict__ att,
+                                                         const float* __restrict__ dwc, const float* __restrict__ datt,
+                                                         int cdf, int Lq, int S, float* __restrict__ dl) {
   __shared__ float rdot[4][GQ];
   const int t = threadIdx.x, lq = t & 63, wv = t >> 6;
-  const int b = blockIdx.y, q0 = blockIdx.x * GQ, tile = blockIdx.x;
-  const int q = q0 + lq;
+  const int b = blockIdx.y, q = blockIdx.x * GQ + lq;
   const bool qok = q < Lq;
-  for (int e = t; e < GS * GQ; e += 256) {
-    const int s = e / GQ, qq = e % GQ;
-    pa[s][qq] = (s < S && q0 + qq < Lq) ? att[((long)b * S + s) * Lq + q0 + qq] : 0.f;
-  }
-  __syncthreads();
-  // g[s][q] = datt[s][q] + sum_c dwc[c][q] value[c][s], s = wv + 4 i
-  float g[GS / 4];
-#pragma unroll
-  for (int i = 0; i < GS / 4; ++i) {
-    const int s = wv + 4 * i;
-    g[i] = (datt != nullptr && qok && s < S) ? datt[((long)b * S + s) * Lq + q] : 0.f;
-  }
-  if (dwc != nullptr) {
-    for (int c = 0; c < cdf; ++c) {
-      const float dw = qok ? dwc[((long)b * cdf + c) * Lq + q] : 0.f;
-      const float* vr = val + ((long)b * cdf + c) * S;
+  float dot = 0.f;
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int s0 = 0; s0 < S; s0 += GS) {
+      float g[GS / 4];
 #pragma unroll
       for (int i = 0; i < GS / 4; ++i) {
-        const int s = wv + 4 * i;
-        if (s < S) g[i] += dw * vr[s];
+        const int s = s0 + wv + 4 * i;
+        g[i] = (datt != nullptr && qok && s < S) ? datt[((long)b * S + s) * Lq + q] : 0.f;
+      }
+      if (dwc != nullptr) {
+        for (int c = 0; c < cdf; ++c) {
+          const float dw = qok ? dwc[((long)b * cdf + c) * Lq + q] : 0.f;
+          const float* vr = val + ((long)b * cdf + c) * S;
+#pragma unroll
+          for (int i = 0; i < GS / 4; ++i) {
+            const int s = s0 + wv + 4 * i;
+            if (s < S) g[i] += dw * vr[s];
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < GS / 4; ++i) {
+        const int s = s0 + wv + 4 * i;
+        const float p = (qok && s < S) ? att[((long)b * S + s) * Lq + q] : 0.f;
+        if (pass == 0) {
+          dot += p * g[i];
+        } else if (qok && s < S) {
+          dl[((long)b * S + s) * Lq + q] = p == 0.f ? 0.f : p * (g[i] - dot);
+        }
       }
     }
-  }
-  float dot = 0.f;
-#pragma unroll
-  for (int i = 0; i < GS / 4; ++i) dot += pa[wv + 4 * i][lq] * g[i];
-  rdot[wv][lq] = dot;
-  __syncthreads();
-  dot = rdot[0][lq] + rdot[1][lq] + rdot[2][lq] + rdot[3][lq];
-#pragma unroll
-  for (int i = 0; i < GS / 4; ++i) {
-    const int s = wv + 4 * i;
-    const float p = pa[s][lq];
-    dl[s][lq] = p == 0.f ? 0.f : p * (g[i] - dot);
-  }
-  __syncthreads();
-  // dinput[d][q] = sum_s key[d][s] dl[s][q]
-  for (int d = wv; d < idf; d += 4) {
-    const float* kr = key + ((long)b * idf + d) * S;
-    float v = 0.f;
-    for (int s = 0; s < S; ++s) v += kr[s] * dl[s][lq];
-    if (qok) din[((long)b * idf + d) * Lq + q] = v;
-  }
-  // partials over this tile's queries: lane = source s
-  const int s = lq;
-  for (int d = wv; d < idf; d += 4) {
-    const float* ir = in + ((long)b * idf + d) * Lq + q0;
-    float v = 0.f;
-    for (int qq = 0; qq < GQ && q0 + qq < Lq; ++qq) v += ir[qq] * dl[s][qq];
-    if (s < S) pkey[(((long)tile * B + b) * idf + d) * S + s] = v;
-  }
-  for (int c = wv; c < cdf; c += 4) {
-    float v = 0.f;
-    if (dwc != nullptr) {
-      const float* dr = dwc + ((long)b * cdf + c) * Lq + q0;
-      for (int qq = 0; qq < GQ && q0 + qq < Lq; ++qq) v += dr[qq] * pa[s][qq];
+    if (pass == 0) {
+      rdot[wv][lq] = dot;
+      __syncthreads();
+      dot = rdot[0][lq] + rdot[1][lq] + rdot[2][lq] + rdot[3][lq];
     }
-    if (s < S) pval[(((long)tile * B + b) * cdf + c) * S + s] = v;
   }
 }
 
-// fixed-order sum of the per-tile partials
-__global__ __launch_bounds__(256) void gag_bwd_reduce_kernel(const float* __restrict__ part, int ntile, long n,
-                                                             float* __restrict__ out) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
+// dinput[b][d][q] = sum_s key[b][d][s] dl[b][s][q]
+__global__ __launch_bounds__(256) void gag_bwd_din_kernel(const float* __restrict__ key, const float* __restrict__ dl,
+                                                          int idf, int Lq, int S, float* __restrict__ din) {
+  const int q = blockIdx.x * 256 + threadIdx.x, d = blockIdx.y, b = blockIdx.z;
+  if (q >= Lq) return;
+  const float* kr = key + ((long)b * idf + d) * S;
+  const float* dr = dl + (long)b * S * Lq + q;
   float v = 0.f;
-  for (int k = 0; k < ntile; ++k) v += part[(long)k * n + i];
-  out[i] = v;
+  for (int s = 0; s < S; ++s) v += kr[s] * dr[(long)s * Lq];
+  din[((long)b * idf + d) * Lq + q] = v;
+}
+
+// out[b][r][s] = sum_q x[b][r][q] y[b][s][q]  (dkey: x = input, y = dl; dvalue: x = dwc, y = att)
+__global__ __launch_bounds__(256) void gag_bwd_rowdot_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                             int R, int Lq, int S, float* __restrict__ out) {
+  const int s = blockIdx.x * 256 + threadIdx.x, r = blockIdx.y, b = blockIdx.z;
+  if (s >= S) return;
+  const float* xr = x + ((long)b * R + r) * Lq;
+  const float* yr = y + ((long)b * S + s) * Lq;
+  float v = 0.f;
+  for (int q = 0; q < Lq; ++q) v += xr[q] * yr[q];
+  out[((long)b * R + r) * S + s] = v;
+}
+
+__global__ void fill_zero_kernel(float* __restrict__ p, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) p[i] = 0.f;
 }
 
 bool gag_check(int B, int idf, int cdf, int Lq, int S, const char* what) {
-  if (B < 1 || idf < 1 || cdf < 1 || Lq < 1 || S < 1 || S > GS) {
-    ee_set_error("%s: need B, idf, cdf, queryL >= 1 and 1 <= sourceL <= %d (B=%d idf=%d cdf=%d queryL=%d sourceL=%d)",
-                 what, GS, B, idf, cdf, Lq, S);
+  if (B < 1 || idf < 1 || cdf < 1 || Lq < 1 || S < 1) {
+    ee_set_error("%s: need B, idf, cdf, queryL, sourceL >= 1 (B=%d idf=%d cdf=%d queryL=%d sourceL=%d)", what, B, idf,
+                 cdf, Lq, S);
     return false;
   }
-  if ((long)B * Lq >= (1L << 31)) {
-    ee_set_error("%s: B * queryL too large", what);
+  if ((long)B * Lq >= (1L << 31) || (long)B * S * Lq >= (1L << 40) || cdf > 65535 * 64 || idf > 65535) {
+    ee_set_error("%s: sizes too large", what);
     return false;
   }
   return true;
@@ -270,37 +324,50 @@ bool gag_check(int B, int idf, int cdf, int Lq, int S, const char* what) {
 
 extern "C" {
 
+long eegan_gag_fwd_workspace(int B, int queryL) { return (long)B * queryL * (long)sizeof(float2); }
+
 int eegan_gag_fwd(const float* input, const float* context_key, const float* content_value, const unsigned char* mask,
-                  int B, int idf, int cdf, int queryL, int sourceL, float* weighted_context, float* attn,
+                  int B, int idf, int cdf, int queryL, int sourceL, float* weighted_context, float* attn, void* ws,
                   hipStream_t s) {
   if (!gag_check(B, idf, cdf, queryL, sourceL, "gag_fwd")) return -22;
-  ee_launch(gag_fwd_kernel, dim3((queryL + GQ - 1) / GQ, B), dim3(256), 0, s, input, context_key, content_value,
-            (const uint8_t*)mask, B, idf, cdf, queryL, sourceL, weighted_context, attn);
-  return ee_check_launch("gag_fwd");
+  const dim3 grid((queryL + GQ - 1) / GQ, B);
+  float2* stats = static_cast<float2*>(ws);
+  ee_launch(gag_stats_kernel, grid, dim3(256), 0, s, input, context_key, (const uint8_t*)mask, B, idf, queryL,
+            sourceL, stats);
+  int rc = ee_check_launch("gag_fwd(stats)");
+  if (rc) return rc;
+  ee_launch(gag_ctx_kernel, dim3(grid.x, B, (cdf + 63) / 64), dim3(256), 0, s, input, context_key, content_value,
+            (const uint8_t*)mask, (const float2*)stats, B, idf, cdf, queryL, sourceL, weighted_context, attn);
+  return ee_check_launch("gag_fwd(ctx)");
 }
 
 long eegan_gag_workspace(int B, int idf, int cdf, int queryL, int sourceL) {
-  const long ntile = (queryL + GQ - 1) / GQ;
-  return ntile * B * (long)(idf + cdf) * sourceL * (long)sizeof(float);
+  return (long)B * sourceL * queryL * (long)sizeof(float);
 }
 
 int eegan_gag_bwd(const float* input, const float* context_key, const float* content_value, const float* attn,
                   const float* d_weighted_context, const float* d_attn, int B, int idf, int cdf, int queryL,
                   int sourceL, float* d_input, float* d_key, float* d_value, void* ws, hipStream_t s) {
   if (!gag_check(B, idf, cdf, queryL, sourceL, "gag_bwd")) return -22;
-  const int ntile = (queryL + GQ - 1) / GQ;
-  float* pkey = static_cast<float*>(ws);
-  float* pval = pkey + (long)ntile * B * idf * sourceL;
-  ee_launch(gag_bwd_tile_kernel, dim3(ntile, B), dim3(256), 0, s, input, context_key, content_value, attn,
-            d_weighted_context, d_attn, B, idf, cdf, queryL, sourceL, d_input, pkey, pval);
-  int rc = ee_check_launch("gag_bwd_tile");
+  float* dl = static_cast<float*>(ws);
+  ee_launch(gag_bwd_dl_kernel, dim3((queryL + GQ - 1) / GQ, B), dim3(256), 0, s, content_value, attn,
+            d_weighted_context, d_attn, cdf, queryL, sourceL, dl);
+  int rc = ee_check_launch("gag_bwd(dl)");
   if (rc) return rc;
-  const long nk = (long)B * idf * sourceL, nv = (long)B * cdf * sourceL;
-  ee_launch(gag_bwd_reduce_kernel, dim3((nk + 255) / 256), dim3(256), 0, s, (const float*)pkey, ntile, nk, d_key);
-  rc = ee_check_launch("gag_bwd_reduce");
-  if (rc) return rc;
-  ee_launch(gag_bwd_reduce_kernel, dim3((nv + 255) / 256), dim3(256), 0, s, (const float*)pval, ntile, nv, d_value);
-  return ee_check_launch("gag_bwd_reduce");
+  ee_launch(gag_bwd_din_kernel, dim3((queryL + 255) / 256, idf, B), dim3(256), 0, s, context_key, (const float*)dl,
+            idf, queryL, sourceL, d_input);
+  if ((rc = ee_check_launch("gag_bwd(dinput)"))) return rc;
+  ee_launch(gag_bwd_rowdot_kernel, dim3((sourceL + 255) / 256, idf, B), dim3(256), 0, s, input, (const float*)dl, idf,
+            queryL, sourceL, d_key);
+  if ((rc = ee_check_launch("gag_bwd(dkey)"))) return rc;
+  if (d_weighted_context != nullptr) {
+    ee_launch(gag_bwd_rowdot_kernel, dim3((sourceL + 255) / 256, cdf, B), dim3(256), 0, s, d_weighted_context, attn,
+              cdf, queryL, sourceL, d_value);
+  } else {
+    const long n = (long)B * cdf * sourceL;
+    ee_launch(fill_zero_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_value, n);
+  }
+  return ee_check_launch("gag_bwd(dvalue)");
 }
 
 }  // extern "C"

@@ -113,7 +113,8 @@ _SIGS = {
     'eegan_words_sim_bwd': ([P, P, P, I, I, I, P, P, P, P, I, P], I),
     'eegan_sim_ce': ([P, I, P, P, P, P], I),
     'eegan_sim_ce_bwd': ([P, I, P, P, P, P, P], I),
-    'eegan_gag_fwd': ([P, P, P, P, I, I, I, I, I, P, P, P], I),
+    'eegan_gag_fwd_workspace': ([I, I], L),
+    'eegan_gag_fwd': ([P, P, P, P, I, I, I, I, I, P, P, P, P], I),
     'eegan_gag_workspace': ([I, I, I, I, I], L),
     'eegan_gag_bwd': ([P, P, P, P, P, P, I, I, I, I, I, P, P, P, P, P], I),
     'eegan_sent_sim': ([P, P, I, I, I, P, P], I),
@@ -150,7 +151,7 @@ def _load():
 
 LIB = _load()
 ABI_VERSION = LIB.eegan_abi_version()
-EXPECTED_ABI = 6
+EXPECTED_ABI = 7
 if ABI_VERSION != EXPECTED_ABI:
     raise ImportError('%s has ABI %d, these bindings need %d: rebuild (make -C ee-gan_amd/csrc)'
                       % (LIB_PATH, ABI_VERSION, EXPECTED_ABI))

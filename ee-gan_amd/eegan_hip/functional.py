@@ -1586,8 +1586,9 @@ class GlobalAttentionFn(torch.autograd.Function):
         m = mask.to(device=inp.device, dtype=torch.uint8).contiguous() if mask is not None else None
         wc = torch.empty((B, cdf, ih, iw), dtype=F32, device=inp.device)
         att = torch.empty((B, S, ih, iw), dtype=F32, device=inp.device)
+        ws = workspace(ops.gag_fwd_workspace(B, Lq), inp.device)
         ops.gag_fwd(x.data_ptr(), k.data_ptr(), v.data_ptr(), ptr(m), B, idf, cdf, Lq, S, wc.data_ptr(),
-                    att.data_ptr(), stream())
+                    att.data_ptr(), ws.data_ptr(), stream())
         ctx.save_for_backward(x, k, v, att)
         return wc, att
 

@@ -47,7 +47,7 @@ def func_attention(query, context, gamma1):
 
 class GlobalAttentionGeneral(nn.Module):
     """word <-> feature-map attention (DAMSM_losses.py:65-132; unused by the reference step).
-    sourceL <= 64; the mask (B, sourceL) bool is applied like the reference's
+    Any sourceL (64-source chunks, online softmax); the mask (B, sourceL) bool is applied like the reference's
     ``mask.repeat(queryL, 1)`` (row b*queryL + q reads mask[(b*queryL + q) % B])."""
 
     def __init__(self, idf, cdf):

@@ -26,10 +26,11 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 6  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
+#define EEGAN_ABI_VERSION 7  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
                                 4: rectangular (local x global) DAMSM words / sentence blocks on MFMA;
                                 5: GlobalAttentionGeneral (eegan_gag_*), words backward reuses the forward's prep;
-                                6: device input pipeline (eegan_pipe_*) */
+                                6: device input pipeline (eegan_pipe_*);
+                                7: GlobalAttentionGeneral for any source length (eegan_gag_fwd workspace) */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
@@ -253,11 +254,13 @@ int eegan_sent_sim_bwd(const float* cnn, const float* rnn, int na, int nb, int D
 /* GlobalAttentionGeneral.forward (DAMSM_losses.py:65-132; defined, never called by the reference step):
  * input [B][idf][queryL] (queryL = ih*iw), context_key [B][idf][sourceL], content_value [B][cdf][sourceL],
  * mask (optional) uint8 [B][sourceL], row (b, q) masked by mask[(b*queryL + q) % B] exactly like the
- * reference's mask.repeat(queryL, 1); sourceL <= 64.  weighted_context [B][cdf][queryL], attn [B][sourceL][queryL].
+ * reference's mask.repeat(queryL, 1); any sourceL (chunks of 64, online softmax statistics in
+ * ws: eegan_gag_fwd_workspace bytes).  weighted_context [B][cdf][queryL], attn [B][sourceL][queryL].
  * Backward: d_weighted_context / d_attn may be NULL (no gradient); d_input [B][idf][queryL], d_key, d_value
- * overwritten; ws of eegan_gag_workspace bytes. */
+ * overwritten; ws of eegan_gag_workspace bytes; deterministic. */
+long eegan_gag_fwd_workspace(int B, int queryL);
 int eegan_gag_fwd(const float* input, const float* context_key, const float* content_value, const unsigned char* mask,
-                  int B, int idf, int cdf, int queryL, int sourceL, float* weighted_context, float* attn,
+                  int B, int idf, int cdf, int queryL, int sourceL, float* weighted_context, float* attn, void* ws,
                   hipStream_t s);
 long eegan_gag_workspace(int B, int idf, int cdf, int queryL, int sourceL);
 int eegan_gag_bwd(const float* input, const float* context_key, const float* content_value, const float* attn,

@@ -2,7 +2,8 @@
 against the golden vectors captured from the reference
 (DAMSM_losses.py:65-132: damsm/gag_wc, damsm/gag_att, which include the
 reference's mask.repeat(queryL, 1) row indexing) and against the fp32 oracle's
-autograd for the backward.
+autograd for the backward, for source lengths within one 64-source chunk and
+across several (100, 300: the online-softmax path).
 
 Tolerances: the logits and the weighted context are split-bf16 MFMA products
 (hi*hi + lo*hi + hi*lo, relative error per product ~2^-16), so the forward is
@@ -50,6 +51,9 @@ def test_gag_golden(gpu):
     (3, 48, 40, 20, 20, 37, True),   # 7 query tiles (ragged last), ragged idf / cdf K-steps
     (1, 7, 3, 1, 5, 64, False),      # queryL < one tile, sourceL at the maximum, tiny channels
     (4, 256, 32, 17, 17, 18, True),  # DAMSM-like shapes: 289 regions x 18 words
+    (2, 64, 96, 9, 11, 100, True),   # sources beyond one 64-chunk: 2 chunks, 2 channel groups
+    (2, 40, 24, 5, 7, 300, True),    # 5 chunks, ragged last chunk, masked tails
+    (1, 16, 8, 3, 3, 300, False),
 ])
 def test_gag_fwd_bwd(gpu, B, idf, cdf, ih, iw, S, masked):
     from oracle import eegan_oracle as O
@@ -86,8 +90,10 @@ def test_gag_fwd_bwd(gpu, B, idf, cdf, ih, iw, S, masked):
         assert torch.equal(a, b)
 
 
-def test_gag_rejects_long_source(gpu):
-    from eegan_hip._lib import HipError
-    x = torch.randn(1, 8, 4, 4, device=gpu)
-    with pytest.raises(HipError, match='sourceL'):
-        _module(None)(x, torch.randn(1, 8, 65, device=gpu), torch.randn(1, 8, 65, device=gpu))
+def test_gag_fully_masked_row_is_nan_like_the_reference(gpu):
+    """A row whose sources are all masked: the reference's softmax of an
+    all -inf row gives NaN (DAMSM_losses.py:121-122); so does the kernel."""
+    x = torch.randn(1, 8, 2, 2, device=gpu)
+    key, val = torch.randn(1, 8, 70, device=gpu), torch.randn(1, 4, 70, device=gpu)
+    wc, att = _module(torch.ones(1, 70, dtype=torch.bool, device=gpu))(x, key, val)
+    assert torch.isnan(att).all() and torch.isnan(wc).all()
