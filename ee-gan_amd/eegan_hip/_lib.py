@@ -132,6 +132,9 @@ _SIGS = {
     'eegan_adam': ([P, P, P, P, L, F, F, F, F, F, P, P], I),
     'eegan_embedding': ([P, L, P, I, P, P], I),
     'eegan_lstm_bidir': ([P, P, P, I, I, I, I, P, P, P], I),
+    'eegan_fid_preprocess': ([P, I, I, I, I, I, P, P, P, I, P], I),
+    'eegan_fid_stats_workspace': ([I], L),
+    'eegan_fid_stats': ([P, I, I, P, P, P, P], I),
     'eegan_pipe_workspace': ([I, I, I, I, P], L),
     'eegan_pipe_transform': ([P, P, I, I, I, P, P, I, P, P, P, I, P, P, P], I),
 }
@@ -151,7 +154,7 @@ def _load():
 
 LIB = _load()
 ABI_VERSION = LIB.eegan_abi_version()
-EXPECTED_ABI = 7
+EXPECTED_ABI = 8
 if ABI_VERSION != EXPECTED_ABI:
     raise ImportError('%s has ABI %d, these bindings need %d: rebuild (make -C ee-gan_amd/csrc)'
                       % (LIB_PATH, ABI_VERSION, EXPECTED_ABI))

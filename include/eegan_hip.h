@@ -26,11 +26,12 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 7  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
+#define EEGAN_ABI_VERSION 8  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
                                 4: rectangular (local x global) DAMSM words / sentence blocks on MFMA;
                                 5: GlobalAttentionGeneral (eegan_gag_*), words backward reuses the forward's prep;
                                 6: device input pipeline (eegan_pipe_*);
-                                7: GlobalAttentionGeneral for any source length (eegan_gag_fwd workspace) */
+                                7: GlobalAttentionGeneral for any source length (eegan_gag_fwd workspace);
+                                8: FID leg (eegan_fid_*) */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
@@ -331,6 +332,18 @@ int eegan_pipe_transform(const uint8_t* src, const eegan_img_job* jobs, int B, i
                          const int* coef, const int* bounds, int nscales, const eegan_scale_table* scales,
                          float* const* out_f32, uint16_t* const* out_bf16, int ld_bf16, uint8_t* crop_u8_out,
                          void* ws, hipStream_t s);
+
+/* ------------------------------------------------------------------- FID leg --
+ * replaces: InceptionV3.forward's input handling (metrics/FID/inception.py:131-138) and the activation
+ * statistics of fid_score.py:110-127 (np.mean / np.cov of the float64 pool_3 activations).
+ * preprocess: x NCHW fp32 [N][3][H][W] in [0, 1] -> bilinear (align_corners=True) to Ho x Wo, then
+ * x * scale3[c] + shift3[c] (host arrays of 3), written NHWC bf16 with channel stride ldy (>= 3, padding zeroed).
+ * stats: act fp32 [N][D] -> mu fp64 [D], sigma fp64 [D][D] (divisor N - 1), deterministic; ws of
+ * eegan_fid_stats_workspace bytes; synchronises the stream once (tile list upload). */
+int eegan_fid_preprocess(const float* x, int N, int H, int W, int Ho, int Wo, const float* scale3,
+                         const float* shift3, uint16_t* y, int ldy, hipStream_t s);
+long eegan_fid_stats_workspace(int D);
+int eegan_fid_stats(const float* act, int N, int D, double* mu, double* sigma, void* ws, hipStream_t s);
 
 /* -------------------------------------------------------------------- adam --
  * replaces: torch.optim.Adam(betas=(0.0, 0.9)) of train.py:252-263 on one flat buffer.

@@ -614,6 +614,38 @@ def cnn_encoder(sd, x):
     return feats, code
 
 
+def fid_inception(sd, x, output_blocks=(3,)):
+    """InceptionV3.forward of the FID leg (metrics/FID/inception.py:115-147).
+    PARITY UNPINNED: the blocks are torchvision's inception_v3 (absent here),
+    restated as in cnn_encoder; eval-mode BN.  x: (B, 3, H, W) in [0, 1]."""
+    x = F.interpolate(x, size=(299, 299), mode='bilinear', align_corners=True)
+    x = x.clone()
+    x[:, 0] = x[:, 0] * (0.229 / 0.5) + (0.485 - 0.5) / 0.5
+    x[:, 1] = x[:, 1] * (0.224 / 0.5) + (0.456 - 0.5) / 0.5
+    x[:, 2] = x[:, 2] * (0.225 / 0.5) + (0.406 - 0.5) / 0.5
+    out = []
+    x = _basic_conv(sd, 'Conv2d_1a_3x3.', x, stride=2)
+    x = _basic_conv(sd, 'Conv2d_2a_3x3.', x)
+    x = F.max_pool2d(_basic_conv(sd, 'Conv2d_2b_3x3.', x, pad=1), 3, 2)
+    if 0 in output_blocks:
+        out.append(x)
+    x = _basic_conv(sd, 'Conv2d_3b_1x1.', x)
+    x = F.max_pool2d(_basic_conv(sd, 'Conv2d_4a_3x3.', x), 3, 2)
+    if 1 in output_blocks:
+        out.append(x)
+    for n in ['Mixed_5b', 'Mixed_5c', 'Mixed_5d']:
+        x = _incA(sd, n + '.', x)
+    x = _incB(sd, 'Mixed_6a.', x)
+    for n in ['Mixed_6b', 'Mixed_6c', 'Mixed_6d', 'Mixed_6e']:
+        x = _incC(sd, n + '.', x)
+    if 2 in output_blocks:
+        out.append(x)
+    x = _incE(sd, 'Mixed_7c.', _incE(sd, 'Mixed_7b.', _incD(sd, 'Mixed_7a.', x)))
+    if 3 in output_blocks:
+        out.append(F.adaptive_avg_pool2d(x, (1, 1)))
+    return out
+
+
 def standin_image_encoder(sd, x):
     """The small image encoder used by the golden full-step fixtures in place
     of Inception-v3 (which needs torchvision): regions = conv15x15/s15 (3->256)
