@@ -110,6 +110,64 @@ def _sink_of(ctx, i):
     return g
 
 
+# Weight gradients on a side stream (EEGAN_WGRAD_SIDE=1): a direct-sink dW
+# (first-order backward, accumulated straight into the FlatAdam flat gradient)
+# is launched on a side stream of the current one, forked behind the kernels
+# that produced its operands, so it runs beside the data-gradient chain that
+# the next layer's backward waits for.  The owning FlatAdam joins its side
+# streams at step(); the operands are recorded on the side stream so their
+# memory is not reused before it has run.  Side streams are created on first
+# use (outside graph capture: a warm-up step creates them).  Only streams in
+# WGRAD_SIDE_FROM fork them (the trainer puts its step's main stream there):
+# a side stream forked from a stream that is itself forked into a graph
+# capture (a discriminator lane) makes the runtime's capture-end walk recurse
+# without end (stack overflow in hipStreamEndCapture, ROCm 7.0; the same
+# failure as round 2's per-lane side streams and Inception branch streams).
+WGRAD_SIDE = os.environ.get('EEGAN_WGRAD_SIDE', '0') == '1'
+WGRAD_SIDE_FROM = set()
+_SIDES = {}
+
+
+def _side_of(cur):
+    s = _SIDES.get(cur.cuda_stream)
+    if s is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError('weight-gradient side stream first needed during graph capture: run an eager '
+                               'warm-up step first')
+        s = _SIDES[cur.cuda_stream] = T.new_stream(cur.device)
+    return s
+
+
+def _sink_wgrad(ctx, i, x, dz, g, W_shape):
+    """dW of input i accumulated into its FlatAdam gradient view; False when
+    the gradient has to go through autograd instead."""
+    side = owner = None
+    if WGRAD_SIDE and _sink_of(ctx, i) is not None:
+        owner = getattr(ctx.next_functions[i][0].variable, '_eegan_opt', None)
+        cur = torch.cuda.current_stream()
+        if owner is not None and cur.cuda_stream in WGRAD_SIDE_FROM:
+            side = _side_of(cur)
+            side.wait_stream(cur)
+    with torch.cuda.stream(side) if side is not None else _NullCtx():
+        sink = _grad_sink(ctx, i)
+        if sink is None or not sink.is_contiguous(memory_format=CL):
+            return False
+        conv_bwd_weight_raw(x, dz, g, W_shape, out=sink)
+    if side is not None:
+        x.record_stream(side)
+        dz.record_stream(side)
+        owner._pending_sides.add(side)
+    return True
+
+
+class _NullCtx(object):
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
 # ============================================================== weights ===
 class PackCache:
     """bf16 packed images of one conv weight (forward and bwd-data layouts),
@@ -420,12 +478,8 @@ class Conv2dFn(torch.autograd.Function):
                                        gate_slope=ctx.in_slope)
             else:
                 dx = ConvBwdDataFn.apply(dz, W, g, ctx.x_shape, ctx.cache)
-        if _needed(ctx, 1):
-            sink = _grad_sink(ctx, 1)
-            if sink is not None and sink.is_contiguous(memory_format=CL):
-                conv_bwd_weight_raw(x, dz, g, W.shape, out=sink)
-            else:
-                dW = ConvBwdWeightFn.apply(x, dz, g) if not g.up2 else conv_bwd_weight_raw(x, dz, g, W.shape)
+        if _needed(ctx, 1) and not _sink_wgrad(ctx, 1, x, dz, g, W.shape):
+            dW = ConvBwdWeightFn.apply(x, dz, g) if not g.up2 else conv_bwd_weight_raw(x, dz, g, W.shape)
         if ctx.needs_input_grad[2] and _needed(ctx, 2):
             sink = _grad_sink(ctx, 2)
             if sink is not None:
@@ -506,13 +560,9 @@ class ConvBwdDataFn(torch.autograd.Function):
         g_dz = g_W = None
         if ctx.needs_input_grad[0]:
             g_dz = Conv2dFn.apply(gdx, W, None, ctx.g, 0, 0.0, False, ctx.cache)
-        if ctx.needs_input_grad[1] and _needed(ctx, 1):
-            sink = _grad_sink(ctx, 1)
-            if sink is not None and sink.is_contiguous(memory_format=CL):
-                # the gradient penalty's second backward: dW straight into p.grad
-                conv_bwd_weight_raw(gdx, dz, ctx.g, W.shape, out=sink)
-            else:
-                g_W = ConvBwdWeightFn.apply(gdx, dz, ctx.g)
+        # the gradient penalty's second backward: dW straight into p.grad when it can
+        if ctx.needs_input_grad[1] and _needed(ctx, 1) and not _sink_wgrad(ctx, 1, gdx, dz, ctx.g, W.shape):
+            g_W = ConvBwdWeightFn.apply(gdx, dz, ctx.g)
         return g_dz, g_W, None, None, None
 
 

@@ -11,6 +11,7 @@ cap_lens.tolist()).  Scalar loss combinations stay torch expressions on
 """
 import contextlib
 import os
+import sys
 
 import torch
 
@@ -35,7 +36,9 @@ def prepare_class_labels(batch_size, class_num, class_ids, device):
     return lab
 
 
-LANE_PRIO = os.environ.get('EEGAN_LANE_PRIO', '1') != '0'
+# EEGAN_LANE_PRIO: 1 the largest D's lane at the highest stream priority, the
+# others default; 2 the others at the lowest priority too; 0 all default
+LANE_PRIO = int(os.environ.get('EEGAN_LANE_PRIO', '1'))
 # EEGAN_G_EARLY=0: g_update's passes through the three D's wait for all of d_update.
 G_EARLY = os.environ.get('EEGAN_G_EARLY', '1') != '0'
 # EEGAN_DAMSM_EARLY=0: the DAMSM branch runs inside g_update, after d_update (A/B switch).
@@ -82,7 +85,8 @@ class Trainer(object):
             # path through d_update and g_update) at high priority, the others
             # filling around it (EEGAN_LANE_PRIO=0: all default)
             hi = len(self.netsD) - 1 if LANE_PRIO else -1
-            self._streams = [new_stream(self.device, 1 if i == hi else 0) for i in range(n)]
+            lo = -1 if LANE_PRIO == 2 else 0
+            self._streams = [new_stream(self.device, 1 if i == hi else lo) for i in range(n)]
             for i, st in enumerate(self._streams):
                 D.bind_stream(st, i)   # one RCCL communicator per stream lane
         main = torch.cuda.current_stream()
@@ -412,6 +416,8 @@ class Trainer(object):
         """One iteration of train.py:163-206 on a device-resident batch."""
         B = self.batch_size
         dev = self.device
+        if Fn.WGRAD_SIDE and self.use_streams:
+            Fn.WGRAD_SIDE_FROM.add(torch.cuda.current_stream().cuda_stream)
         Fn.stamp('start')
         words, sent, attrs, unpair = emb if emb is not None else self.encode_text(batch)
         Fn.stamp('text encode')
@@ -472,11 +478,19 @@ class StepGraph(object):
         # gathers, gradient buckets) are captured too; thread-local capture
         # keeps the process group's watchdog thread from invalidating it
         mode = 'thread_local' if D.collective() else 'global'
+        dbg = os.environ.get('EEGAN_DEBUG_CAPTURE') == '1'
+
         def capture():
             # captured on the stream the warm-up ran on: per-stream side streams
             # (weight gradients) were created there, outside the capture
+            if dbg:
+                print('StepGraph: capture begin', file=sys.stderr, flush=True)
             with torch.cuda.graph(self.graph, stream=side, capture_error_mode=mode):
                 self.out = trainer.train_step(batch, **step_kw)
+                if dbg:
+                    print('StepGraph: step recorded, ending capture', file=sys.stderr, flush=True)
+            if dbg:
+                print('StepGraph: capture ended (instantiated)', file=sys.stderr, flush=True)
 
         try:
             stack_mb = int(os.environ.get('EEGAN_CAPTURE_STACK_MB', '0'))
