@@ -49,6 +49,17 @@ DAMSM_GRAD_EARLY = os.environ.get('EEGAN_DAMSM_GRAD_EARLY', '1') != '0'
 # first packets of the critical lane then do not queue behind the others' (C2: 678 vs 656 img/s,
 # tools/gpu_lane_ab.sh); EEGAN_LANE_ORDER=fwd: D64, D128, D256 after the DAMSM lane
 LANE_ORDER = os.environ.get('EEGAN_LANE_ORDER', 'rev')
+# EEGAN_LATE_JOIN=1: the discriminator lanes are joined into the main stream only
+# after g_update's backward: the backward starts from the per-D terms as roots
+# (their gradients flow lane -> generator, the generator's kernels wait for a
+# lane only where they consume its image gradient), so a lane still busy with
+# its update does not hold up the generator's backward.
+LATE_JOIN = os.environ.get('EEGAN_LATE_JOIN', '0') == '1'
+# EEGAN_DEFER_D=<phase>: the smaller discriminators' lanes start only after the
+# largest D's lane has finished <phase> (a d_update stamp name, e.g. 'loss
+# backward'): they stop competing with the critical lane and fill the GPU
+# during the generator's backward instead (needs LATE_JOIN).
+DEFER_D = os.environ.get('EEGAN_DEFER_D', '').replace('_', ' ')   # underscores stand for spaces
 
 
 class Trainer(object):
@@ -76,8 +87,9 @@ class Trainer(object):
             streams = os.environ.get('EEGAN_STREAMS', '1') != '0'
         self.use_streams = bool(streams) and torch.cuda.is_available() and torch.device(device).type == 'cuda'
         self._streams = None
+        self._mark_want = self._mark_ev = None
 
-    def _side_streams(self, n):
+    def _side_streams(self, n, fork=True):
         if not self.use_streams:
             return [None] * n
         if self._streams is None or len(self._streams) < n:
@@ -89,9 +101,10 @@ class Trainer(object):
             self._streams = [new_stream(self.device, 1 if i == hi else lo) for i in range(n)]
             for i, st in enumerate(self._streams):
                 D.bind_stream(st, i)   # one RCCL communicator per stream lane
-        main = torch.cuda.current_stream()
-        for s in self._streams[:n]:
-            s.wait_stream(main)
+        if fork:
+            main = torch.cuda.current_stream()
+            for s in self._streams[:n]:
+                s.wait_stream(main)
         return self._streams[:n]
 
     @staticmethod
@@ -104,6 +117,9 @@ class Trainer(object):
         for s in streams:
             if s is not None:
                 main.wait_stream(s)
+
+    def _late_join(self, terms):
+        return LATE_JOIN and self.use_streams and terms is not None
 
     @staticmethod
     def load_optimizers(netG, netDs, attr_enhance):
@@ -225,11 +241,18 @@ class Trainer(object):
         on its own stream).  `g_early` (a list): also run g_update's generator
         loss term through each D right after that D's update, into the list."""
         streams = self._side_streams(len(self.netsD))
-        g_terms = [None] * len(self.netsD)
-        order = range(len(self.netsD))
+        nD = len(self.netsD)
+        g_terms = [None] * nD
+        order = range(nD)
         if LANE_ORDER == 'rev':
             order = reversed(order)
+        late = self._late_join(g_early)
+        defer = late and DEFER_D and LANE_ORDER == 'rev' and streams[0] is not None
+        self._mark_want = 'D%d %s' % (nD - 1, DEFER_D) if defer else None
+        self._mark_ev = None
         for i in order:
+            if defer and i < nD - 1 and self._mark_ev is not None:
+                streams[i].wait_event(self._mark_ev)
             with self._on(streams[i]):
                 Fn.stamp('D%d start' % i)
                 self._d_update_one(i, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec)
@@ -238,12 +261,23 @@ class Trainer(object):
                     # final parameters and the fake images: it runs on the lane as soon as
                     # the update is done, while the larger D's update still runs
                     g_terms[i] = self._g_term(i, fake_imgs, sent_emb, class_labels, iter_rec)
+        self._mark_want = None
         if before_join is not None:
             before_join()
-        self._join(streams)
-        Fn.stamp('d_update joined')
+        if not late:
+            self._join(streams)
+            Fn.stamp('d_update joined')
         if g_early is not None:
             g_early[:] = g_terms
+
+    def _phase(self, name):
+        """Phase boundary of the current lane: a diagnostics stamp, and the
+        event the deferred lanes wait on (EEGAN_DEFER_D)."""
+        Fn.stamp(name)
+        if self._mark_want is not None and name == self._mark_want:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._mark_ev = ev
 
     def _d_update_one(self, i, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec):
         """One D of d_update (train.py:439-466)."""
@@ -256,19 +290,19 @@ class Trainer(object):
         else:
             e_real, e_fake, e_unpair = self.d_loss(real_img, fake_img, sent_emb, unpair_sent_emb, netD)
             d_loss = e_real + (e_fake + e_unpair) / 2.0
-        Fn.stamp('D%d loss forward' % i)
+        self._phase('D%d loss forward' % i)
         optD.zero_grad()
         d_loss.backward(inputs=optD.params)
-        Fn.stamp('D%d loss backward' % i)
+        self._phase('D%d loss backward' % i)
         optD.step()
-        Fn.stamp('D%d adam' % i)
+        self._phase('D%d adam' % i)
         d_loss_gp = self.MA_gradient_penalty(real_img, sent_emb, netD, disc_class)
-        Fn.stamp('D%d gp forward + grad' % i)
+        self._phase('D%d gp forward + grad' % i)
         optD.zero_grad()
         d_loss_gp.backward(inputs=optD.params)
-        Fn.stamp('D%d gp backward' % i)
+        self._phase('D%d gp backward' % i)
         optD.step()
-        Fn.stamp('D%d gp adam' % i)
+        self._phase('D%d gp adam' % i)
         if iter_rec:
             self.records['errD_%d/real_sent' % i] = e_real.detach()
             self.records['errD_%d/fake_sent' % i] = e_fake.detach()
@@ -340,6 +374,10 @@ class Trainer(object):
         """train.py:471-502 (`damsm`: the losses from damsm_early, `terms`: the
         per-D terms from d_update(g_early=...); else computed here)."""
         nD = len(self.netsD)
+        late = self._late_join(terms) and bool(terms) and damsm is not None and len(damsm) > 3 and \
+            damsm[3] is not None
+        if late:
+            return self._g_update_late(fake_imgs, damsm, terms, iter_rec)
         streams = self._side_streams(nD + 1)
         if not terms:
             terms = []
@@ -383,6 +421,38 @@ class Trainer(object):
         self.optimizerG.step()
         Fn.stamp('G adam')
         return g_loss.detach()
+
+    def _g_update_late(self, fake_imgs, damsm, terms, iter_rec):
+        """g_update's backward with the discriminator lanes still unjoined
+        (EEGAN_LATE_JOIN): roots = the per-D terms (on their lanes) and the
+        DAMSM image gradient (its lane is joined first: the seed must be ready
+        on this stream); each lane is joined after the backward.  The same
+        gradients as g_loss.backward() of train.py:493-497, summed at the
+        fake images in another order."""
+        nD = len(self.netsD)
+        streams = self._side_streams(nD + 1, fork=False)
+        w_loss, s_loss, a_loss, (alias, dfake) = damsm
+        main = torch.cuda.current_stream()
+        main.wait_stream(streams[nD])
+        Fn.stamp('g_update DAMSM joined')
+        if iter_rec:
+            self.records['errG/s_loss'] = s_loss.detach()
+            self.records['errG/w_loss'] = w_loss.detach()
+            self.records['errG/a_loss'] = a_loss.detach()
+        if Fn.STAMPS is not None:
+            for i, f in enumerate(fake_imgs):
+                f.register_hook(lambda g, i=i: (Fn.stamp('dfake%d ready' % i), g)[1])
+        self.optimizerG.zero_grad()
+        torch.autograd.backward(list(terms) + [alias], [None] * nD + [dfake], inputs=self.optimizerG.params)
+        Fn.stamp('G backward (D, DAMSM, G)')
+        self._join(streams)
+        g_loss = terms[0].detach()
+        for t in terms[1:]:
+            g_loss = g_loss + t.detach()
+        g_loss = g_loss + self.DAMSM_coe * (s_loss + w_loss + a_loss)
+        self.optimizerG.step()
+        Fn.stamp('G adam')
+        return g_loss
 
     # -------------------------------------------------------- inner step --
     def encode_text(self, batch):
