@@ -1,0 +1,192 @@
+// One-shot peer-write all-reduce for the SyncBN statistics messages
+// (reference: sync_batchnorm/batchnorm.py:90-111 -- the master gathers every
+// device's (sum, ssum) pair, reduces and broadcasts the mean / inv-std back;
+// here every rank reduces locally instead, so there is no master and no second
+// hop).
+//
+// Each rank owns one small uncached "region" per stream lane, mapped into every
+// peer's address space over IPC (xGMI on a multi-GPU node):
+//
+//   [0, 256)     flags[2][16] uint64   flags[parity][src] = epoch of src's slice
+//   [256, 264)   counter uint64        epoch of the last completed call (local)
+//   [264, 268)   error   uint32        set when a wait timed out (local)
+//   [512, ...)   data[2][16][cap] fp64 data[parity][src][i]
+//
+// A call (one 256-thread block): read epoch e = counter + 1, write this rank's
+// message into slot [e & 1][rank] of EVERY rank's region (vector stores into
+// peer memory), release-store flag[e & 1][rank] = e there, wait until all
+// `world` flags of parity e & 1 in the OWN region equal e, then sum the slots
+// in rank order 0..world-1 (identical bits on every rank), store counter = e.
+// Double buffering by parity is safe: a rank reaches epoch e + 2 only after
+// every peer finished epoch e + 1, i.e. after every peer finished reading the
+// parity of epoch e.  The epoch lives on the device, so a captured call keeps
+// counting when the step graph is replayed.
+//
+// Every wait is bounded (~2 s of the 100 MHz wall clock): a rank whose peer
+// never arrives records an error and exits, so the grid always drains;
+// eegan_peer_status reports it.
+#include <string.h>
+
+#include "common.h"
+#include "../../include/eegan_hip.h"
+
+namespace {
+
+constexpr int PEER_MAXW = 16;
+constexpr long OFF_CTR = 256, OFF_ERR = 264, OFF_DATA = 512;
+constexpr unsigned long long WAIT_TICKS = 200000000ull;  // 2 s at 100 MHz
+
+struct PeerSet {
+  char* base[PEER_MAXW];
+};
+
+EE_DEV unsigned long long* flag_at(char* base, int par, int src) {
+  return reinterpret_cast<unsigned long long*>(base) + par * PEER_MAXW + src;
+}
+EE_DEV double* slot_at(char* base, int par, int src, int cap) {
+  return reinterpret_cast<double*>(base + OFF_DATA) + ((long)par * PEER_MAXW + src) * cap;
+}
+
+__global__ __launch_bounds__(256) void peer_allreduce_kernel(double* t, int n, int cap, int rank, int world,
+                                                             PeerSet ps) {
+  const int tid = threadIdx.x;
+  char* own = ps.base[rank];
+  unsigned long long* ctr = reinterpret_cast<unsigned long long*>(own + OFF_CTR);
+  __shared__ unsigned long long s_ep;
+  if (tid == 0) s_ep = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1ull;
+  __syncthreads();
+  const unsigned long long ep = s_ep;
+  const int par = (int)(ep & 1ull);
+
+  // push this rank's message into every rank's slot [par][rank]
+  for (int p = 0; p < world; ++p) {
+    double* dst = slot_at(ps.base[p], par, rank, cap);
+    for (int i = tid; i < n; i += 256) dst[i] = t[i];
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (tid < world)
+    __hip_atomic_store(flag_at(ps.base[tid], par, rank), ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+
+  // wait for every rank's slice in the own region (bounded)
+  if (tid < world) {
+    const unsigned long long t0 = wall_clock64();
+    unsigned long long* f = flag_at(own, par, tid);
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != ep) {
+      if (wall_clock64() - t0 > WAIT_TICKS) {
+        __hip_atomic_store(reinterpret_cast<unsigned*>(own + OFF_ERR), 1u + (unsigned)tid, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+
+  // fixed-order combine: 0 + m_0 + m_1 + ... + m_{world-1}
+  for (int i = tid; i < n; i += 256) {
+    double acc = 0.0;
+    for (int q = 0; q < world; ++q) {
+      const unsigned long long* src = reinterpret_cast<const unsigned long long*>(slot_at(own, par, q, cap)) + i;
+      acc += __longlong_as_double((long long)__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    }
+    t[i] = acc;
+  }
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(ctr, ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+}  // namespace
+
+extern "C" {
+
+long eegan_peer_region_bytes(int cap) {
+  if (cap < 1) return -1;
+  return OFF_DATA + 2L * PEER_MAXW * cap * (long)sizeof(double);
+}
+
+int eegan_peer_alloc(long bytes, void** base, void* handle) {
+  if (bytes < OFF_DATA || !base || !handle) {
+    ee_set_error("peer_alloc: bad arguments (bytes=%ld)", bytes);
+    return -1;
+  }
+  void* p = nullptr;
+  hipError_t e = hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) {
+    ee_set_error("peer_alloc: hipExtMallocWithFlags(uncached, %ld): %s", bytes, hipGetErrorString(e));
+    return -1;
+  }
+  e = hipMemset(p, 0, (size_t)bytes);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  hipIpcMemHandle_t h;
+  if (e == hipSuccess) e = hipIpcGetMemHandle(&h, p);
+  if (e != hipSuccess) {
+    (void)hipFree(p);
+    ee_set_error("peer_alloc: %s", hipGetErrorString(e));
+    return -1;
+  }
+  memcpy(handle, &h, sizeof(h));
+  *base = p;
+  return 0;
+}
+
+int eegan_peer_open(const void* handle, void** base) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  hipError_t e = hipIpcOpenMemHandle(base, h, hipIpcMemLazyEnablePeerAccess);
+  if (e != hipSuccess) {
+    ee_set_error("peer_open: hipIpcOpenMemHandle: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+int eegan_peer_close(void* base) {
+  hipError_t e = hipIpcCloseMemHandle(base);
+  if (e != hipSuccess) {
+    ee_set_error("peer_close: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+int eegan_peer_free(void* base) {
+  hipError_t e = hipFree(base);
+  if (e != hipSuccess) {
+    ee_set_error("peer_free: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+int eegan_peer_allreduce_f64(double* t, int n, int cap, int rank, int world, void* const* bases, hipStream_t s) {
+  if (world < 1 || world > PEER_MAXW || rank < 0 || rank >= world || n < 0 || n > cap || !bases) {
+    ee_set_error("peer_allreduce: bad arguments (n=%d cap=%d rank=%d world=%d, at most %d ranks)", n, cap, rank,
+                 world, PEER_MAXW);
+    return -1;
+  }
+  PeerSet ps = {};
+  for (int p = 0; p < world; ++p) {
+    if (!bases[p]) {
+      ee_set_error("peer_allreduce: region of rank %d not mapped", p);
+      return -1;
+    }
+    ps.base[p] = static_cast<char*>(bases[p]);
+  }
+  ee_launch(peer_allreduce_kernel, dim3(1), dim3(256), 0, s, t, n, cap, rank, world, ps);
+  EE_LAUNCH_CHECK("peer_allreduce_kernel");
+}
+
+int eegan_peer_status(void* own, int reset, int* timed_out) {
+  unsigned err = 0;
+  hipError_t e = hipMemcpy(&err, static_cast<char*>(own) + OFF_ERR, sizeof(err), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && reset && err) e = hipMemset(static_cast<char*>(own) + OFF_ERR, 0, sizeof(err));
+  if (e != hipSuccess) {
+    ee_set_error("peer_status: %s", hipGetErrorString(e));
+    return -1;
+  }
+  *timed_out = (int)err;
+  return 0;
+}
+
+}  // extern "C"

@@ -135,6 +135,13 @@ _SIGS = {
     'eegan_fid_preprocess': ([P, I, I, I, I, I, P, P, P, I, P], I),
     'eegan_fid_stats_workspace': ([I], L),
     'eegan_fid_stats': ([P, I, I, P, P, P, P], I),
+    'eegan_peer_region_bytes': ([I], L),
+    'eegan_peer_alloc': ([L, P, P], I),
+    'eegan_peer_open': ([P, P], I),
+    'eegan_peer_close': ([P], I),
+    'eegan_peer_free': ([P], I),
+    'eegan_peer_allreduce_f64': ([P, I, I, I, I, P, P], I),
+    'eegan_peer_status': ([P, I, P], I),
     'eegan_pipe_workspace': ([I, I, I, I, P], L),
     'eegan_pipe_transform': ([P, P, I, I, I, P, P, I, P, P, P, I, P, P, P], I),
 }
@@ -154,7 +161,7 @@ def _load():
 
 LIB = _load()
 ABI_VERSION = LIB.eegan_abi_version()
-EXPECTED_ABI = 8
+EXPECTED_ABI = 9
 if ABI_VERSION != EXPECTED_ABI:
     raise ImportError('%s has ABI %d, these bindings need %d: rebuild (make -C ee-gan_amd/csrc)'
                       % (LIB_PATH, ABI_VERSION, EXPECTED_ABI))

@@ -25,6 +25,9 @@ from . import functional as Fn
 # path (incl. its capture into the step's HIP graph) runs on a one-GPU box.
 FORCE = os.environ.get('EEGAN_FORCE_DIST') == '1'
 COMMS = []    # eegan_hip.rccl.Communicator per stream lane when the ranks own GPUs (graph-capturable)
+# SyncBN statistics by the one-shot peer-write kernel (eegan_hip.peer) instead
+# of RCCL (EEGAN_SYNCBN_PEER=1; off by default -- unmeasured at N > 1)
+PEER = os.environ.get('EEGAN_SYNCBN_PEER', '0') == '1'
 N_LANES = 6   # lane 0: the caller's (main) stream; 1..: streams bound with bind_stream
 _LANE_OF = {}
 
@@ -82,7 +85,10 @@ def init_from_env(backend=None):
 
 def install_syncbn_hook(group=None):
     if is_on() and (dist.get_world_size(group) > 1 or FORCE):
-        if COMMS and group is None:
+        if PEER:
+            from .peer import PeerAllReduce
+            Fn.SYNC_BN_ALLREDUCE = PeerAllReduce(group)
+        elif COMMS and group is None:
             Fn.SYNC_BN_ALLREDUCE = all_reduce
         else:
             Fn.SYNC_BN_ALLREDUCE = lambda t: dist.all_reduce(t, group=group)

@@ -1,0 +1,134 @@
+"""One-shot peer-write all-reduce for the SyncBN statistics (EEGAN_SYNCBN_PEER=1).
+
+The reference exchanges every BN layer's (sum, ssum) message through a master
+replica (sync_batchnorm/batchnorm.py:90-111 over SyncMaster / SlavePipe,
+sync_batchnorm/comm.py:18-137): gather to GPU0, reduce, broadcast back.  With
+one process per GPU these messages (2C fp64 values, at most a few KB) are
+latency-bound; a ring all-reduce spends most of its time in protocol steps.
+Here each rank owns a small uncached device region per stream lane, mapped by
+every peer over IPC (xGMI between MI355X GPUs), and one kernel per call
+(csrc/peer.hip) stores the rank's message into every rank's region, raises a
+flag there, waits for all flags in its own region, and sums the slots in rank
+order -- every rank gets identical bits, with no second hop.  The epoch
+counter lives on the device, so the calls are graph-capturable and replay
+correctly.
+
+Regions are created collectively (the 64-byte IPC handles are exchanged with
+all_gather_object over the process group) the first time a stream issues a
+reduction, which must happen outside graph capture -- the trainer's eager
+warm-up steps do it.  Messages longer than the region capacity go to the
+group's regular all-reduce; host tensors (CPU process groups) take
+`fixed_order_sum`.
+
+`fixed_order_sum` is the combine's host restatement for CPU process groups
+(the gloo tests): all-gather, then 0 + m_0 + ... + m_{W-1} in fp64.
+"""
+import ctypes as C
+
+import torch
+import torch.distributed as dist
+
+from ._lib import LIB, ops
+
+MAX_RANKS = 16
+CAP = 4096   # doubles per message: SyncBN sends 2C values, C <= 2048
+
+
+class PeerRegion(object):
+    """This rank's region for one stream lane plus the mapped regions of its peers."""
+
+    def __init__(self, group=None, cap=CAP, device=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if self.world > MAX_RANKS:
+            raise ValueError('eegan_hip.peer: at most %d ranks (got %d)' % (MAX_RANKS, self.world))
+        self.cap = cap
+        nbytes = LIB.eegan_peer_region_bytes(cap)
+        own = C.c_void_p()
+        handle = (C.c_ubyte * 64)()
+        with torch.cuda.device(device if device is not None else torch.cuda.current_device()):
+            ops.peer_alloc(nbytes, C.byref(own), handle)
+        self.own = own.value
+        handles = [None] * self.world
+        dist.all_gather_object(handles, bytes(handle), group=self.group)
+        bases = []
+        self._opened = []
+        for r, h in enumerate(handles):
+            if r == self.rank:
+                bases.append(self.own)
+                continue
+            hb = (C.c_ubyte * 64).from_buffer_copy(h)
+            p = C.c_void_p()
+            ops.peer_open(hb, C.byref(p))
+            bases.append(p.value)
+            self._opened.append(p.value)
+        self._bases = (C.c_void_p * self.world)(*bases)
+
+    def all_reduce(self, t):
+        """In-place sum over the ranks of a contiguous fp64 device tensor (n <= cap)."""
+        assert t.is_cuda and t.dtype == torch.float64 and t.is_contiguous() and t.numel() <= self.cap
+        ops.peer_allreduce_f64(t.data_ptr(), t.numel(), self.cap, self.rank, self.world, self._bases,
+                               torch.cuda.current_stream().cuda_stream)
+
+    def timed_out(self, reset=True):
+        """0, or 1 + the rank whose slice a wait gave up on (synchronises)."""
+        v = C.c_int()
+        ops.peer_status(self.own, int(reset), C.byref(v))
+        return v.value
+
+    def close(self):
+        """Unmap and free (after a barrier: no peer may still write into the own region)."""
+        for p in self._opened:
+            ops.peer_close(p)
+        self._opened = []
+        if self.own:
+            ops.peer_free(self.own)
+            self.own = None
+
+
+class PeerAllReduce(object):
+    """callable(t) -> in-place sum over the ranks; one region per issuing stream."""
+
+    def __init__(self, group=None, cap=CAP):
+        self.group = group
+        self.cap = cap
+        self.regions = {}
+
+    def region(self):
+        s = torch.cuda.current_stream()
+        r = self.regions.get(s.cuda_stream)
+        if r is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError('eegan_hip.peer: first SyncBN reduction of a stream inside graph capture; run '
+                                   'one eager step first (regions are created collectively, outside capture)')
+            r = self.regions[s.cuda_stream] = PeerRegion(self.group, self.cap)
+        return r
+
+    def __call__(self, t):
+        if not t.is_cuda:
+            fixed_order_sum(t, self.group)   # CPU process groups (gloo tests): the same combine
+        elif t.dtype != torch.float64 or not t.is_contiguous() or t.numel() > self.cap:
+            dist.all_reduce(t, group=self.group)
+        else:
+            self.region().all_reduce(t)
+
+    def timed_out(self):
+        return max([r.timed_out() for r in self.regions.values()] or [0])
+
+    def close(self):
+        for r in self.regions.values():
+            r.close()
+        self.regions = {}
+
+
+def fixed_order_sum(t, group=None):
+    """The peer kernel's combine on a CPU process group: every rank ends with
+    0 + m_0 + m_1 + ... + m_{W-1} (fp64, rank order) -- identical bits on all
+    ranks, whatever the group's own all-reduce order would be."""
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, t.contiguous(), group=group)
+    acc = torch.zeros_like(t)
+    for p in parts:
+        acc += p
+    t.copy_(acc)

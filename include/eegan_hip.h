@@ -8,7 +8,8 @@
  *  - Parameters / statistics / losses: fp32.
  *  - Every entry point is asynchronous on the `hipStream_t` it is given,
  *    never allocates or frees (the caller owns all memory, including
- *    workspaces sized by the *_workspace queries), keeps no global mutable
+ *    workspaces sized by the *_workspace queries; the eegan_peer_* region
+ *    calls are the one exception, since IPC needs a whole allocation), keeps no global mutable
  *    state (safe to call concurrently from several threads/devices) and
  *    returns 0 or a negative error code; eegan_last_error() then returns a
  *    thread-local description.
@@ -26,12 +27,13 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 8  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
+#define EEGAN_ABI_VERSION 9  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
                                 4: rectangular (local x global) DAMSM words / sentence blocks on MFMA;
                                 5: GlobalAttentionGeneral (eegan_gag_*), words backward reuses the forward's prep;
                                 6: device input pipeline (eegan_pipe_*);
                                 7: GlobalAttentionGeneral for any source length (eegan_gag_fwd workspace);
-                                8: FID leg (eegan_fid_*) */
+                                8: FID leg (eegan_fid_*);
+                                9: SyncBN peer-write all-reduce (eegan_peer_*) */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
@@ -344,6 +346,25 @@ int eegan_fid_preprocess(const float* x, int N, int H, int W, int Ho, int Wo, co
                          const float* shift3, uint16_t* y, int ldy, hipStream_t s);
 long eegan_fid_stats_workspace(int D);
 int eegan_fid_stats(const float* act, int N, int D, double* mu, double* sigma, void* ws, hipStream_t s);
+
+/* ------------------------------------------------ SyncBN peer-write reduce --
+ * replaces: the statistics exchange of _SynchronizedBatchNorm (sync_batchnorm/batchnorm.py:90-111, through
+ * SyncMaster / SlavePipe of sync_batchnorm/comm.py:18-137) for ranks in separate processes: a one-shot
+ * all-reduce of a small fp64 message by vector stores into every rank's IPC-mapped region, then a local
+ * fixed-order sum (identical bits on every rank).  One region per rank and stream lane:
+ *   region_bytes(cap)        bytes of a region holding messages of up to `cap` doubles (ranks <= 16);
+ *   alloc(bytes, &base, h)   uncached device allocation, zeroed; h receives its 64-byte IPC handle;
+ *   open(h, &base) / close   map / unmap a peer's region; free releases an own region;
+ *   allreduce_f64(t, n, cap, rank, world, bases, s)  in-place sum of t[0..n) over the ranks; bases = host
+ *                            array of `world` region pointers (own at [rank]); every wait is bounded;
+ *   status(own, reset, &timed_out)  nonzero timed_out: a wait gave up (1 + the missing rank). */
+long eegan_peer_region_bytes(int cap);
+int eegan_peer_alloc(long bytes, void** base, void* handle);
+int eegan_peer_open(const void* handle, void** base);
+int eegan_peer_close(void* base);
+int eegan_peer_free(void* base);
+int eegan_peer_allreduce_f64(double* t, int n, int cap, int rank, int world, void* const* bases, hipStream_t s);
+int eegan_peer_status(void* own, int reset, int* timed_out);
 
 /* -------------------------------------------------------------------- adam --
  * replaces: torch.optim.Adam(betas=(0.0, 0.9)) of train.py:252-263 on one flat buffer.

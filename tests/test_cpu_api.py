@@ -20,7 +20,7 @@ def test_library_exports_header_symbols():
         assert hasattr(_lib.LIB, name), name          # exported by libeegan_hip.so
         assert name in _lib._SIGS, name               # bound with a ctypes signature
     assert set(_lib._SIGS) == set(declared)
-    assert eegan_hip.ABI_VERSION == 8
+    assert eegan_hip.ABI_VERSION == 9
     # rows padded to 128; every tap's channel run padded to 32 (to 8 for <= 8
     # channels: 4 taps per K step), rows padded to whole 32-deep steps
     assert _lib.ops.conv_packed_elems(100, 3, 3, 3, 0) == 128 * 96
@@ -103,3 +103,33 @@ def test_att_maps_lazy_list():
     att = torch.arange(2 * 3 * 289, dtype=torch.float32).reshape(2, 3, 289)
     m = _AttMaps(att, torch.tensor([3, 1]))
     assert len(m) == 2 and m[1].shape == (1, 1, 17, 17) and m[0].shape == (1, 3, 17, 17)
+
+
+def test_sync_master_rendezvous():
+    """sync_batchnorm.comm keeps the reference's in-process rendezvous
+    (sync_batchnorm/comm.py:18-137): slaves' messages reach the master's
+    callback after the master's own, each slave gets its own reply, over
+    several rounds."""
+    import threading
+    from sync_batchnorm.comm import SyncMaster
+
+    def callback(msgs):
+        total = sum(m for _, m in msgs)
+        return [(i, (total, m)) for i, m in msgs]
+    master = SyncMaster(callback)
+    pipes = [master.register_slave(i) for i in (1, 2, 3)]
+    for rnd in range(3):
+        got = {}
+
+        def slave(p):
+            got[p.identifier] = p.run_slave(10 * p.identifier + rnd)
+        ts = [threading.Thread(target=slave, args=(p,)) for p in pipes]
+        for t in ts:
+            t.start()
+        mine = master.run_master(rnd)
+        for t in ts:
+            t.join(10)
+        total = rnd + sum(10 * i + rnd for i in (1, 2, 3))
+        assert mine == (total, rnd)
+        assert got == {i: (total, 10 * i + rnd) for i in (1, 2, 3)}
+    assert master.nr_slaves == 3

@@ -25,17 +25,17 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(fn, *args):
+def _run(fn, *args, world=WORLD):
     port = _free_port()
-    mp.spawn(_entry, args=(fn, port, args), nprocs=WORLD, join=True)
+    mp.spawn(_entry, args=(fn, port, args, world), nprocs=world, join=True)
 
 
-def _entry(rank, fn, port, args):
+def _entry(rank, fn, port, args, world):
     sys.path.insert(0, os.path.join(REPO, 'ee-gan_amd'))
     sys.path.insert(0, REPO)
-    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     torch.set_num_threads(1)
-    dist.init_process_group('gloo', rank=rank, world_size=WORLD)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
         fn(rank, *args)
     finally:
@@ -237,6 +237,43 @@ def _case_syncbn_stats(rank):
     assert torch.allclose(rv.float(), sd['bn.running_var'], atol=1e-5)
 
 
-@pytest.mark.parametrize('case', ['all_gather', 'flat_adam_allreduce', 'flat_adam_overlap_plans', 'grad_reducer', 'grad_hooks_adam', 'syncbn_stats'])
+def _case_syncbn_peer_combine(rank):
+    """EEGAN_SYNCBN_PEER's combine (eegan_hip.peer): every rank ends with the
+    same bits, 0 + m_0 + ... + m_{W-1} in rank order (the peer kernel's sum),
+    within fp64 rounding of the group's own all-reduce; the SyncBN hook routes
+    through it when the switch is on."""
+    from eegan_hip import dist as D
+    from eegan_hip import functional as Fn
+    from eegan_hip.peer import PeerAllReduce
+    W = dist.get_world_size()
+    D.PEER = True
+    try:
+        D.install_syncbn_hook()
+        assert isinstance(Fn.SYNC_BN_ALLREDUCE, PeerAllReduce) and Fn.SYNC_BN_WORLD == W
+        for n in (1, 7, 2 * 512):
+            msgs = [torch.randn(n, dtype=torch.float64, generator=torch.Generator().manual_seed(1000 * r + n)) *
+                    10.0 ** (r - 1) for r in range(W)]   # magnitudes differ: the order shows in the bits
+            t = msgs[rank].clone()
+            Fn.SYNC_BN_ALLREDUCE(t)
+            want = torch.zeros(n, dtype=torch.float64)
+            for m in msgs:
+                want += m
+            assert torch.equal(t, want)
+            everyone = [torch.empty_like(t) for _ in range(W)]
+            dist.all_gather(everyone, t)
+            assert all(torch.equal(e, t) for e in everyone)
+            ref = msgs[rank].clone()
+            dist.all_reduce(ref)
+            assert torch.allclose(t, ref, rtol=1e-14, atol=0)
+    finally:
+        D.PEER = False
+        D.install_syncbn_hook()
+
+
+def test_gloo_world3_syncbn_peer_combine():
+    _run(_case_syncbn_peer_combine, world=3)
+
+
+@pytest.mark.parametrize('case', ['syncbn_peer_combine', 'all_gather', 'flat_adam_allreduce', 'flat_adam_overlap_plans', 'grad_reducer', 'grad_hooks_adam', 'syncbn_stats'])
 def test_gloo_world2(case):
     _run(globals()['_case_' + case])
