@@ -47,7 +47,7 @@ DAMSM_EARLY = os.environ.get('EEGAN_DAMSM_EARLY', '1') != '0'
 DAMSM_GRAD_EARLY = os.environ.get('EEGAN_DAMSM_GRAD_EARLY', '1') != '0'
 # the discriminator lanes are issued largest (critical) first and the DAMSM lane after them: the
 # first packets of the critical lane then do not queue behind the others' (C2: 678 vs 656 img/s,
-# tools/gpu_lane_ab.sh); EEGAN_LANE_ORDER=fwd: D64, D128, D256 after the DAMSM lane
+# tools/gpu_env_ab.sh); EEGAN_LANE_ORDER=fwd: D64, D128, D256 after the DAMSM lane
 LANE_ORDER = os.environ.get('EEGAN_LANE_ORDER', 'rev')
 # EEGAN_LATE_JOIN=1: the discriminator lanes are joined into the main stream only
 # after g_update's backward: the backward starts from the per-D terms as roots
