@@ -87,6 +87,7 @@ struct ConvArgs {
   int res_vec;  // res rows 8-byte aligned (ldres % 4 == 0, aligned base): vector residual loads
   int wide;     // conv_fast_kernel pairs: one 64-channel stage of whole 128-B lines per K-step pair
   int stage_epi;  // conv_fast_kernel: LDS-staged epilogue (unsplit bf16 output, 16-B aligned rows; host-checked)
+  unsigned* tickets;  // conv_fast_kernel split-K: per-tile counters, last workgroup reduces (ee_tickets) or null
 };
 
 // K step kt, 8-channel chunk kc -> kernel tap and channel.  Normal mode: the
@@ -287,6 +288,133 @@ EE_DEV void staged_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], flo
     *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + p * a.ldo + co) =
         make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
   }
+}
+
+// split-K reduction + epilogue: out[p][co] = res + gamma*act(sum_z part[z][p][co] + bias).
+// The per-item bodies are shared by the reduce kernel and the last-workgroup
+// finish of conv_fast_kernel (same arithmetic, same z order: bit-identical).
+//
+// 4 consecutive channels of one pixel: 16-byte slab loads (4 splits in
+// flight), 8-byte residual / gate loads and stores; 32-bit index math (the
+// host enables this path only for P * Mrows < 2^31)
+EE_DEV void splitk_item4(const ConvArgs& a, unsigned p, unsigned co, float gam) {
+  const unsigned total4 = (unsigned)(((long)a.P * a.Mrows) >> 2);
+  const unsigned i = (p * (unsigned)a.Mrows + co) >> 2;
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  const f32x4_t* src = reinterpret_cast<const f32x4_t*>(a.part) + i;
+  int z = 0;
+  for (; z + 4 <= a.nsplit; z += 4) {
+    const f32x4_t v0 = src[(long)z * total4], v1 = src[(long)(z + 1) * total4];
+    const f32x4_t v2 = src[(long)(z + 2) * total4], v3 = src[(long)(z + 3) * total4];
+    acc += v0;  // same order as the scalar path: bit-identical sums
+    acc += v1;
+    acc += v2;
+    acc += v3;
+  }
+  for (; z < a.nsplit; ++z) acc += src[(long)z * total4];
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = act_fwd(acc[r] + (a.bias ? a.bias[co + r] : 0.f), a.act, a.slope);
+  if (a.gate) {
+    const uint2 gv = *reinterpret_cast<const uint2*>(a.gate + (long)p * a.ldgate + co);
+    const float gg[4] = {lo_f(gv.x), hi_f(gv.x), lo_f(gv.y), hi_f(gv.y)};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] *= act_dgrad_from_y(gg[r], a.gate_act, a.gate_slope);
+  }
+  if (a.res) {
+    long rpix = p;
+    if (a.res_up2) {
+      const unsigned hw = (unsigned)a.OH * (unsigned)a.OW;
+      const unsigned n = p / hw, rem = p - n * hw;
+      const unsigned y = rem / (unsigned)a.OW, x = rem - y * (unsigned)a.OW;
+      rpix = ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
+    }
+    const uint2 rv = *reinterpret_cast<const uint2*>(a.res + rpix * a.ldres + co);
+    const float rr[4] = {lo_f(rv.x), hi_f(rv.x), lo_f(rv.y), hi_f(rv.y)};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = res_combine(a.res_scale, rr[r], gam, v[r]);
+  }
+  if (a.out_f32) {
+    *reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(a.out) + (long)p * a.ldo + co) = {v[0], v[1], v[2], v[3]};
+  } else {
+    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(a.out) + (long)p * a.ldo + co) =
+        make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+  }
+}
+
+EE_DEV void splitk_item1(const ConvArgs& a, long p, int co, float gam) {
+  const long total = (long)a.P * a.Mrows, e = p * a.Mrows + co;
+  float v = 0.f;
+  for (int z = 0; z < a.nsplit; ++z) v += a.part[(long)z * total + e];
+  v = act_fwd(v + (a.bias ? a.bias[co] : 0.f), a.act, a.slope);
+  if (a.gate) v *= act_dgrad_from_y(bf2f(a.gate[p * a.ldgate + co]), a.gate_act, a.gate_slope);
+  if (a.res) {
+    long rpix = p;
+    if (a.res_up2) {
+      const unsigned hw = (unsigned)a.OH * (unsigned)a.OW;
+      const unsigned n = (unsigned)p / hw, rem = (unsigned)p - n * hw;
+      const unsigned y = rem / (unsigned)a.OW, x = rem - y * (unsigned)a.OW;
+      rpix = ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
+    }
+    v = res_combine(a.res_scale, bf2f(a.res[rpix * a.ldres + co]), gam, v);
+  }
+  if (a.out_f32) reinterpret_cast<float*>(a.out)[p * a.ldo + co] = v;
+  else reinterpret_cast<bf16_t*>(a.out)[p * a.ldo + co] = f2bf(v);
+}
+
+template <int MODE>  // MODE only tags the kernel name (profiles tell fwd / bwd-data apart)
+__global__ void conv_splitk_reduce_kernel(ConvArgs a) {
+  const long total = (long)a.P * a.Mrows;
+  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
+  if (a.red_vec4) {
+    const unsigned total4 = (unsigned)(total >> 2), M = (unsigned)a.Mrows;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
+      const unsigned e = i * 4, p = e / M, co = e - p * M;
+      splitk_item4(a, p, co, gam);
+    }
+    return;
+  }
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long p = e / a.Mrows;
+    splitk_item1(a, p, (int)(e - p * a.Mrows), gam);
+  }
+}
+
+// Last-workgroup finish of a split-K tile (a.tickets set): every split writes
+// its fp32 partial tile, publishes it (device-scope fence) and takes a ticket
+// on the tile's counter; the workgroup drawing the last ticket sums the slabs
+// of the tile in split order and applies the epilogue -- the reduce kernel's
+// items over this tile only, so the result is bit-identical to it -- then
+// resets the counter for the next launch that is handed this run.
+template <int MODE, int TCO, int TPIX>
+EE_DEV void splitk_finish_tile(const ConvArgs& a, int tid, int pix0, int co0, int Pc, int CH, int CW, int qy, int qx,
+                               int stc, int cls) {
+  __shared__ int s_last;
+  __threadfence();
+  __syncthreads();
+  const int tile = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * cls);
+  if (tid == 0) s_last = atomicAdd(a.tickets + tile, 1u) == (unsigned)(a.nsplit - 1);
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
+  const int ncol = min(TCO, a.Mrows - co0);
+  const int per = a.red_vec4 ? 4 : 1, ncv = (ncol + per - 1) / per;
+  for (int item = tid; item < TPIX * ncv; item += 256) {
+    const int pix = item / ncv, c = item - pix * ncv;
+    const int pc = pix0 + pix;
+    if (pc >= Pc) break;   // items are pixel-major: the rest of the tile is past the end too
+    long p = pc;
+    if (MODE == MODE_BWDD && a.ncls > 1) {
+      const int hw = CH * CW;
+      const int n = pc / hw, rem = pc - n * hw;
+      const int yy = rem / CW, xx = rem - yy * CW;
+      p = ((long)n * a.OH + qy + stc * yy) * a.OW + qx + stc * xx;
+    }
+    if (a.red_vec4) splitk_item4(a, (unsigned)p, (unsigned)(co0 + 4 * c), gam);
+    else splitk_item1(a, p, co0 + c, gam);
+  }
+  if (tid == 0) atomicExch(a.tickets + tile, 0u);
 }
 
 // ------------------------------------------------------- FWD / BWDD kernel --
@@ -1004,83 +1132,7 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
     return;
   }
   igemm_epilogue<MODE, FI, FJ, WT_CO, WT_PIX>(a, acc, pix0, co0, wi, wj, lane, split, Pc, CH, CW, qy, qx, stc);
-}
-
-// split-K reduction + epilogue: out[p][co] = res + gamma*act(sum_z part[z][p][co] + bias)
-template <int MODE>  // MODE only tags the kernel name (profiles tell fwd / bwd-data apart)
-__global__ void conv_splitk_reduce_kernel(ConvArgs a) {
-  const long total = (long)a.P * a.Mrows;
-  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
-  if (a.red_vec4) {
-    // 4 consecutive channels of one pixel per thread: 16-byte slab loads (4
-    // splits in flight), 8-byte residual / gate loads and stores; 32-bit
-    // index math (the host enables this path only for total < 2^31)
-    const unsigned total4 = (unsigned)(total >> 2), M = (unsigned)a.Mrows;
-    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
-      const unsigned e = i * 4, p = e / M, co = e - p * M;
-      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-      const f32x4_t* src = reinterpret_cast<const f32x4_t*>(a.part) + i;
-      int z = 0;
-      for (; z + 4 <= a.nsplit; z += 4) {
-        const f32x4_t v0 = src[(long)z * total4], v1 = src[(long)(z + 1) * total4];
-        const f32x4_t v2 = src[(long)(z + 2) * total4], v3 = src[(long)(z + 3) * total4];
-        acc += v0;  // same order as the scalar path: bit-identical sums
-        acc += v1;
-        acc += v2;
-        acc += v3;
-      }
-      for (; z < a.nsplit; ++z) acc += src[(long)z * total4];
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = act_fwd(acc[r] + (a.bias ? a.bias[co + r] : 0.f), a.act, a.slope);
-      if (a.gate) {
-        const uint2 gv = *reinterpret_cast<const uint2*>(a.gate + (long)p * a.ldgate + co);
-        const float gg[4] = {lo_f(gv.x), hi_f(gv.x), lo_f(gv.y), hi_f(gv.y)};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] *= act_dgrad_from_y(gg[r], a.gate_act, a.gate_slope);
-      }
-      if (a.res) {
-        long rpix = p;
-        if (a.res_up2) {
-          const unsigned hw = (unsigned)a.OH * (unsigned)a.OW;
-          const unsigned n = p / hw, rem = p - n * hw;
-          const unsigned y = rem / (unsigned)a.OW, x = rem - y * (unsigned)a.OW;
-          rpix = ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
-        }
-        const uint2 rv = *reinterpret_cast<const uint2*>(a.res + rpix * a.ldres + co);
-        const float rr[4] = {lo_f(rv.x), hi_f(rv.x), lo_f(rv.y), hi_f(rv.y)};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = res_combine(a.res_scale, rr[r], gam, v[r]);
-      }
-      if (a.out_f32) {
-        *reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(a.out) + (long)p * a.ldo + co) = {v[0], v[1], v[2], v[3]};
-      } else {
-        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(a.out) + (long)p * a.ldo + co) =
-            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-      }
-    }
-    return;
-  }
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const long p = e / a.Mrows;
-    const int co = e - p * a.Mrows;
-    float v = 0.f;
-    for (int z = 0; z < a.nsplit; ++z) v += a.part[(long)z * total + e];
-    v = act_fwd(v + (a.bias ? a.bias[co] : 0.f), a.act, a.slope);
-    if (a.gate) v *= act_dgrad_from_y(bf2f(a.gate[p * a.ldgate + co]), a.gate_act, a.gate_slope);
-    if (a.res) {
-      long rpix = p;
-      if (a.res_up2) {
-        const unsigned hw = (unsigned)a.OH * (unsigned)a.OW;
-        const unsigned n = (unsigned)p / hw, rem = (unsigned)p - n * hw;
-        const unsigned y = rem / (unsigned)a.OW, x = rem - y * (unsigned)a.OW;
-        rpix = ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
-      }
-      v = res_combine(a.res_scale, bf2f(a.res[rpix * a.ldres + co]), gam, v);
-    }
-    if (a.out_f32) reinterpret_cast<float*>(a.out)[p * a.ldo + co] = v;
-    else reinterpret_cast<bf16_t*>(a.out)[p * a.ldo + co] = f2bf(v);
-  }
+  if (a.tickets) splitk_finish_tile<MODE, TCO, TPIX>(a, tid, pix0, co0, Pc, CH, CW, qy, qx, stc, cls);
 }
 
 // ---------------------------------------------------------- WGRAD kernel --
@@ -2533,6 +2585,14 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
     return -22;
   }
   dim3 grid(ee_cdiv(Pc_max, p.tpix), ee_cdiv(a.Mrows, p.tco), a.ncls * p.nsplit);
+  const long total = (long)a.P * a.Mrows;
+  if (p.nsplit > 1) {
+    const uintptr_t oal = a.out_f32 ? 15 : 7;
+    // EEGAN_CONV_RED_VEC4=0 forces the scalar reduce (A/B and bit-identity tests)
+    a.red_vec4 = a.Mrows % 4 == 0 && total < 0x7fffffffL && a.ldo % 4 == 0 && ((uintptr_t)a.out & oal) == 0 &&
+                 ((uintptr_t)a.part & 15) == 0 && (!a.gate || a.gate_vec) && (!a.res || a.res_vec) &&
+                 env_int("EEGAN_CONV_RED_VEC4", 1);
+  }
   const long w_bytes = (long)ee_round_up(a.Mrows, 128) * a.Kw * 2;
 #define GL(TC, TP) ee_launch(conv_glds_kernel<MODE, TC, TP>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
 #define FA(TC, TP)                                                                                          \
@@ -2550,6 +2610,12 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   if (MODE == MODE_BWDD && a.st > 1) tr_ = ee_cdiv(a.R, a.st), ts_ = ee_cdiv(a.S, a.st);
   const bool fast = glds && a.Cgp % BK == 0 && !a.up2 && tr_ * ts_ <= 32 && env_int("EEGAN_CONV_FAST", 1);
   if (fast) {
+    // split-K: the last workgroup of each tile reduces it (EEGAN_CONV_SPLITK_FUSED=1).  Off by
+    // default: the device-scope fences around the tickets (an L2 writeback + invalidate per
+    // workgroup on this multi-XCD part) made the 4x4 / 8x8 deep layers 2.8-6.8x slower than
+    // the separate reduce kernel (profiles/r03_splitk_fused.log)
+    if (p.nsplit > 1 && env_int("EEGAN_CONV_SPLITK_FUSED", 0))
+      a.tickets = ee_tickets((long)grid.x * grid.y * a.ncls, s);
     if (p.tco == 128) { if (p.tpix == 128) FA(128, 128); else FA(128, 64); }
     else if (p.tco == 64) { if (p.tpix == 128) FA(64, 128); else FA(64, 64); }
     else if (p.tco == 32) { if (p.tpix == 256) FA(32, 256); else FA(32, 64); }
@@ -2569,13 +2635,7 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
 #undef GL
 #undef FA
   int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd" : "conv_bwd_data");
-  if (rc || a.nsplit == 1) return rc;
-  const long total = (long)a.P * a.Mrows;
-  const uintptr_t oal = a.out_f32 ? 15 : 7;
-  // EEGAN_CONV_RED_VEC4=0 forces the scalar reduce (A/B and bit-identity tests)
-  a.red_vec4 = a.Mrows % 4 == 0 && total < 0x7fffffffL && a.ldo % 4 == 0 && ((uintptr_t)a.out & oal) == 0 &&
-               ((uintptr_t)a.part & 15) == 0 && (!a.gate || a.gate_vec) && (!a.res || a.res_vec) &&
-               env_int("EEGAN_CONV_RED_VEC4", 1);
+  if (rc || a.nsplit == 1 || a.tickets) return rc;
   const long work = a.red_vec4 ? total / 4 : total;
   ee_launch(conv_splitk_reduce_kernel<MODE>, dim3((int)std::min<long>((work + 255) / 256, 4096)), dim3(256), 0, s, a);
   return ee_check_launch("conv_splitk_reduce");

@@ -185,6 +185,49 @@ def test_splitk_reduce_vector_path_bit_identical(gpu, monkeypatch):
             assert torch.equal(a, c)
 
 
+def test_splitk_last_workgroup_finish_bit_identical(gpu, monkeypatch):
+    """Split-K tiles reduced by their last-arriving workgroup (ticket counters,
+    EEGAN_CONV_SPLITK_FUSED=1; off by default, slower) against the separate
+    reduce kernel (=0, default): the same per-item sums in split order, so torch.equal -- vector and
+    scalar items, forward with bias / act / residual + gain and fp32 out,
+    backward-data with gate, the half-resolution residual and stride-2 parity
+    classes.  Each fused call runs three times: the counters reset themselves,
+    so repeated launches on the same ticket runs stay identical."""
+    Fn, T, _ = _mods()
+    monkeypatch.setenv('EEGAN_CONV_TARGET', '4096')
+    monkeypatch.setenv('EEGAN_CONV_MINK', '2')
+    lrelu = Fn.ACT_CODES['lrelu']
+    for N, Cin, H, W, Cout, k, st, pad in [(2, 256, 4, 4, 128, 3, 1, 1), (2, 96, 8, 8, 64, 4, 2, 1),
+                                            (3, 128, 6, 6, 36, 3, 1, 1), (2, 64, 8, 8, 9, 4, 2, 1),
+                                            (16, 512, 4, 4, 512, 3, 1, 1)]:
+        torch.manual_seed(N * Cin + Cout + 1)
+        g = Fn.Geom(Cout, k, k, st, pad, pad, 0)
+        x = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        Wt = (torch.randn(Cout, Cin, k, k) * 0.05).to(gpu)
+        b = torch.randn(Cout).to(gpu)
+        gam = torch.tensor([0.7]).to(gpu)
+        Ho, Wo = g.out_hw(H, W)
+        res = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
+        dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
+        gate = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        halfres = _nhwc(torch.randn(N, Cin, H // 2, W // 2), gpu)
+
+        def run():
+            return [Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, res=res, gamma=gam).float().cpu(),
+                    Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, out_f32=True).cpu(),
+                    Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), gate=gate, gate_act=lrelu).float().cpu(),
+                    Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), res=halfres, res_up2=1,
+                                         res_scale=0.25).float().cpu()]
+        for vec in ('0', '1'):
+            monkeypatch.setenv('EEGAN_CONV_RED_VEC4', vec)
+            monkeypatch.setenv('EEGAN_CONV_SPLITK_FUSED', '0')
+            ref = run()
+            monkeypatch.setenv('EEGAN_CONV_SPLITK_FUSED', '1')
+            for _ in range(3):
+                for a, c in zip(ref, run()):
+                    assert torch.equal(a, c), (N, Cin, Cout, k, vec)
+
+
 @pytest.mark.parametrize('target', ['512', '4096'])
 def test_conv_wide_stages_bit_identical(gpu, monkeypatch, target):
     """Wide pair stages (one 64-channel stage of whole 128-B lines per K-step

@@ -89,8 +89,16 @@ def main():
                 for _ in range(args.iters):
                     fn()
                 summ = Fn.TIMER.summary()
+                parts = [0.0, 0.0]
+                ms = __import__('ctypes').c_float()
+                for _, _, _, pairs in Fn.TIMER.rec:
+                    for i, (a0, a1) in enumerate(pairs[:2]):
+                        Fn.ops.event_elapsed(a0, a1, __import__('ctypes').byref(ms))
+                        parts[i] += ms.value * 1e3 / args.iters
                 Fn.TIMER = None
                 us = sum(v[3] for v in summ.values()) * 1e6 / args.iters
+                if parts[1]:
+                    print('%-16s %-6s   kernel %7.2f us + reduce %6.2f us' % (name, dname, parts[0], parts[1]))
             else:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
