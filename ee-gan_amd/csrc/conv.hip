@@ -1001,7 +1001,9 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
   constexpr int YNG = S - 2 * KS;  // stages allowed in flight at the wait
   static_assert(YNG >= 0, "stages");
   if (wide) {
-    if (nk > 0) issue_wide(0);   // stages 0 and 1 (S - KS == 2)
+#pragma unroll
+    for (int st = 0; st < S - KS; st += 2)   // (S - KS) / 2 wide stages: slots (st, st + 1)
+      if (st < nk) issue_wide(st);
   } else {
 #pragma unroll
     for (int st = 0; st < S - KS; ++st)
@@ -2616,7 +2618,13 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
     // the separate reduce kernel (profiles/r03_splitk_fused.log)
     if (p.nsplit > 1 && env_int("EEGAN_CONV_SPLITK_FUSED", 0))
       a.tickets = ee_tickets((long)grid.x * grid.y * a.ncls, s);
+    // small grids (<= deep_blocks workgroups, about one per CU): an 8-stage ring keeps
+    // three K-step pairs in flight per workgroup instead of one (EEGAN_CONV_DEEP=0: 4 stages)
+    const int deep_blocks = env_int("EEGAN_CONV_DEEP", 0);
+    const bool deep = ksv == 22 && (long)grid.x * grid.y * grid.z <= deep_blocks;
     if (p.tco == 128) { if (p.tpix == 128) FA(128, 128); else FA(128, 64); }
+    else if (p.tco == 64 && p.tpix == 64 && deep)
+      ee_launch(conv_fast_kernel<MODE, 64, 64, 2, 8, 2>, grid, dim3(256), 0, s, a, src_bytes, w_bytes);
     else if (p.tco == 64) { if (p.tpix == 128) FA(64, 128); else FA(64, 64); }
     else if (p.tco == 32) { if (p.tpix == 256) FA(32, 256); else FA(32, 64); }
     else { if (p.tpix == 256) FA(16, 256); else FA(16, 64); }
