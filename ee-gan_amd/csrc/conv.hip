@@ -157,6 +157,10 @@ EE_DEV void igemm_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], int 
       if (co >= a.Mrows) continue;
       if (a.nsplit > 1) {
         float* dst = a.part + ((long)split * a.P + p) * a.Mrows + co;
+        if ((a.Mrows & 3) == 0) {   // one 16-B store (slab rows 16-B aligned): 4x fewer store issues
+          *reinterpret_cast<f32x4_t*>(dst) = acc[i][j];
+          continue;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (co + r < a.Mrows) dst[r] = acc[i][j][r];
@@ -1148,6 +1152,7 @@ struct WgradArgs {
   int lddy, Cout, P, p_per_split;
   float* dw;           // nsplit == 1: epilogue writes the torch layout directly
   int accumulate;
+  int quad;            // split slab in co-quad order [Cout/4][K][4] (Cout % 4 == 0): one 16-B store per lane
 };
 
 // split-slab column (co, (tap, c)) -> channels-last weight layout [Cout][R][S][Cin]
@@ -1162,6 +1167,53 @@ struct WgradMap {
     return c < Cin ? ((long)co * RS + tap) * Cin + c : -1;
   }
 };
+
+// Split-slab reduce of co-quad slabs (WgradArgs::quad: [nsplit][Cout/4][K][4]):
+// thread (k, quad) sums its four columns as one 16-B load per split and writes
+// the four dW entries (each a coalesced run along k across the wave).  Row
+// groups, chunking and the final group order are colsum_rows_kernel's, per
+// column, so the sums are bit-identical to the row-major slab's reduce.
+template <int COLS, int RG>
+__global__ __launch_bounds__(COLS * RG) void wgrad_quad_reduce_kernel(const float* __restrict__ in, int nrows,
+                                                                      long stride, float* __restrict__ out,
+                                                                      int accumulate, WgradMap map) {
+  __shared__ f32x4_t sh[RG][COLS];
+  const int lane = threadIdx.x % COLS, g = threadIdx.x / COLS;
+  const int k = blockIdx.x * COLS + lane, c4 = blockIdx.y;
+  const bool ok = k < map.K;
+  const f32x4_t* src = reinterpret_cast<const f32x4_t*>(in) + ((long)c4 * map.K + k);
+  const long st4 = stride / 4;
+  f32x4_t s = {0.f, 0.f, 0.f, 0.f};
+  if (ok) {
+    int r = g;
+    for (; r + 3 * RG < nrows; r += 4 * RG) {
+      const f32x4_t a0 = src[(long)r * st4], a1 = src[(long)(r + RG) * st4];
+      const f32x4_t a2 = src[(long)(r + 2 * RG) * st4], a3 = src[(long)(r + 3 * RG) * st4];
+      s += a0;
+      s += a1;
+      s += a2;
+      s += a3;
+    }
+    for (; r < nrows; r += RG) s += src[(long)r * st4];
+  }
+  if (RG > 1) {
+    sh[g][lane] = s;
+    __syncthreads();
+  }
+  if (g == 0 && ok) {
+    f32x4_t t = s;
+    if (RG > 1) {
+      t = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+      for (int i = 0; i < RG; ++i) t += sh[i][lane];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long o = map((long)(c4 * 4 + j) * map.K + k);
+      if (o >= 0) out[o] = accumulate ? out[o] + t[j] : t[j];
+    }
+  }
+}
 
 constexpr int TRP = 4;  // row padding (elements) for transposed-read tiles
 
@@ -1198,6 +1250,20 @@ EE_DEV void wgrad_epilogue(const WgradArgs& w, const f32x4_t (&acc)[FI][FJ], int
     return;
   }
   float* ws = w.ws + (long)blockIdx.z * w.Cout * w.K;
+  if (w.quad) {
+    // lane (g, li) holds co = ...+ 4g + r, r = 0..3: one co quad at one k -> 16 contiguous bytes
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const int co = co0 + wi * WT_CO + i * 16 + g * 4;
+      if (co >= w.Cout) continue;
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) {
+        const int k = kb0 + wj * WT_K + j * 16 + li;
+        if (k < w.K) *reinterpret_cast<f32x4_t*>(ws + ((long)(co >> 2) * w.K + k) * 4) = acc[i][j];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < FI; ++i) {
 #pragma unroll
@@ -2618,13 +2684,7 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
     // the separate reduce kernel (profiles/r03_splitk_fused.log)
     if (p.nsplit > 1 && env_int("EEGAN_CONV_SPLITK_FUSED", 0))
       a.tickets = ee_tickets((long)grid.x * grid.y * a.ncls, s);
-    // small grids (<= deep_blocks workgroups, about one per CU): an 8-stage ring keeps
-    // three K-step pairs in flight per workgroup instead of one (EEGAN_CONV_DEEP=0: 4 stages)
-    const int deep_blocks = env_int("EEGAN_CONV_DEEP", 0);
-    const bool deep = ksv == 22 && (long)grid.x * grid.y * grid.z <= deep_blocks;
     if (p.tco == 128) { if (p.tpix == 128) FA(128, 128); else FA(128, 64); }
-    else if (p.tco == 64 && p.tpix == 64 && deep)
-      ee_launch(conv_fast_kernel<MODE, 64, 64, 2, 8, 2>, grid, dim3(256), 0, s, a, src_bytes, w_bytes);
     else if (p.tco == 64) { if (p.tpix == 128) FA(64, 128); else FA(64, 64); }
     else if (p.tco == 32) { if (p.tpix == 256) FA(32, 256); else FA(32, 64); }
     else { if (p.tpix == 256) FA(16, 256); else FA(16, 64); }
@@ -2929,6 +2989,9 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
     const int rc = ee_check_launch("conv_wgrad(thin)");
     if (rc) return rc;
   } else if (w.P > 0) {
+    // co-quad slabs where they measured ahead (K > 1024; at K <= 1024 the quad reduce has too few blocks)
+    w.quad = nsplit > 1 && d->K % 4 == 0 && ((uintptr_t)ws & 15) == 0 && K > env_int("EEGAN_WGRAD_QUAD_MINK", 1024) &&
+             env_int("EEGAN_WGRAD_QUAD", 1);
     dim3 grid(ee_cdiv(K, TK), ee_cdiv(d->K, TCO), nsplit);
     const long x_bytes = wgrad_x_bytes(d), dy_bytes = wgrad_dy_bytes(d);
 #define WG(TC, TKK, WC) ee_launch(conv_wgrad_kernel<TC, TKK, WC>, grid, dim3(256), 0, stream, w)
@@ -2964,8 +3027,21 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
     nsplit = 0;
   }
   const long cols = (long)d->K * K;
-  launch_colsum<float, float>(ws, nsplit, cols, cols, 0, dw, 0, 1, accumulate, stream,
-                              WgradMap{K, w.Cg, d->C, d->R * d->S});
+  if (w.quad) {
+    const WgradMap map{K, w.Cg, d->C, d->R * d->S};
+    const unsigned c4 = (unsigned)(d->K / 4);
+    if (nsplit <= 8)
+      ee_launch(wgrad_quad_reduce_kernel<256, 1>, dim3(ee_cdiv(K, 256), c4), dim3(256), 0, stream, ws, nsplit, cols,
+                dw, accumulate, map);
+    else if (nsplit <= 128)
+      ee_launch(wgrad_quad_reduce_kernel<32, 8>, dim3(ee_cdiv(K, 32), c4), dim3(256), 0, stream, ws, nsplit, cols, dw,
+                accumulate, map);
+    else
+      ee_launch(wgrad_quad_reduce_kernel<32, 32>, dim3(ee_cdiv(K, 32), c4), dim3(1024), 0, stream, ws, nsplit, cols,
+                dw, accumulate, map);
+  } else
+    launch_colsum<float, float>(ws, nsplit, cols, cols, 0, dw, 0, 1, accumulate, stream,
+                                WgradMap{K, w.Cg, d->C, d->R * d->S});
   return ee_check_launch("wgrad_reduce");
 }
 

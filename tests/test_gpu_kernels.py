@@ -685,6 +685,67 @@ def test_elementwise_ops(gpu):
     assert rel_l2(fcd.grad.cpu(), gv.reshape(3, -1)) < 1e-6
 
 
+def test_wgrad_quad_slab_bit_identical(gpu, monkeypatch):
+    """Split weight gradients written as co-quad slabs (EEGAN_WGRAD_QUAD=1,
+    default: one 16-B store per lane) reduce to the same bits as the row-major
+    slabs: the column sums visit the same splits in the same order.  Covers
+    accumulation into an existing gradient and Cout % 4 != 0 (row-major)."""
+    Fn, T, _ = _mods()
+    monkeypatch.setenv('EEGAN_WGRAD_QUAD_MINK', '0')   # quad slabs at every K (default: K > 1024)
+    for N, Cin, H, W, Cout, k, st, pad in [(4, 64, 32, 32, 64, 3, 1, 1), (2, 128, 16, 16, 256, 4, 2, 1),
+                                            (8, 32, 64, 64, 36, 3, 1, 1), (16, 256, 8, 8, 512, 3, 1, 1)]:
+        torch.manual_seed(Cin + H + Cout)
+        g = Fn.Geom(Cout, k, k, st, pad, pad, 0)
+        x = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        Ho, Wo = g.out_hw(H, W)
+        dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
+        outs = []
+        for q in ('0', '1'):
+            monkeypatch.setenv('EEGAN_WGRAD_QUAD', q)
+            dW = torch.ones(Cout, Cin, k, k, device=gpu).contiguous(memory_format=torch.channels_last)
+            Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, k, k), out=dW)
+            outs.append((Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, k, k)).cpu(), dW.cpu()))
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), (N, Cin, H, Cout)
+        xr = x.float().cpu().requires_grad_()
+        wr = torch.zeros(Cout, Cin, k, k, requires_grad=True)
+        F.conv2d(x.float().cpu(), wr, None, st, pad).backward(dz.float().cpu())
+        assert rel_l2(outs[1][0], wr.grad) < 1e-4
+
+
+@pytest.mark.parametrize('P', [64, 4096, 1 << 18])
+def test_dot_in_kernel_finish(gpu, monkeypatch, P):
+    """<g, h> partials finished by the last-arriving block (ticket) == the
+    separate dot_final launch (EEGAN_DOT_FUSED=0) to fp32 rounding of a
+    different summation tree; repeated calls (each launch resets its ticket),
+    the scale-add backward's fused <g, h> accumulated into a sink, and the
+    fp64 sum of the bf16 inputs."""
+    Fn, T, _ = _mods()
+    torch.manual_seed(11)
+    C = 40
+    x = _nhwc(_bf(torch.randn(1, C, P // 64, 64)), gpu)
+    y = _nhwc(_bf(torch.randn(1, C, P // 64, 64)), gpu)
+    ref = (x.double() * y.double()).sum().item()
+    outs = {}
+    for fused in ('0', '1'):
+        monkeypatch.setenv('EEGAN_DOT_FUSED', fused)
+        vals = [Fn._dot_raw(x, y).item() for _ in range(3)]
+        assert vals[0] == vals[1] == vals[2], vals       # deterministic, tickets reset
+        outs[fused] = vals[0]
+        g = torch.zeros(1, device=gpu)
+        gm = torch.tensor([0.5], device=gpu)
+        d = torch.empty_like(x)
+        ws = T.workspace(Fn.ops.dot_workspace(), gpu)
+        for _ in range(2):   # accumulate twice into the sink
+            Fn.ops.scale_dot(x.data_ptr(), Fn.ld_of(x), y.data_ptr(), Fn.ld_of(y), gm.data_ptr(), 1.0, P, C,
+                             d.data_ptr(), Fn.ld_of(d), ws.data_ptr(), g.data_ptr(), 1, 0, 0.2, Fn.stream())
+        assert abs(g.item() - 2 * ref) <= 1e-5 * abs(2 * ref) + 1e-3, (fused, g.item(), ref)
+        assert rel_l2(d.float().cpu(), 0.5 * x.float().cpu()) < 1e-2
+    scale = max(abs(ref), 1.0)
+    assert abs(outs['1'] - outs['0']) <= 1e-5 * scale, outs
+    assert abs(outs['1'] - ref) <= 1e-5 * scale, (outs, ref)
+
+
 def test_linear_and_attr(gpu):
     Fn, T, _ = _mods()
     from eegan_hip.nn import Linear
