@@ -60,6 +60,11 @@ LATE_JOIN = os.environ.get('EEGAN_LATE_JOIN', '0') == '1'
 # backward'): they stop competing with the critical lane and fill the GPU
 # during the generator's backward instead (needs LATE_JOIN).
 DEFER_D = os.environ.get('EEGAN_DEFER_D', '').replace('_', ' ')   # underscores stand for spaces
+# EEGAN_EARLY_D0=1: Dis64's whole d_update (and its g_update term) is issued on
+# its lane as soon as the generator has produced img_64 (Gen._image_hook), so it
+# runs beside the generator's stages 2-3 -- a stretch where the generator's
+# small launches leave most of the GPU idle -- instead of beside D256's update.
+EARLY_D0 = os.environ.get('EEGAN_EARLY_D0', '0') == '1'   # measured: G's forward slows by ~1 ms beside it, neutral to -0.7 % (profiles/r03_early_d0.txt)
 
 
 class Trainer(object):
@@ -88,6 +93,7 @@ class Trainer(object):
         self.use_streams = bool(streams) and torch.cuda.is_available() and torch.device(device).type == 'cuda'
         self._streams = None
         self._mark_want = self._mark_ev = None
+        self._early_done = {}
 
     def _side_streams(self, n, fork=True):
         if not self.use_streams:
@@ -235,14 +241,41 @@ class Trainer(object):
         return (w[0] + w[1]) * lam, (s[0] + s[1]) * lam, (a[0] + a[1]) * lam
 
     # ----------------------------------------------------------- updates --
+    def d_update_early(self, i, imgs, fake_img, sent_emb, unpair_sent_emb, class_labels, iter_rec, g_early):
+        """Issue discriminator i's d_update (train.py:439-466) and, when
+        `g_early` is a list, its g_update term on its own lane now -- forked
+        from the caller's stream at this point, so it waits only for the work
+        issued so far (the generator up to `fake_img`).  d_update then skips
+        it and joins its lane with the others.  Returns the g term or None."""
+        lane = self._side_streams(len(self.netsD), fork=False)[i]
+        lane.wait_stream(torch.cuda.current_stream())
+        fakes = [None] * len(self.netsD)
+        fakes[i] = fake_img
+        with self._on(lane):
+            Fn.stamp('D%d start' % i)
+            self._d_update_one(i, imgs, fakes, sent_emb, unpair_sent_emb, class_labels, iter_rec)
+            term = self._g_term(i, fakes, sent_emb, class_labels, iter_rec) if g_early is not None else None
+        self._early_done[i] = term
+        return term
+
     def d_update(self, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec=False, g_early=None,
                  before_join=None):
         """train.py:437-469: per D a hinge(+class) step, then a GP step (each D
         on its own stream).  `g_early` (a list): also run g_update's generator
-        loss term through each D right after that D's update, into the list."""
-        streams = self._side_streams(len(self.netsD))
+        loss term through each D right after that D's update, into the list.
+        Discriminators already issued by d_update_early are only joined."""
         nD = len(self.netsD)
+        done = self._early_done
+        self._early_done = {}
+        streams = self._side_streams(nD, fork=False)
+        if streams[0] is not None:
+            main = torch.cuda.current_stream()
+            for i, s in enumerate(streams):
+                if i not in done:
+                    s.wait_stream(main)
         g_terms = [None] * nD
+        for i, t in done.items():
+            g_terms[i] = t
         order = range(nD)
         if LANE_ORDER == 'rev':
             order = reversed(order)
@@ -251,6 +284,8 @@ class Trainer(object):
         self._mark_want = 'D%d %s' % (nD - 1, DEFER_D) if defer else None
         self._mark_ev = None
         for i in order:
+            if i in done:
+                continue
             if defer and i < nD - 1 and self._mark_ev is not None:
                 streams[i].wait_event(self._mark_ev)
             with self._on(streams[i]):
@@ -498,7 +533,15 @@ class Trainer(object):
             noise = torch.randn(B, 100, device=dev)
         _, attn_attr_emb = self.attr_enhance(sent, attrs)
         attn_attr_emb = self.attr_enhance.module.attr_merge(attn_attr_emb)
-        fake_imgs = self.netG(noise, sent, attn_attr_emb)
+        gen = getattr(self.netG, 'module', self.netG)
+        g_early_on = G_EARLY and self.use_streams
+        if EARLY_D0 and self.use_streams and len(self.netsD) == 3 and not LATE_JOIN and not DEFER_D:
+            gen._image_hook = lambda i, img: self.d_update_early(
+                i, batch['imgs'], img, sent, unpair, class_labels, iter_rec, [] if g_early_on else None)
+        try:
+            fake_imgs = self.netG(noise, sent, attn_attr_emb)
+        finally:
+            gen._image_hook = None
         Fn.stamp('ATTR + G forward')
         _, _, match_labels = prepare_labels(B, dev)
         cls_ids = batch.get('cls_ids')  # train.py:490 passes class ids to DAMSM_loss even without USE_CLASS
