@@ -2422,7 +2422,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_thin_kernel(WgradArgs w, int x
       xv[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? off : 0x80000000, 0, 0));
     }
     const int dr = tid >> 6, dc = tid & 63;
-    const int doff = ((((n * w.OH + y0 + dr) * w.OW) + x0 + dc) * w.lddy) * 2;
+    const int doff = ((((n * w.OH + y0 + dr) * w.OW) + x0 + dc) * w.lddy + 8 * (int)blockIdx.y) * 2;
     const uint4 dv = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rd, doff, 0, 0));
     __syncthreads();  // previous tile's reads done
 #pragma unroll
@@ -2468,8 +2468,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_thin_kernel(WgradArgs w, int x
     const int tap = t / CGB, cb = t - tap * CGB;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int co = 4 * kg + i;
-      if (co < w.Cout) slab[co * w.K + tap * (16 * CGB) + cb * 16 + li] = acc[j][i];
+      const int co = 4 * kg + i, cog = 8 * (int)blockIdx.y + co;   // this block's 8-channel group
+      if (co < 8 && cog < w.Cout) slab[cog * w.K + tap * (16 * CGB) + cb * 16 + li] = acc[j][i];
     }
   }
 }
@@ -2906,7 +2906,8 @@ static int wgrad_thin_blocks(const eegan_conv_desc* d) {
   if (!env_int("EEGAN_CONV_THIN", 1)) return 0;
   if (d->R != 3 || d->S != 3 || d->stride != 1 || d->pad_h != 1 || d->pad_w != 1 || d->up2) return 0;
   const int cg = ee_round_up(d->C, 8);
-  if (d->K > 8 || (cg != 32 && cg != 64) || d->Wo % WTH_W || d->Ho % WTH_H) return 0;
+  // output channels in 8-channel groups on blockIdx.y (each group re-reads the x halo)
+  if (d->K > env_int("EEGAN_WGRAD_THIN_MAXK", 8) || (cg != 32 && cg != 64) || d->Wo % WTH_W || d->Ho % WTH_H) return 0;
   if (wgrad_x_bytes(d) >= 0x7fffffffL || wgrad_dy_bytes(d) >= 0x7fffffffL) return 0;
   const int tiles = d->N * (d->Ho / WTH_H) * (d->Wo / WTH_W);
   if (tiles < 8) return 0;
@@ -2980,11 +2981,12 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
   }
   if (w.P > 0 && wgrad_thin_blocks(d)) {
     const int tiles = d->N * (d->Ho / WTH_H) * (d->Wo / WTH_W);
+    const dim3 grid(nsplit, ee_cdiv(d->K, 8));
     if (w.Cg == 32)
-      ee_launch(conv_wgrad_thin_kernel<2>, dim3(nsplit), dim3(256), 0, stream, w, (int)wgrad_x_bytes(d),
+      ee_launch(conv_wgrad_thin_kernel<2>, grid, dim3(256), 0, stream, w, (int)wgrad_x_bytes(d),
                 (int)wgrad_dy_bytes(d), ee_cdiv(tiles, nsplit));
     else
-      ee_launch(conv_wgrad_thin_kernel<4>, dim3(nsplit), dim3(256), 0, stream, w, (int)wgrad_x_bytes(d),
+      ee_launch(conv_wgrad_thin_kernel<4>, grid, dim3(256), 0, stream, w, (int)wgrad_x_bytes(d),
                 (int)wgrad_dy_bytes(d), ee_cdiv(tiles, nsplit));
     const int rc = ee_check_launch("conv_wgrad(thin)");
     if (rc) return rc;

@@ -148,6 +148,30 @@ def test_conv_thin_wgrad(gpu, monkeypatch):
         assert torch.allclose(outs[0], outs[1], rtol=1e-5, atol=1e-4)
 
 
+def test_conv_thin_wgrad_channel_groups(gpu, monkeypatch):
+    """The thin weight-gradient kernel for up to 64 output channels, in
+    8-channel groups on the grid's y axis (EEGAN_WGRAD_THIN_MAXK): against
+    torch fp32 and the tile path; a ragged last group (Cout % 8 != 0) and a
+    padded dy row (its channels past Cout are never read into written rows)."""
+    Fn, T, _ = _mods()
+    monkeypatch.setenv('EEGAN_WGRAD_THIN_MAXK', '64')
+    for N, Cin, H, W, Cout in [(2, 32, 8, 64, 32), (1, 64, 12, 128, 64), (2, 32, 4, 64, 36), (2, 28, 8, 64, 16),
+                               (1, 64, 8, 64, 20)]:
+        torch.manual_seed(N + Cin + H + Cout)
+        g = Fn.Geom(Cout, 3, 3, 1, 1, 1, 0)
+        xl = _bf(torch.randn(N, Cin, H, W))
+        dzl = _bf(torch.randn(N, Cout, H, W))
+        x, dz = _nhwc(xl, gpu), _nhwc(dzl, gpu)
+        outs = []
+        for thin in ('0', '1'):
+            monkeypatch.setenv('EEGAN_CONV_THIN', thin)
+            outs.append(Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, 3, 3)).cpu())
+        wr = torch.zeros(Cout, Cin, 3, 3, requires_grad=True)
+        F.conv2d(xl, wr, None, 1, 1).backward(dzl)
+        assert rel_l2(outs[1], wr.grad) < 1e-4, (N, Cin, H, Cout)
+        assert torch.allclose(outs[0], outs[1], rtol=1e-5, atol=1e-4)
+
+
 def test_splitk_reduce_vector_path_bit_identical(gpu, monkeypatch):
     """The split-K reduce's 4-channel vector path (default) against the scalar
     path (EEGAN_CONV_RED_VEC4=0): same summation order, so torch.equal, over

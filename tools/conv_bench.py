@@ -45,6 +45,8 @@ SHAPES = {
     'c1x1_100_128': (16, 100, 128, 128, 1, 1, 1, 0),
     'c3x3_64_100_128': (16, 64, 128, 128, 100, 3, 1, 1),
     'c3x3_128_100_64': (16, 128, 64, 64, 100, 3, 1, 1),
+    'c3x3_64_32_128': (16, 64, 128, 128, 32, 3, 1, 1),
+    'c3x3_32_16_256': (16, 32, 256, 256, 16, 3, 1, 1),
 }
 
 
