@@ -60,6 +60,16 @@ LATE_JOIN = os.environ.get('EEGAN_LATE_JOIN', '0') == '1'
 # backward'): they stop competing with the critical lane and fill the GPU
 # during the generator's backward instead (needs LATE_JOIN).
 DEFER_D = os.environ.get('EEGAN_DEFER_D', '').replace('_', ' ')   # underscores stand for spaces
+# EEGAN_TEXT_AHEAD=1: the frozen text encoder (train.py:169-184, no parameter
+# of it is trained) encodes the NEXT batch's captions on its own lane while
+# g_update's backward runs -- a stretch where the generator's small launches
+# leave the GPU mostly idle -- and the step starts from the embeddings the
+# previous step produced, instead of encoding its own batch first on the
+# critical path.  Every step still encodes exactly one batch; the next
+# batch's token tensors come from batch['next'] (the same keys as the batch;
+# absent: the batch itself, the fixed-buffer steady state of bench.py).  The
+# first step of a trainer encodes its own batch up front.
+TEXT_AHEAD = os.environ.get('EEGAN_TEXT_AHEAD', '0') == '1'   # measured -0.6 % (profiles/r03_text_ahead.txt): off
 # EEGAN_EARLY_D0=1: Dis64's whole d_update (and its g_update term) is issued on
 # its lane as soon as the generator has produced img_64 (Gen._image_hook), so it
 # runs beside the generator's stages 2-3 -- a stretch where the generator's
@@ -94,6 +104,8 @@ class Trainer(object):
         self._streams = None
         self._mark_want = self._mark_ev = None
         self._early_done = {}
+        self._emb_cur = self._emb_nxt = None   # TEXT_AHEAD buffers: this step's / the next step's embeddings
+        self._text_lane = None
 
     def _side_streams(self, n, fork=True):
         if not self.use_streams:
@@ -524,7 +536,14 @@ class Trainer(object):
         if Fn.WGRAD_SIDE and self.use_streams:
             Fn.WGRAD_SIDE_FROM.add(torch.cuda.current_stream().cuda_stream)
         Fn.stamp('start')
-        words, sent, attrs, unpair = emb if emb is not None else self.encode_text(batch)
+        ahead = emb is None and TEXT_AHEAD and self.use_streams and self.text_encoder is not None
+        if ahead:
+            if self._emb_cur is None:   # a trainer's first step: its own batch, now
+                self._emb_cur = [t.detach().clone() for t in self.encode_text(batch)]
+                self._emb_nxt = [torch.empty_like(t) for t in self._emb_cur]
+            words, sent, attrs, unpair = self._emb_cur
+        else:
+            words, sent, attrs, unpair = emb if emb is not None else self.encode_text(batch)
         Fn.stamp('text encode')
         class_labels = None
         if self.disc_class:
@@ -557,8 +576,20 @@ class Trainer(object):
         self.d_update(batch['imgs'], fake_imgs, sent, unpair, class_labels, iter_rec, g_early=terms,
                       before_join=issue_damsm if early and LANE_ORDER == 'rev' else None)
         damsm = damsm or None
+        if ahead:   # the next batch's embeddings, beside g_update's backward
+            if self._text_lane is None:
+                self._text_lane = new_stream(self.device)
+            lane = self._text_lane
+            lane.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(lane):
+                for d, t in zip(self._emb_nxt, self.encode_text(batch.get('next', batch))):
+                    d.copy_(t)
         g = self.g_update(fake_imgs, sent, words, attn_attr_emb, cls_ids, B, match_labels, batch['cap_lens'],
                           class_labels, iter_rec, damsm=damsm, terms=terms)
+        if ahead:   # every reader of this step's embeddings is joined into this stream by now
+            torch.cuda.current_stream().wait_stream(lane)
+            for c, n in zip(self._emb_cur, self._emb_nxt):
+                c.copy_(n)
         Fn.stamp('end')
         return fake_imgs, g
 
