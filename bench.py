@@ -327,6 +327,8 @@ def main():
                 e['pmc_over_algorithmic'] = round(q['hbm_bytes_per_call'] / max(v[2] / n_k, 1), 3)
             if q.get('mfma_util') is not None:
                 e['mfma_busy'] = q['mfma_util']
+            if q.get('mfma_busy_cycles_per_call'):
+                e['mfma_busy_at_event_time'] = round(q['mfma_busy_cycles_per_call'] / (v[3] / n_k * 2.4e9 * 1024), 4)
         fam_out[k] = e
     roof = {'kernel': kind, 'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': MFMA_PEAK_TFLOPS,
             'unit': 'TFLOP/s', 'frac': round(achieved / MFMA_PEAK_TFLOPS, 4), 'traffic': traffic,
@@ -344,6 +346,11 @@ def main():
             'algorithmic_hbm_GBs': round(nb / tsec / 1e9, 1),
             'mfma_busy': pf.get('mfma_util') if pf.get('mfma_util_unit') else None,
             'mfma_busy_unit': pf.get('mfma_util_unit'),
+            # the same counter (MFMA-busy cycles per launch, PMC pass) over THIS run's event-timed launch
+            # duration x 2.4 GHz x 1024 SIMDs: the denominator `frac` uses, so the two compare directly
+            # (counted cycles >= the FLOP count's cycles, so this is >= frac unless the counter under-counts)
+            'mfma_busy_at_event_time': round(pf['mfma_busy_cycles_per_call'] / (tsec / n * 2.4e9 * 1024), 4)
+            if pf.get('mfma_busy_cycles_per_call') else None,
             # north_star's conv-path HBM figure: PMC FETCH+WRITE bytes over kernel time, / 8 TB/s
             # (wasted re-reads count as achieved bandwidth here; pmc_over_algorithmic says how many)
             'pmc_hbm_GBs': round(traffic / pf['avg_call_us'] / 1e3, 1) if traffic and pf.get('avg_call_us') else None,
