@@ -322,12 +322,12 @@ def main():
             e['algorithmic_flops_per_launch'] = round(v[1] / n_k)
             e['frac_of_mfma_peak'] = round(v[1] / max(v[3], 1e-12) / 1e12 / MFMA_PEAK_TFLOPS, 4)
             q = pfams.get(k, {})
-            if q.get('hbm_bytes_per_call'):
+            if q.get('hbm_bytes_per_call') and v[2] > 0:
                 e['pmc_bytes_per_launch'] = q['hbm_bytes_per_call']
                 e['pmc_over_algorithmic'] = round(q['hbm_bytes_per_call'] / max(v[2] / n_k, 1), 3)
             if q.get('mfma_util') is not None:
                 e['mfma_busy'] = q['mfma_util']
-            if q.get('mfma_busy_cycles_per_call'):
+            if q.get('mfma_busy_cycles_per_call') and v[1] > 0:
                 e['mfma_busy_at_event_time'] = round(q['mfma_busy_cycles_per_call'] / (v[3] / n_k * 2.4e9 * 1024), 4)
         fam_out[k] = e
     roof = {'kernel': kind, 'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': MFMA_PEAK_TFLOPS,
@@ -339,7 +339,7 @@ def main():
             'traffic_git_head': (summ or {}).get('git_head'),
             'algorithmic_bytes_per_launch': round(nb / n),
             'algorithmic_flops_per_launch': round(fl / n),
-            'pmc_over_algorithmic': round(traffic / (nb / n), 3) if traffic else None,
+            'pmc_over_algorithmic': round(traffic / (nb / n), 3) if traffic and nb > 0 else None,
             'launches_per_step': n // per, 'avg_launch_us': round(tsec / n * 1e6, 2),
             'timing': 'HIP start/stop events per dispatch (hipExtLaunchKernel) over %d eager step(s) of the same '
                       'workload right after the timed region' % per,
@@ -350,7 +350,7 @@ def main():
             # duration x 2.4 GHz x 1024 SIMDs: the denominator `frac` uses, so the two compare directly
             # (counted cycles >= the FLOP count's cycles, so this is >= frac unless the counter under-counts)
             'mfma_busy_at_event_time': round(pf['mfma_busy_cycles_per_call'] / (tsec / n * 2.4e9 * 1024), 4)
-            if pf.get('mfma_busy_cycles_per_call') else None,
+            if pf.get('mfma_busy_cycles_per_call') and fl > 0 else None,
             # north_star's conv-path HBM figure: PMC FETCH+WRITE bytes over kernel time, / 8 TB/s
             # (wasted re-reads count as achieved bandwidth here; pmc_over_algorithmic says how many)
             'pmc_hbm_GBs': round(traffic / pf['avg_call_us'] / 1e3, 1) if traffic and pf.get('avg_call_us') else None,
