@@ -1153,6 +1153,7 @@ struct WgradArgs {
   float* dw;           // nsplit == 1: epilogue writes the torch layout directly
   int accumulate;
   int quad;            // split slab in co-quad order [Cout/4][K][4] (Cout % 4 == 0): one 16-B store per lane
+  int stage;           // unsplit dW through LDS: 16-B read-add-write runs along Cin (Cin % 4 == 0, host-checked)
 };
 
 // split-slab column (co, (tap, c)) -> channels-last weight layout [Cout][R][S][Cin]
@@ -1276,6 +1277,50 @@ EE_DEV void wgrad_epilogue(const WgradArgs& w, const f32x4_t (&acc)[FI][FJ], int
         if (k < w.K) ws[(long)co * w.K + k] = acc[i][j][r];
       }
     }
+  }
+}
+
+// Unsplit dW epilogue through the idle LDS ring: the fp32 tile is written as
+// [co][k] with the 16-B chunk index XOR 4 * ((co >> 2) & (TK / 16 - 1)) (conflict-free
+// ds_write_b32 for the fragments' 4-row lane groups, conflict-free ds_read_b128
+// along k; the XOR stays inside the row's TK / 4 chunks), then every thread owns 4 consecutive k of one output channel: one
+// 16-B load of the old dW (when accumulating), one 16-B store -- instead of
+// four dword loads and stores per fragment row.  Same fp32 additions: bit-
+// identical to wgrad_epilogue.
+template <int TCO, int TK, int FI, int FJ, int WT_CO, int WT_K>
+EE_DEV void wgrad_epilogue_staged(const WgradArgs& w, const f32x4_t (&acc)[FI][FJ], int co0, int kb0, int wi,
+                                  int wj, int lane, int tid, float* st) {
+  static_assert(TK % 16 == 0 && TCO % 16 == 0, "tile");
+  const int g = lane >> 4, li = lane & 15;
+  constexpr int CM = TK / 16 - 1;   // XOR masks stay inside the row's TK / 4 chunks
+  auto phys = [](int row, int k) { return row * TK + ((((k >> 2) ^ (4 * ((row >> 2) & CM))) << 2) | (k & 3)); };
+  __syncthreads();   // every wave's last ring reads are done
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wi * WT_CO + i * 16 + g * 4 + r, k = wj * WT_K + j * 16 + li;
+        st[phys(row, k)] = acc[i][j][r];
+      }
+  __syncthreads();
+  const WgradMap map{w.K, w.Cg, w.Cin, w.R * w.S};
+  constexpr int K4 = TK / 4, ITEMS = TCO * K4;
+#pragma unroll 4
+  for (int item = tid; item < ITEMS; item += 256) {
+    const int row = item / K4, k = (item - row * K4) * 4;
+    const int co = co0 + row, kk = kb0 + k;
+    if (co >= w.Cout || kk >= w.K) continue;
+    const long o = map((long)co * w.K + kk);
+    if (o < 0) continue;   // padding channels (Cin % 4 == 0: a run is all valid or all padding)
+    f32x4_t v = *reinterpret_cast<const f32x4_t*>(st + phys(row, k));
+    f32x4_t* dst = reinterpret_cast<f32x4_t*>(w.dw + o);
+    if (w.accumulate) {
+      const f32x4_t old = *dst;
+      v = old + v;
+    }
+    *dst = v;
   }
 }
 
@@ -1751,6 +1796,12 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fast_kernel(WgradArgs w, lo
         for (int j = 0; j < FJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[k][i], fb[k][j], acc[i][j], 0, 0, 0);
     }
+  }
+  static_assert(TCO * TK * 4 <= S * STAGE * 2, "staged dW tile exceeds the LDS ring");
+  if (w.dw && w.stage) {
+    wgrad_epilogue_staged<TCO, TK, FI, FJ, WT_CO, WT_K>(w, acc, co0, kb0, wi, wj, lane, tid,
+                                                       reinterpret_cast<float*>(lds));
+    return;
   }
   wgrad_epilogue<FI, FJ, WT_CO, WT_K>(w, acc, co0, kb0, wi, wj, lane);
 }
@@ -2978,6 +3029,7 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
   if (nsplit == 1 && w.P > 0) {
     w.dw = dw;
     w.accumulate = accumulate;
+    w.stage = d->C % 4 == 0 && ((uintptr_t)dw & 15) == 0 && env_int("EEGAN_WGRAD_STAGE_EPI", 1);
   }
   if (w.P > 0 && wgrad_thin_blocks(d)) {
     const int tiles = d->N * (d->Ho / WTH_H) * (d->Wo / WTH_W);

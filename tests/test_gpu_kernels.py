@@ -709,6 +709,35 @@ def test_elementwise_ops(gpu):
     assert rel_l2(fcd.grad.cpu(), gv.reshape(3, -1)) < 1e-6
 
 
+def test_wgrad_staged_epilogue_bit_identical(gpu, monkeypatch):
+    """Unsplit weight gradients through the LDS-staged dW epilogue
+    (EEGAN_WGRAD_STAGE_EPI=1, default: 16-B read-add-write runs) equal the
+    direct epilogue bit for bit, fresh and accumulated into an existing
+    gradient; the DiscCond-head shapes (4x4 grids, 768 / 1024 channels) and
+    ragged tiles (Cout, K not multiples of the tile)."""
+    Fn, T, _ = _mods()
+    monkeypatch.setenv('EEGAN_WGRAD_TARGET', '1')   # one split: the direct dW path
+    for N, Cin, H, W, Cout, k, st, pad in [(8, 768, 4, 4, 1024, 3, 1, 1), (8, 1024, 4, 4, 512, 4, 4, 0),
+                                            (4, 96, 8, 8, 72, 3, 1, 1), (2, 64, 16, 16, 200, 4, 2, 1),
+                                            (4, 256, 8, 8, 48, 1, 1, 0)]:
+        torch.manual_seed(Cin + H + Cout)
+        g = Fn.Geom(Cout, k, k, st, pad, pad, 0)
+        x = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        Ho, Wo = g.out_hw(H, W)
+        dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
+        outs = []
+        for v in ('0', '1'):
+            monkeypatch.setenv('EEGAN_WGRAD_STAGE_EPI', v)
+            dW = torch.full((Cout, Cin, k, k), 0.5, device=gpu).contiguous(memory_format=torch.channels_last)
+            Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, k, k), out=dW)
+            outs.append((Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, k, k)).cpu(), dW.cpu()))
+        for a_, b_ in zip(*outs):
+            assert torch.equal(a_, b_), (N, Cin, H, Cout, k)
+        wr = torch.zeros(Cout, Cin, k, k, requires_grad=True)
+        F.conv2d(x.float().cpu(), wr, None, st, pad).backward(dz.float().cpu())
+        assert rel_l2(outs[1][0], wr.grad) < 1e-4
+
+
 def test_wgrad_quad_slab_bit_identical(gpu, monkeypatch):
     """Split weight gradients written as co-quad slabs (EEGAN_WGRAD_QUAD=1,
     default: one 16-B store per lane) reduce to the same bits as the row-major
