@@ -1312,6 +1312,11 @@ EE_DEV void wgrad_epilogue_staged(const WgradArgs& w, const f32x4_t (&acc)[FI][F
     const int row = item / K4, k = (item - row * K4) * 4;
     const int co = co0 + row, kk = kb0 + k;
     if (co >= w.Cout || kk >= w.K) continue;
+    if (!w.dw) {   // split: this split's row-major slab [Cout][K] (K % 4 == 0, 16-B aligned)
+      *reinterpret_cast<f32x4_t*>(w.ws + ((long)blockIdx.z * w.Cout + co) * w.K + kk) =
+          *reinterpret_cast<const f32x4_t*>(st + phys(row, k));
+      continue;
+    }
     const long o = map((long)co * w.K + kk);
     if (o < 0) continue;   // padding channels (Cin % 4 == 0: a run is all valid or all padding)
     f32x4_t v = *reinterpret_cast<const f32x4_t*>(st + phys(row, k));
@@ -1798,7 +1803,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fast_kernel(WgradArgs w, lo
     }
   }
   static_assert(TCO * TK * 4 <= S * STAGE * 2, "staged dW tile exceeds the LDS ring");
-  if (w.dw && w.stage) {
+  if (w.stage) {
     wgrad_epilogue_staged<TCO, TK, FI, FJ, WT_CO, WT_K>(w, acc, co0, kb0, wi, wj, lane, tid,
                                                        reinterpret_cast<float*>(lds));
     return;
@@ -3029,7 +3034,8 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
   if (nsplit == 1 && w.P > 0) {
     w.dw = dw;
     w.accumulate = accumulate;
-    w.stage = d->C % 4 == 0 && ((uintptr_t)dw & 15) == 0 && env_int("EEGAN_WGRAD_STAGE_EPI", 1);
+    // EEGAN_WGRAD_STAGE_EPI: 0 off, 1 unsplit dW only, 2 (default) also the row-major split slabs
+    w.stage = d->C % 4 == 0 && ((uintptr_t)dw & 15) == 0 && env_int("EEGAN_WGRAD_STAGE_EPI", 2);
   }
   if (w.P > 0 && wgrad_thin_blocks(d)) {
     const int tiles = d->N * (d->Ho / WTH_H) * (d->Wo / WTH_W);
@@ -3046,6 +3052,9 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
     // co-quad slabs where they measured ahead (K > 1024; at K <= 1024 the quad reduce has too few blocks)
     w.quad = nsplit > 1 && d->K % 4 == 0 && ((uintptr_t)ws & 15) == 0 && K > env_int("EEGAN_WGRAD_QUAD_MINK", 1024) &&
              env_int("EEGAN_WGRAD_QUAD", 1);
+    // split slabs through the LDS-staged epilogue too (row-major, 16-B stores) where not co-quad
+    if (nsplit > 1 && !w.quad)
+      w.stage = ((uintptr_t)ws & 15) == 0 && env_int("EEGAN_WGRAD_STAGE_EPI", 2) >= 2;
     dim3 grid(ee_cdiv(K, TK), ee_cdiv(d->K, TCO), nsplit);
     const long x_bytes = wgrad_x_bytes(d), dy_bytes = wgrad_dy_bytes(d);
 #define WG(TC, TKK, WC) ee_launch(conv_wgrad_kernel<TC, TKK, WC>, grid, dim3(256), 0, stream, w)

@@ -753,13 +753,16 @@ def test_wgrad_quad_slab_bit_identical(gpu, monkeypatch):
         Ho, Wo = g.out_hw(H, W)
         dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
         outs = []
-        for q in ('0', '1'):
+        # row-major slabs with direct stores / co-quad slabs / row-major slabs through the LDS-staged epilogue
+        for q, stg in (('0', '1'), ('1', '1'), ('0', '2')):
+            monkeypatch.setenv('EEGAN_WGRAD_STAGE_EPI', stg)
             monkeypatch.setenv('EEGAN_WGRAD_QUAD', q)
             dW = torch.ones(Cout, Cin, k, k, device=gpu).contiguous(memory_format=torch.channels_last)
             Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, k, k), out=dW)
             outs.append((Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, k, k)).cpu(), dW.cpu()))
-        for a, b in zip(*outs):
-            assert torch.equal(a, b), (N, Cin, H, Cout)
+        for o in outs[1:]:
+            for a, b in zip(outs[0], o):
+                assert torch.equal(a, b), (N, Cin, H, Cout)
         xr = x.float().cpu().requires_grad_()
         wr = torch.zeros(Cout, Cin, k, k, requires_grad=True)
         F.conv2d(x.float().cpu(), wr, None, st, pad).backward(dz.float().cpu())
