@@ -1154,6 +1154,7 @@ struct WgradArgs {
   int accumulate;
   int quad;            // split slab in co-quad order [Cout/4][K][4] (Cout % 4 == 0): one 16-B store per lane
   int stage;           // unsplit dW through LDS: 16-B read-add-write runs along Cin (Cin % 4 == 0, host-checked)
+  int xcd_remap;       // conv_wgrad_fast_kernel: blocks of one (co tile, split) on one XCD (grid size % 8 == 0)
 };
 
 // split-slab column (co, (tap, c)) -> channels-last weight layout [Cout][R][S][Cin]
@@ -1222,7 +1223,8 @@ constexpr int TRP = 4;  // row padding (elements) for transposed-read tiles
 // written straight into torch's layout when unsplit, else into the split slab
 template <int FI, int FJ, int WT_CO, int WT_K>
 EE_DEV void wgrad_epilogue(const WgradArgs& w, const f32x4_t (&acc)[FI][FJ], int co0, int kb0, int wi, int wj,
-                           int lane) {
+                           int lane, int split = -1) {
+  if (split < 0) split = blockIdx.z;
   const int g = lane >> 4, li = lane & 15;
   if (w.dw) {
     // one fragment row block at a time: all 4*FJ old values are loaded before any
@@ -1250,7 +1252,7 @@ EE_DEV void wgrad_epilogue(const WgradArgs& w, const f32x4_t (&acc)[FI][FJ], int
     }
     return;
   }
-  float* ws = w.ws + (long)blockIdx.z * w.Cout * w.K;
+  float* ws = w.ws + (long)split * w.Cout * w.K;
   if (w.quad) {
     // lane (g, li) holds co = ...+ 4g + r, r = 0..3: one co quad at one k -> 16 contiguous bytes
 #pragma unroll
@@ -1289,7 +1291,7 @@ EE_DEV void wgrad_epilogue(const WgradArgs& w, const f32x4_t (&acc)[FI][FJ], int
 // identical to wgrad_epilogue.
 template <int TCO, int TK, int FI, int FJ, int WT_CO, int WT_K>
 EE_DEV void wgrad_epilogue_staged(const WgradArgs& w, const f32x4_t (&acc)[FI][FJ], int co0, int kb0, int wi,
-                                  int wj, int lane, int tid, float* st) {
+                                  int wj, int lane, int tid, float* st, int split) {
   static_assert(TK % 16 == 0 && TCO % 16 == 0, "tile");
   const int g = lane >> 4, li = lane & 15;
   constexpr int CM = TK / 16 - 1;   // XOR masks stay inside the row's TK / 4 chunks
@@ -1313,7 +1315,7 @@ EE_DEV void wgrad_epilogue_staged(const WgradArgs& w, const f32x4_t (&acc)[FI][F
     const int co = co0 + row, kk = kb0 + k;
     if (co >= w.Cout || kk >= w.K) continue;
     if (!w.dw) {   // split: this split's row-major slab [Cout][K] (K % 4 == 0, 16-B aligned)
-      *reinterpret_cast<f32x4_t*>(w.ws + ((long)blockIdx.z * w.Cout + co) * w.K + kk) =
+      *reinterpret_cast<f32x4_t*>(w.ws + ((long)split * w.Cout + co) * w.K + kk) =
           *reinterpret_cast<const f32x4_t*>(st + phys(row, k));
       continue;
     }
@@ -1633,8 +1635,24 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fast_kernel(WgradArgs w, lo
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wi = wave / WKK, wj = wave % WKK;
-  const int co0 = blockIdx.y * TCO, kb0 = blockIdx.x * TK;
-  const int p_begin = blockIdx.z * w.p_per_split;
+  // logical tile: with xcd_remap the linear block id's XCD (id % 8) owns a
+  // contiguous run of logical tiles, k tiles fastest, so every k tile of one
+  // (co tile, split) -- which all read the same pixels of x and dy -- shares
+  // one XCD's L2 (round-robin dispatch spread them over the 8 XCDs: each XCD
+  // re-fetched the same rows from HBM)
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (w.xcd_remap) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int total = gx * gy * gridDim.z;
+    const int lin = bx + gx * (by + gy * bz);
+    const int logical = (lin & 7) * (total >> 3) + (lin >> 3);
+    bx = logical % gx;
+    const int t = logical / gx;
+    by = t % gy;
+    bz = t / gy;
+  }
+  const int co0 = by * TCO, kb0 = bx * TK;
+  const int p_begin = bz * w.p_per_split;
   const int p_end = min(w.P, p_begin + w.p_per_split);
   const int nk = p_begin < p_end ? (p_end - p_begin + BK - 1) / BK : 0;
   const bool d_wave = D_TOT >= 256 || tid < D_TOT;
@@ -1805,10 +1823,10 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fast_kernel(WgradArgs w, lo
   static_assert(TCO * TK * 4 <= S * STAGE * 2, "staged dW tile exceeds the LDS ring");
   if (w.stage) {
     wgrad_epilogue_staged<TCO, TK, FI, FJ, WT_CO, WT_K>(w, acc, co0, kb0, wi, wj, lane, tid,
-                                                       reinterpret_cast<float*>(lds));
+                                                       reinterpret_cast<float*>(lds), bz);
     return;
   }
-  wgrad_epilogue<FI, FJ, WT_CO, WT_K>(w, acc, co0, kb0, wi, wj, lane);
+  wgrad_epilogue<FI, FJ, WT_CO, WT_K>(w, acc, co0, kb0, wi, wj, lane, bz);
 }
 
 // ------------------------------------------------------- weight packing --
@@ -2992,6 +3010,18 @@ static void wgrad_plan(const eegan_conv_desc* d, int& TCO, int& TK, int& nsplit,
   nsplit = std::min(want, maxsplit);
   pps = ee_round_up(ee_cdiv(P, nsplit), BK);
   nsplit = ee_cdiv(P, pps);
+  // many-split grids: a split count that makes the grid a multiple of 8, so the
+  // fast kernel can keep each split's k tiles on one XCD (WgradArgs::xcd_remap)
+  if (nsplit >= 8 && (tiles * nsplit) % 8 && env_int("EEGAN_WGRAD_SPLIT8", 1)) {
+    for (int ns = nsplit + 1; ns < nsplit + 16 && ns <= maxsplit; ++ns) {
+      const int pp = ee_round_up(ee_cdiv(P, ns), BK), n2 = ee_cdiv(P, pp);
+      if ((tiles * n2) % 8 == 0) {
+        pps = pp;
+        nsplit = n2;
+        break;
+      }
+    }
+  }
 }
 
 long eegan_conv_wgrad_workspace(const eegan_conv_desc* d) {
@@ -3056,6 +3086,10 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
     if (nsplit > 1 && !w.quad)
       w.stage = ((uintptr_t)ws & 15) == 0 && env_int("EEGAN_WGRAD_STAGE_EPI", 2) >= 2;
     dim3 grid(ee_cdiv(K, TK), ee_cdiv(d->K, TCO), nsplit);
+    // (measured ahead on the many-split shapes: 3x3 128-ch 64^2 51 -> 35 us, 4x4/s2 64->128 50 -> 32 us;
+    // behind on the few-split deep layers, profiles/r03_wgrad_xcd.txt)
+    w.xcd_remap = grid.x > 1 && grid.z >= 8 && ((long)grid.x * grid.y * grid.z) % 8 == 0 &&
+                  env_int("EEGAN_WGRAD_XCD", 1);
     const long x_bytes = wgrad_x_bytes(d), dy_bytes = wgrad_dy_bytes(d);
 #define WG(TC, TKK, WC) ee_launch(conv_wgrad_kernel<TC, TKK, WC>, grid, dim3(256), 0, stream, w)
 #define WL(TC, TKK) ee_launch(conv_wgrad_glds_kernel<TC, TKK>, grid, dim3(256), 0, stream, w, x_bytes, dy_bytes)

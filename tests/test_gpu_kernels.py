@@ -738,6 +738,28 @@ def test_wgrad_staged_epilogue_bit_identical(gpu, monkeypatch):
         assert rel_l2(outs[1][0], wr.grad) < 1e-4
 
 
+def test_wgrad_xcd_remap_bit_identical(gpu, monkeypatch):
+    """Weight-gradient tiles remapped so one (co tile, split)'s k tiles share an
+    XCD (EEGAN_WGRAD_XCD=1, default) compute the same tiles: torch.equal with
+    the plain block order, split and unsplit, fresh and accumulated."""
+    Fn, T, _ = _mods()
+    for N, Cin, H, W, Cout, k, st, pad in [(16, 128, 32, 32, 128, 3, 1, 1), (8, 64, 64, 64, 64, 3, 1, 1),
+                                            (8, 64, 32, 32, 128, 4, 2, 1), (8, 768, 4, 4, 1024, 3, 1, 1)]:
+        torch.manual_seed(Cin + H + Cout)
+        g = Fn.Geom(Cout, k, k, st, pad, pad, 0)
+        x = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        Ho, Wo = g.out_hw(H, W)
+        dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
+        outs = []
+        for v in ('0', '1'):
+            monkeypatch.setenv('EEGAN_WGRAD_XCD', v)
+            dW = torch.full((Cout, Cin, k, k), 0.25, device=gpu).contiguous(memory_format=torch.channels_last)
+            Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, k, k), out=dW)
+            outs.append((Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, k, k)).cpu(), dW.cpu()))
+        for a_, b_ in zip(*outs):
+            assert torch.equal(a_, b_), (N, Cin, H, Cout, k)
+
+
 def test_wgrad_quad_slab_bit_identical(gpu, monkeypatch):
     """Split weight gradients written as co-quad slabs (EEGAN_WGRAD_QUAD=1,
     default: one 16-B store per lane) reduce to the same bits as the row-major
