@@ -16,6 +16,23 @@ namespace {
 
 __global__ void adam_tick_kernel(double* step) { *step += 1.0; }
 
+template <bool B1ZERO>
+__device__ __forceinline__ void adam_elem(float& P, float G, float& M, float& V, float b1, float b2, float wd,
+                                          float step_size, float bc2_sqrt, float eps) {
+  const float gr = G + wd * P;
+  // torch: exp_avg.lerp_(g, 1 - b1); at b1 = 0 (train.py:252-263's betas) the
+  // lerp with weight 1 is g - (g - m) * 0 = g exactly for any finite m, so
+  // the old moment is not read
+  if (B1ZERO)
+    M = gr;
+  else
+    M = (1.f - b1) >= 0.5f ? gr - (gr - M) * b1 : M + (1.f - b1) * (gr - M);
+  V = V * b2 + (1.f - b2) * gr * gr;
+  const float denom = sqrtf(V) / bc2_sqrt + eps;
+  P = P + (-step_size) * (M / denom);
+}
+
+template <bool B1ZERO>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long n, float b1,
                                                    float b2, float lr, float eps, float wd,
@@ -26,34 +43,59 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   const float step_size = (float)((double)lr / (1.0 - pow((double)b1, t)));
   const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, t));
   const long n4 = n / 4;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n4; e += (long)gridDim.x * blockDim.x) {
-    float4 pp = reinterpret_cast<float4*>(p)[e];
-    const float4 gg = reinterpret_cast<const float4*>(g)[e];
-    float4 mm = reinterpret_cast<float4*>(m)[e];
-    float4 vv = reinterpret_cast<float4*>(v)[e];
-    float* P = &pp.x;
-    const float* G = &gg.x;
-    float* Mv = &mm.x;
-    float* V = &vv.x;
+  const long stride = (long)gridDim.x * blockDim.x;
+  float4* P4 = reinterpret_cast<float4*>(p);
+  const float4* G4 = reinterpret_cast<const float4*>(g);
+  float4* M4 = reinterpret_cast<float4*>(m);
+  float4* V4 = reinterpret_cast<float4*>(v);
+  long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  // two float4 groups per iteration: every load of both issued before the
+  // arithmetic (more bytes in flight per wave)
+  for (; e + stride < n4; e += 2 * stride) {
+    float4 pp[2], gg[2], mm[2], vv[2];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float gr = G[j] + wd * P[j];
-      Mv[j] = (1.f - b1) >= 0.5f ? gr - (gr - Mv[j]) * b1 : Mv[j] + (1.f - b1) * (gr - Mv[j]);
-      V[j] = V[j] * b2 + (1.f - b2) * gr * gr;
-      const float denom = sqrtf(V[j]) / bc2_sqrt + eps;
-      P[j] = P[j] + (-step_size) * (Mv[j] / denom);
+    for (int u = 0; u < 2; ++u) {
+      pp[u] = P4[e + u * stride];
+      gg[u] = G4[e + u * stride];
+      if (!B1ZERO) mm[u] = M4[e + u * stride];
+      vv[u] = V4[e + u * stride];
     }
-    reinterpret_cast<float4*>(p)[e] = pp;
-    reinterpret_cast<float4*>(m)[e] = mm;
-    reinterpret_cast<float4*>(v)[e] = vv;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float* Pp = &pp[u].x;
+      const float* Gp = &gg[u].x;
+      float* Mp = &mm[u].x;
+      float* Vp = &vv[u].x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) adam_elem<B1ZERO>(Pp[j], Gp[j], Mp[j], Vp[j], b1, b2, wd, step_size, bc2_sqrt, eps);
+      P4[e + u * stride] = pp[u];
+      M4[e + u * stride] = mm[u];
+      V4[e + u * stride] = vv[u];
+    }
+  }
+  for (; e < n4; e += stride) {
+    float4 pp = P4[e];
+    const float4 gg = G4[e];
+    float4 mm;
+    if (!B1ZERO) mm = M4[e];
+    float4 vv = V4[e];
+    float* Pp = &pp.x;
+    const float* Gp = &gg.x;
+    float* Mp = &mm.x;
+    float* Vp = &vv.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) adam_elem<B1ZERO>(Pp[j], Gp[j], Mp[j], Vp[j], b1, b2, wd, step_size, bc2_sqrt, eps);
+    P4[e] = pp;
+    M4[e] = mm;
+    V4[e] = vv;
   }
   // tail
-  for (long e = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
-    float gr = g[e] + wd * p[e];
-    m[e] = (1.f - b1) >= 0.5f ? gr - (gr - m[e]) * b1 : m[e] + (1.f - b1) * (gr - m[e]);
-    v[e] = v[e] * b2 + (1.f - b2) * gr * gr;
-    const float denom = sqrtf(v[e]) / bc2_sqrt + eps;
-    p[e] = p[e] + (-step_size) * (m[e] / denom);
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    float pv = p[i], mv = m[i], vv = v[i];
+    adam_elem<false>(pv, g[i], mv, vv, b1, b2, wd, step_size, bc2_sqrt, eps);
+    p[i] = pv;
+    m[i] = mv;
+    v[i] = vv;
   }
 }
 
@@ -72,7 +114,10 @@ int eegan_adam(float* p, const float* g, float* m, float* v, long n, float beta1
   adam_tick_kernel<<<1, 1, 0, s>>>(step);
   int rc = ee_check_launch("adam_tick");
   if (rc) return rc;
-  adam_kernel<<<blocks, 256, 0, s>>>(p, g, m, v, n, beta1, beta2, lr, eps, weight_decay, step);
+  if (beta1 == 0.f)
+    adam_kernel<true><<<blocks, 256, 0, s>>>(p, g, m, v, n, beta1, beta2, lr, eps, weight_decay, step);
+  else
+    adam_kernel<false><<<blocks, 256, 0, s>>>(p, g, m, v, n, beta1, beta2, lr, eps, weight_decay, step);
   return ee_check_launch("adam");
 }
 

@@ -9,6 +9,7 @@ and nothing in the step reads device memory on the host (no .item(), no
 cap_lens.tolist()).  Scalar loss combinations stay torch expressions on
 0-d tensors.
 """
+import collections
 import contextlib
 import os
 import sys
@@ -45,6 +46,12 @@ G_EARLY = os.environ.get('EEGAN_G_EARLY', '1') != '0'
 DAMSM_EARLY = os.environ.get('EEGAN_DAMSM_EARLY', '1') != '0'
 # EEGAN_DAMSM_GRAD_EARLY=0: the DAMSM branch's backward waits for g_update's backward (A/B switch).
 DAMSM_GRAD_EARLY = os.environ.get('EEGAN_DAMSM_GRAD_EARLY', '1') != '0'
+# EEGAN_GTERM_GRAD_EARLY=n: g_update's term through D i (i < n; n = -1: every D) is
+# differentiated w.r.t. its fake image on D i's lane right after the term's
+# forward (g_loss is linear in the per-D terms, train.py:477-493), so the
+# smaller D's input-gradient passes run while the largest D's update still
+# holds the critical lane instead of beside g_update's backward; 0 = off (A/B switch).
+GTERM_GRAD_EARLY = int(os.environ.get('EEGAN_GTERM_GRAD_EARLY', '-1'))   # -1: +1.9 % (profiles/r03_gterm_early.txt)
 # the discriminator lanes are issued largest (critical) first and the DAMSM lane after them: the
 # first packets of the critical lane then do not queue behind the others' (C2: 678 vs 656 img/s,
 # tools/gpu_env_ab.sh); EEGAN_LANE_ORDER=fwd: D64, D128, D256 after the DAMSM lane
@@ -75,6 +82,29 @@ TEXT_AHEAD = os.environ.get('EEGAN_TEXT_AHEAD', '0') == '1'   # measured -0.6 % 
 # runs beside the generator's stages 2-3 -- a stretch where the generator's
 # small launches leave most of the GPU idle -- instead of beside D256's update.
 EARLY_D0 = os.environ.get('EEGAN_EARLY_D0', '0') == '1'   # measured: G's forward slows by ~1 ms beside it, neutral to -0.7 % (profiles/r03_early_d0.txt)
+
+
+# a g_update term already differentiated w.r.t. its fake image on its lane
+# (GTERM_GRAD_EARLY): its value, the image alias and the gradient there
+EarlyTerm = collections.namedtuple('EarlyTerm', 'value alias grad')
+
+
+def _backward_roots(terms):
+    """(roots, grads) for g_update's backward from per-D terms: a plain term
+    is a root with gradient 1, an EarlyTerm enters at its image alias."""
+    roots, grads = [], []
+    for t in terms:
+        if isinstance(t, EarlyTerm):
+            roots.append(t.alias)
+            grads.append(t.grad)
+        else:
+            roots.append(t)
+            grads.append(None)
+    return roots, grads
+
+
+def _term_value(t):
+    return t.value if isinstance(t, EarlyTerm) else t
 
 
 class Trainer(object):
@@ -403,6 +433,12 @@ class Trainer(object):
         """The generator's adversarial term through D i (train.py:477-489)."""
         fake_img, netD = fake_imgs[i], self.netsD[i]
         Fn.stamp('gD%d start' % i)
+        n_early = GTERM_GRAD_EARLY if GTERM_GRAD_EARLY >= 0 else len(self.netsD)
+        grad_early = i < n_early and fake_img.requires_grad and torch.is_grad_enabled()
+        if grad_early:
+            # an alias whose autograd node lives on this lane (as in damsm_early):
+            # autograd.grad stops at it, g_update's backward enters through it
+            fake_img = fake_img.view_as(fake_img)
         if self.disc_class and i == 2:
             errG, errG_class = self.g_loss_class(fake_img, sent_emb, class_labels, netD)
             term = errG + errG_class * self.g_class_coe
@@ -414,6 +450,10 @@ class Trainer(object):
             self.records['errG/G_%d_fake_sent' % i] = errG.detach()
             if self.disc_class and i == 2:
                 self.records['errG/G_%d_fake_class' % i] = errG_class.detach()
+        if grad_early:
+            (dfake,) = torch.autograd.grad(term, fake_img)
+            Fn.stamp('gD%d input grad' % i)
+            return EarlyTerm(term.detach(), fake_img, dfake)
         return term
 
     def g_update(self, fake_imgs, sent_emb, words_emb, attr_emb, class_ids, batch_size, match_labels, cap_lens,
@@ -441,9 +481,9 @@ class Trainer(object):
         dfake = damsm[3] if len(damsm) > 3 else None
         self._join(streams)
         Fn.stamp('g_update forwards joined')
-        g_loss = terms[0]
+        g_loss = _term_value(terms[0])
         for t in terms[1:]:
-            g_loss = g_loss + t
+            g_loss = g_loss + _term_value(t)
         g_adv = g_loss
         g_loss = g_loss + self.DAMSM_coe * (s_loss + w_loss + a_loss)
         if iter_rec:
@@ -459,7 +499,17 @@ class Trainer(object):
         # zeroes those before every use (train.py:451,457), and the GP's
         # interpolated-image gradient is never read -- skipping them changes no
         # parameter and saves the D weight-gradient passes
-        if dfake is not None:
+        if any(isinstance(t, EarlyTerm) for t in terms):
+            # per-D terms differentiated on their lanes enter at their image aliases
+            roots, grads = _backward_roots(terms)
+            if dfake is not None:
+                roots.append(dfake[0])
+                grads.append(dfake[1])
+            else:
+                roots.append(self.DAMSM_coe * (s_loss + w_loss + a_loss))
+                grads.append(None)
+            torch.autograd.backward(roots, grads, inputs=self.optimizerG.params)
+        elif dfake is not None:
             # the DAMSM terms' share, computed by damsm_early, enters at (its alias of) the 256-px image
             torch.autograd.backward([g_adv, dfake[0]], [None, dfake[1]], inputs=self.optimizerG.params)
         else:
@@ -490,12 +540,13 @@ class Trainer(object):
             for i, f in enumerate(fake_imgs):
                 f.register_hook(lambda g, i=i: (Fn.stamp('dfake%d ready' % i), g)[1])
         self.optimizerG.zero_grad()
-        torch.autograd.backward(list(terms) + [alias], [None] * nD + [dfake], inputs=self.optimizerG.params)
+        roots, grads = _backward_roots(terms)
+        torch.autograd.backward(roots + [alias], grads + [dfake], inputs=self.optimizerG.params)
         Fn.stamp('G backward (D, DAMSM, G)')
         self._join(streams)
-        g_loss = terms[0].detach()
+        g_loss = _term_value(terms[0]).detach()
         for t in terms[1:]:
-            g_loss = g_loss + t.detach()
+            g_loss = g_loss + _term_value(t).detach()
         g_loss = g_loss + self.DAMSM_coe * (s_loss + w_loss + a_loss)
         self.optimizerG.step()
         Fn.stamp('G adam')

@@ -905,14 +905,17 @@ def test_class_onehot_bit_exact(gpu):
     assert err.item() == 0
 
 
-def test_adam_matches_torch(gpu):
+@pytest.mark.parametrize('beta1', [0.0, 0.5])
+def test_adam_matches_torch(gpu, beta1):
+    """beta1 = 0 (train.py's betas) takes the kernel form that does not read
+    the old first moment; 0.5 the general lerp."""
     from eegan_hip.optim import FlatAdam
     torch.manual_seed(13)
     # (1000, 3001): several grid-stride groups per thread and a ragged float4 tail
     ps = [torch.nn.Parameter(torch.randn(s, device=gpu)) for s in [(7, 3), (5,), (1,), (33, 2, 3), (1000, 3001)]]
     qs = [torch.nn.Parameter(p.detach().clone()) for p in ps]
-    opt = FlatAdam(ps, lr=4e-4, betas=(0.0, 0.9))
-    ref = torch.optim.Adam(qs, lr=4e-4, betas=(0.0, 0.9))
+    opt = FlatAdam(ps, lr=4e-4, betas=(beta1, 0.9))
+    ref = torch.optim.Adam(qs, lr=4e-4, betas=(beta1, 0.9))
     for it in range(3):
         gs = [torch.randn(p.shape, device=gpu) for p in ps]
         opt.zero_grad()

@@ -47,6 +47,19 @@ SHAPES = {
     'c3x3_128_100_64': (16, 128, 64, 64, 100, 3, 1, 1),
     'c3x3_64_32_128': (16, 64, 128, 128, 32, 3, 1, 1),
     'c3x3_32_16_256': (16, 32, 256, 256, 16, 3, 1, 1),
+    # Dis256 at N = 32 (real + fake batched), models.py resD blocks 0-5
+    'd256_b0_s2': (32, 32, 256, 256, 64, 4, 2, 1),
+    'd256_b0_3x3': (32, 64, 128, 128, 64, 3, 1, 1),
+    'd256_b1_s2': (32, 64, 128, 128, 128, 4, 2, 1),
+    'd256_b1_3x3': (32, 128, 64, 64, 128, 3, 1, 1),
+    'd256_b2_s2': (32, 128, 64, 64, 256, 4, 2, 1),
+    'd256_b2_3x3': (32, 256, 32, 32, 256, 3, 1, 1),
+    'd256_b3_s2': (32, 256, 32, 32, 512, 4, 2, 1),
+    'd256_b3_3x3': (32, 512, 16, 16, 512, 3, 1, 1),
+    'd256_b4_s2': (32, 512, 16, 16, 512, 4, 2, 1),
+    'd256_b4_3x3': (32, 512, 8, 8, 512, 3, 1, 1),
+    'd256_b5_s2': (32, 512, 8, 8, 512, 4, 2, 1),
+    'd256_b5_3x3': (32, 512, 4, 4, 512, 3, 1, 1),
 }
 
 
