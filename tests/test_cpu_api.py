@@ -133,3 +133,37 @@ def test_sync_master_rendezvous():
         assert mine == (total, rnd)
         assert got == {i: (total, 10 * i + rnd) for i in (1, 2, 3)}
     assert master.nr_slaves == 3
+
+
+def test_early_term_roots_match_joint_backward():
+    """g_update's backward from per-D terms already differentiated at their
+    (aliased) fake images (trainer.EarlyTerm, EEGAN_GTERM_GRAD_EARLY) gives the
+    generator the same gradients as backward of the summed loss (train.py:
+    477-493: g_loss is linear in the terms)."""
+    from eegan_hip.trainer import EarlyTerm, _backward_roots, _term_value
+    torch.manual_seed(0)
+    w = torch.nn.Parameter(torch.randn(4, 4, dtype=torch.float64))
+    z = torch.randn(3, 4, dtype=torch.float64)
+    d = [torch.randn(4, 4, dtype=torch.float64) for _ in range(2)]
+
+    def fakes():
+        h = torch.tanh(z @ w)
+        return [h, torch.sin(h @ w)]            # two "stages" sharing w
+
+    def term(i, img):
+        return (torch.tanh(img @ d[i]) ** 2).sum()
+
+    f = fakes()
+    (ref,) = torch.autograd.grad(term(0, f[0]) + term(1, f[1]), w)
+    f = fakes()
+    terms = []
+    for i in range(2):
+        alias = f[i].view_as(f[i])
+        t = term(i, alias)
+        (g,) = torch.autograd.grad(t, alias)
+        terms.append(EarlyTerm(t.detach(), alias, g))
+    roots, grads = _backward_roots(terms)
+    (got,) = torch.autograd.grad(roots, w, grads)
+    assert torch.allclose(got, ref, rtol=1e-12, atol=1e-12)
+    assert float(_term_value(terms[0]) + _term_value(terms[1])) == pytest.approx(
+        float(term(0, f[0]) + term(1, f[1])))
