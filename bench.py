@@ -29,6 +29,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, 'ee-gan_amd'))
 sys.path.insert(0, REPO)
 
+# bench.py sets each rank's device and starts the process group itself
+# (eegan_hip.dist.init_from_env): no import-time pinning (eegan_hip.launch)
+os.environ.setdefault('EEGAN_AUTO_DIST', '0')
+
 import torch  # noqa: E402
 
 CONFIGS = {

@@ -42,9 +42,142 @@ __global__ __launch_bounds__(256) void fid_preprocess_kernel(const float* __rest
     const float* p = x + ((long)n * 3 + c) * H * W;
     const float v = hy * (hx * p[(long)y0 * W + x0] + lx * p[(long)y0 * W + x1]) +
                     ly * (hx * p[(long)y1 * W + x0] + lx * p[(long)y1 * W + x1]);
-    o[c] = f2bf(v * sc[c] + sh[c]);
+    o[c] = f2bf(__builtin_fmaf(v, sc[c], sh[c]));
   }
   for (int c = 3; c < ldy; ++c) o[c] = 0;
+}
+
+// ---- generator samples -> Inception input (test.py:244-304 + fid_score.py:98-128)
+// The reference saves every generated 256 px image with
+// vutils.save_image(img, normalize=True, scale_each=True) (miscc/utils.py:11-15):
+// per image x <- (clamp(x, lo, hi) - lo) * (1 / max(hi - lo, 1e-5)) with lo / hi
+// the image's min / max (torchvision norm_ip, on the GPU tensor: torch's CUDA
+// division by a scalar multiplies by its fp32 reciprocal), then
+// uint8(clamp(x * 255 + 0.5, 0, 255)); fid_score.py reads the files back
+// through PIL, Resize((299, 299)) (PIL bilinear, uint8 out) and ToTensor, and
+// InceptionV3 resizes 299 -> 299 (identity) and renormalises.  Here the same
+// arithmetic runs on the device without the JPEG file in between: min / max per
+// image, then PIL's two fixed-point passes (host-computed 22-bit weights, the
+// input pipeline's kernels' arithmetic) on the quantised pixels, written as the
+// NHWC bf16 Inception input.
+
+// per-image min / max over the 3 channels of the NHWC bf16 image (ld channels per pixel)
+__global__ __launch_bounds__(1024) void fid_minmax_kernel(const uint16_t* __restrict__ img, int HW, int ld,
+                                                          float* __restrict__ mm) {
+  __shared__ float slo[16], shi[16];
+  const uint16_t* p = img + (long)blockIdx.x * HW * ld;
+  float lo = __builtin_huge_valf(), hi = -__builtin_huge_valf();
+  for (int i = threadIdx.x; i < HW; i += 1024) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float v = bf2f(p[(long)i * ld + c]);
+      lo = fminf(lo, v);
+      hi = fmaxf(hi, v);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fminf(lo, __shfl_xor(lo, o));
+    hi = fmaxf(hi, __shfl_xor(hi, o));
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) slo[w] = lo, shi[w] = hi;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < 16; ++k) lo = fminf(lo, slo[k]), hi = fmaxf(hi, shi[k]);
+    lo = fminf(lo, slo[0]);
+    hi = fmaxf(hi, shi[0]);
+    mm[2 * blockIdx.x] = lo;
+    mm[2 * blockIdx.x + 1] = hi;
+  }
+}
+
+// save_image's uint8 of one value (separate fp32 roundings, as torch's elementwise kernels)
+#pragma clang fp contract(off)
+EE_DEV int fid_q8(float v, float lo, float hi, float inv) {
+  v = fminf(fmaxf(v, lo), hi);
+  v = (v - lo) * inv;
+  v = v * 255.f + 0.5f;
+  v = fminf(fmaxf(v, 0.f), 255.f);
+  return (int)v;   // .to(torch.uint8): truncation
+}
+#pragma clang fp contract(on)
+
+constexpr int FID_PB = 22;  // PIL's PRECISION_BITS
+
+EE_DEV uint8_t fid_clip8(int v) {
+  if (v >= (1 << FID_PB << 8)) return 255;
+  if (v <= 0) return 0;
+  return (uint8_t)(v >> FID_PB);
+}
+
+EE_DEV float fid_inv(float lo, float hi) {
+  const float d = (float)fmax((double)hi - (double)lo, 1e-5);   // python floats, then fp32
+  return 1.f / d;
+}
+
+// horizontal PIL pass: quantised image rows (H x W) -> tmp [N][H][Wo][3] uint8
+__global__ __launch_bounds__(256) void fid_samples_hpass_kernel(const uint16_t* __restrict__ img, int H, int W, int ld,
+                                                                const float* __restrict__ mm, int Wo,
+                                                                const int* __restrict__ coef,
+                                                                const int* __restrict__ bounds, int ksize,
+                                                                uint8_t* __restrict__ tmp) {
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  if (pix >= H * Wo) return;
+  const int n = blockIdx.y;
+  const int y = pix / Wo, x = pix - y * Wo;
+  const float lo = mm[2 * n], hi = mm[2 * n + 1], inv = fid_inv(lo, hi);
+  const int xmin = bounds[2 * x], xn = bounds[2 * x + 1];
+  const int* k = coef + x * ksize;
+  const uint16_t* row = img + ((long)n * H + y) * W * ld + (long)xmin * ld;
+  int s0 = 1 << (FID_PB - 1), s1 = s0, s2 = s0;
+  for (int t = 0; t < xn; ++t) {
+    const int w = k[t];
+    const uint16_t* q = row + (long)t * ld;
+    s0 += fid_q8(bf2f(q[0]), lo, hi, inv) * w;
+    s1 += fid_q8(bf2f(q[1]), lo, hi, inv) * w;
+    s2 += fid_q8(bf2f(q[2]), lo, hi, inv) * w;
+  }
+  uint8_t* o = tmp + (((long)n * H + y) * Wo + x) * 3;
+  o[0] = fid_clip8(s0);
+  o[1] = fid_clip8(s1);
+  o[2] = fid_clip8(s2);
+}
+
+// vertical PIL pass -> uint8 -> ToTensor (/ 255) -> x * scale + shift -> NHWC bf16 (optional uint8 copy)
+__global__ __launch_bounds__(256) void fid_samples_vpass_kernel(const uint8_t* __restrict__ tmp, int H, int Ho, int Wo,
+                                                                const int* __restrict__ coef,
+                                                                const int* __restrict__ bounds, int ksize, float s0_,
+                                                                float s1_, float s2_, float b0, float b1, float b2,
+                                                                uint16_t* __restrict__ y, int ldy,
+                                                                uint8_t* __restrict__ u8) {
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  if (pix >= Ho * Wo) return;
+  const int n = blockIdx.y;
+  const int oy = pix / Wo, x = pix - oy * Wo;
+  const int ymin = bounds[2 * oy], yn = bounds[2 * oy + 1];
+  const int* k = coef + oy * ksize;
+  const uint8_t* col = tmp + (((long)n * H + ymin) * Wo + x) * 3;
+  const long rs = 3L * Wo;
+  int a0 = 1 << (FID_PB - 1), a1 = a0, a2 = a0;
+  for (int t = 0; t < yn; ++t) {
+    const int w = k[t];
+    a0 += (int)col[t * rs] * w;
+    a1 += (int)col[t * rs + 1] * w;
+    a2 += (int)col[t * rs + 2] * w;
+  }
+  const uint8_t v[3] = {fid_clip8(a0), fid_clip8(a1), fid_clip8(a2)};
+  const float sc[3] = {s0_, s1_, s2_}, sh[3] = {b0, b1, b2};
+  const long p = ((long)n * Ho + oy) * Wo + x;
+  uint16_t* o = y + p * ldy;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) o[c] = f2bf(__builtin_fmaf((float)v[c] / 255.0f, sc[c], sh[c]));
+  for (int c = 3; c < ldy; ++c) o[c] = 0;
+  if (u8) {
+    u8[3 * p] = v[0];
+    u8[3 * p + 1] = v[1];
+    u8[3 * p + 2] = v[2];
+  }
 }
 
 // mu[d] = (sum_n x[n][d]) / N, rows in order
@@ -121,6 +254,31 @@ int eegan_fid_preprocess(const float* x, int N, int H, int W, int Ho, int Wo, co
   ee_launch(fid_preprocess_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, N, H, W, Ho, Wo, scale3[0],
             scale3[1], scale3[2], shift3[0], shift3[1], shift3[2], y, ldy);
   return ee_check_launch("fid_preprocess");
+}
+
+long eegan_fid_samples_workspace(int N, int H, int Wo) { return 2L * N * 4 + ((long)N * H * Wo * 3 + 15) / 16 * 16; }
+
+int eegan_fid_samples(const uint16_t* img, int N, int H, int W, int ld, int Ho, int Wo, const int* hcoef,
+                      const int* hbounds, int hksize, const int* vcoef, const int* vbounds, int vksize,
+                      const float* scale3, const float* shift3, uint16_t* y, int ldy, uint8_t* u8_out, void* ws,
+                      hipStream_t s) {
+  if (N < 1 || H < 1 || W < 1 || Ho < 1 || Wo < 1 || ld < 3 || ldy < 3 || hksize < 1 || vksize < 1) {
+    ee_set_error("fid_samples: bad sizes");
+    return -22;
+  }
+  float* mm = (float*)ws;
+  uint8_t* tmp = (uint8_t*)ws + 2L * N * 4;
+  ee_launch(fid_minmax_kernel, dim3(N), dim3(1024), 0, s, img, H * W, ld, mm);
+  int rc = ee_check_launch("fid_minmax");
+  if (rc) return rc;
+  ee_launch(fid_samples_hpass_kernel, dim3((H * Wo + 255) / 256, N), dim3(256), 0, s, img, H, W, ld,
+            (const float*)mm, Wo, hcoef, hbounds, hksize, tmp);
+  rc = ee_check_launch("fid_samples_hpass");
+  if (rc) return rc;
+  ee_launch(fid_samples_vpass_kernel, dim3((Ho * Wo + 255) / 256, N), dim3(256), 0, s, (const uint8_t*)tmp, H, Ho,
+            Wo, vcoef, vbounds, vksize, scale3[0], scale3[1], scale3[2], shift3[0], shift3[1], shift3[2], y, ldy,
+            u8_out);
+  return ee_check_launch("fid_samples_vpass");
 }
 
 long eegan_fid_stats_workspace(int D) {

@@ -244,6 +244,61 @@ class TextDataset(data.Dataset):
         return self.iterator(index)
 
 
+class TextOnlyDataset(data.Dataset):
+    """datasets.py:448-535, the sampling side's dataset (test.py:21, 122-128):
+    captions (and attribute phrases) only, traversed per image (one random
+    caption of each) or per sentence (`regard_sent`).  The reference calls
+    TextDataset.load_class_id(data_dir, len(filenames)) without the split
+    (datasets.py:465, a TypeError against its own signature at :287); here the
+    split's class_info.pickle is loaded as the training set's is."""
+
+    def __init__(self, data_dir, split='test', regard_sent=False, attr_name='EE-GAN'):
+        self.embeddings_num = cfg.TEXT.CAPTIONS_PER_IMAGE
+        self.split_name = split
+        self.data_dir = data_dir
+        self.regard_sent = regard_sent
+        self.filenames = TextDataset.load_filenames(data_dir, split)
+        self.captions, self.ixtoword, self.wordtoix, self.n_words = TextDataset.load_captions(data_dir, split)
+        self.class_id = TextDataset.load_class_id(data_dir, split, len(self.filenames))
+        self.get_caption = TextDataset.get_caption
+        self.get_attributes = TextDataset.get_attributes
+        if regard_sent:
+            self.iterator = self.sent_regard_iter
+            self.img_sum = self.__len__() // self.embeddings_num
+        else:
+            self.iterator = self.image_regard_iter
+            self.img_sum = self.__len__()
+        self.use_attr = cfg.TRAIN.USE_ATTR
+        if self.use_attr:
+            self.attributes = TextDataset.load_attributes(data_dir, attr_name, split)
+
+    def image_regard_iter(self, img_ix):
+        """datasets.py:482-488: a random caption of image img_ix."""
+        caps, cap_len, sent_ix, _ = self.get_cap_one(img_ix)
+        rev_attrs = self.get_attributes(sent_ix, self.attributes) if self.use_attr else []
+        return [caps, cap_len, self.class_id[img_ix], self.filenames[img_ix]], rev_attrs
+
+    def sent_regard_iter(self, sent_ix):
+        """datasets.py:490-498."""
+        caps, cap_len = self.get_caption(sent_ix, self.captions)
+        img_ix = sent_ix // self.embeddings_num
+        rev_attrs = self.get_attributes(sent_ix, self.attributes) if self.use_attr else []
+        return [caps, cap_len, self.class_id[img_ix], self.filenames[img_ix]], rev_attrs
+
+    def get_cap_one(self, img_index):
+        """datasets.py:500-505 (numpy randint: high exclusive)."""
+        sub_sent_ix = random.randint(0, self.embeddings_num)
+        sent_ix = img_index * self.embeddings_num + sub_sent_ix
+        caps, cap_len = self.get_caption(sent_ix, self.captions)
+        return caps, cap_len, sent_ix, sub_sent_ix
+
+    def __getitem__(self, index):
+        return self.iterator(index)
+
+    def __len__(self):
+        return len(self.captions) if self.regard_sent else len(self.filenames)
+
+
 def _collate(samples):
     """default_collate for everything but the images (kept as HostImage lists)."""
     from torch.utils.data import default_collate

@@ -133,6 +133,8 @@ _SIGS = {
     'eegan_embedding': ([P, L, P, I, P, P], I),
     'eegan_lstm_bidir': ([P, P, P, I, I, I, I, P, P, P], I),
     'eegan_fid_preprocess': ([P, I, I, I, I, I, P, P, P, I, P], I),
+    'eegan_fid_samples_workspace': ([I, I, I], L),
+    'eegan_fid_samples': ([P, I, I, I, I, I, I, P, P, I, P, P, I, P, P, P, I, P, P, P], I),
     'eegan_fid_stats_workspace': ([I], L),
     'eegan_fid_stats': ([P, I, I, P, P, P, P], I),
     'eegan_peer_region_bytes': ([I], L),
@@ -161,7 +163,7 @@ def _load():
 
 LIB = _load()
 ABI_VERSION = LIB.eegan_abi_version()
-EXPECTED_ABI = 9
+EXPECTED_ABI = 10
 if ABI_VERSION != EXPECTED_ABI:
     raise ImportError('%s has ABI %d, these bindings need %d: rebuild (make -C ee-gan_amd/csrc)'
                       % (LIB_PATH, ABI_VERSION, EXPECTED_ABI))

@@ -67,6 +67,11 @@ def init_from_env(backend=None):
     """Initialise from torchrun's env (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT)."""
     ws = int(os.environ.get('WORLD_SIZE', '1'))
     if (ws <= 1 and not FORCE) or is_on():
+        if is_on() and dist.get_backend() == 'nccl' and not COMMS and \
+                os.environ.get('EEGAN_OWN_RCCL', '1') == '1':
+            # a group started at import (eegan_hip.launch) or by the caller
+            from .rccl import Communicator
+            COMMS[:] = [Communicator(torch.cuda.current_device()) for _ in range(N_LANES)]
         install_syncbn_hook()
         return rank(), world_size()
     if backend is None:
@@ -258,6 +263,9 @@ def ensure_grad_hooks(module):
     """Install GradHooks on `module` once, when the step is data-parallel
     (called from the drop-in models' forward, so reference code that wraps D
     and ATTR_Enhance in torch's own nn.DataParallel gets them too)."""
+    if getattr(module, '_eegan_grad_hooks', None) is None:
+        from .launch import check_process_group
+        check_process_group()   # torchrun ranks without a process group: refuse to train alone
     if getattr(module, '_eegan_grad_hooks', None) is None and collective():
         if any(p.requires_grad and not p.is_leaf for p in module.parameters()):
             # torch's nn.DataParallel replicated the module over several visible

@@ -412,21 +412,28 @@ class Trainer(object):
             Fn.stamp('DAMSM start')
             img = fake_imgs[-1]
             grad_early = DAMSM_GRAD_EARLY and img.requires_grad
+            attr = attr_emb
             if grad_early:
-                # an alias whose autograd node lives on this lane: autograd.grad stops at
-                # it, so the gradient it captures makes no stream of the generator's
+                # aliases whose autograd nodes live on this lane: autograd.grad stops at
+                # them, so the gradients they capture make no stream of the generator's
                 # (main) wait for this lane -- only g_update's backward, through the
-                # alias, joins them
+                # aliases, joins them
                 img = img.view_as(img)
-            w, s, a = self.DAMSM_loss(img, sent_emb, words_emb, attr_emb, class_ids, batch_size,
+                if attr_emb is not None and attr_emb.requires_grad:
+                    # a_loss = sent_loss(cnn_code, attrs_emb) (train.py:432) with attrs_emb
+                    # the trainable ATTR_Enhance's output (train.py:193-194): g_loss.backward()
+                    # trains ATTR_Enhance through it too, so its gradient is captured here
+                    attr = attr_emb.view_as(attr_emb)
+            w, s, a = self.DAMSM_loss(img, sent_emb, words_emb, attr, class_ids, batch_size,
                                       match_labels, cap_lens, self.image_encoder)
             Fn.stamp('DAMSM forward')
             dfake = None
             if grad_early:
-                (dfake,) = torch.autograd.grad(self.DAMSM_coe * (s + w + a), img)
+                leaves = (img, attr) if attr is not attr_emb else (img,)
+                grads = torch.autograd.grad(self.DAMSM_coe * (s + w + a), leaves)
                 w, s, a = w.detach(), s.detach(), a.detach()
                 Fn.stamp('DAMSM backward')
-                dfake = (img, dfake)
+                dfake = list(zip(leaves, grads))   # (alias, gradient there) pairs
         return w, s, a, dfake
 
     def _g_term(self, i, fake_imgs, sent_emb, class_labels, iter_rec):
@@ -503,15 +510,18 @@ class Trainer(object):
             # per-D terms differentiated on their lanes enter at their image aliases
             roots, grads = _backward_roots(terms)
             if dfake is not None:
-                roots.append(dfake[0])
-                grads.append(dfake[1])
+                for alias, g in dfake:
+                    roots.append(alias)
+                    grads.append(g)
             else:
                 roots.append(self.DAMSM_coe * (s_loss + w_loss + a_loss))
                 grads.append(None)
             torch.autograd.backward(roots, grads, inputs=self.optimizerG.params)
         elif dfake is not None:
-            # the DAMSM terms' share, computed by damsm_early, enters at (its alias of) the 256-px image
-            torch.autograd.backward([g_adv, dfake[0]], [None, dfake[1]], inputs=self.optimizerG.params)
+            # the DAMSM terms' share, computed by damsm_early, enters at its aliases of the
+            # 256-px image and of ATTR_Enhance's attribute embedding
+            torch.autograd.backward([g_adv] + [al for al, _ in dfake], [None] + [g for _, g in dfake],
+                                    inputs=self.optimizerG.params)
         else:
             g_loss.backward(inputs=self.optimizerG.params)
         Fn.stamp('G backward (D, DAMSM, G)')
@@ -528,7 +538,7 @@ class Trainer(object):
         fake images in another order."""
         nD = len(self.netsD)
         streams = self._side_streams(nD + 1, fork=False)
-        w_loss, s_loss, a_loss, (alias, dfake) = damsm
+        w_loss, s_loss, a_loss, dfake = damsm
         main = torch.cuda.current_stream()
         main.wait_stream(streams[nD])
         Fn.stamp('g_update DAMSM joined')
@@ -541,7 +551,8 @@ class Trainer(object):
                 f.register_hook(lambda g, i=i: (Fn.stamp('dfake%d ready' % i), g)[1])
         self.optimizerG.zero_grad()
         roots, grads = _backward_roots(terms)
-        torch.autograd.backward(roots + [alias], grads + [dfake], inputs=self.optimizerG.params)
+        torch.autograd.backward(roots + [al for al, _ in dfake], grads + [g for _, g in dfake],
+                                inputs=self.optimizerG.params)
         Fn.stamp('G backward (D, DAMSM, G)')
         self._join(streams)
         g_loss = _term_value(terms[0]).detach()

@@ -26,6 +26,21 @@ from eegan_hip.tensor import stream, workspace
 from .inception import InceptionV3
 
 
+def get_filenames(data_path):
+    """miscc/utils.py:76-86, what img_data.Dataset lists (img_data.py:17-20):
+    os.walk order (subfolders included, not sorted), every regular file whose
+    name contains 'jpg' or 'png' anywhere -- so the image set, its order and
+    the batches drop_last removes match the reference's."""
+    filenames = []
+    for path, _subdirs, files in os.walk(data_path):
+        for name in files:
+            if name.rfind('jpg') != -1 or name.rfind('png') != -1:
+                filename = os.path.join(path, name)
+                if os.path.isfile(filename):
+                    filenames.append(filename)
+    return filenames
+
+
 def _batches(images):
     for b in images:
         yield b[0] if isinstance(b, (list, tuple)) else b
@@ -45,6 +60,15 @@ class MeasureFID(object):
     def _features(model, batch, device):
         pred = model(batch.to(device))[0]
         if pred.shape[2] != 1 or pred.shape[3] != 1:   # fid_score.py:177-179
+            pred = torch.nn.functional.adaptive_avg_pool2d(pred, output_size=(1, 1))
+        return pred.reshape(pred.shape[0], -1)
+
+    @staticmethod
+    def _features_prepared(model, x):
+        """_features on an input already in Inception's NHWC bf16 layout
+        (metrics.FID.sampling.samples_to_inception_input)."""
+        pred = model.forward_prepared(x)[0]
+        if pred.shape[2] != 1 or pred.shape[3] != 1:
             pred = torch.nn.functional.adaptive_avg_pool2d(pred, output_size=(1, 1))
         return pred.reshape(pred.shape[0], -1)
 
@@ -89,8 +113,7 @@ class MeasureFID(object):
             with np.load(given_path) as f:
                 return f['mu'][:], f['sigma'][:]
         from PIL import Image
-        files = sorted(os.path.join(given_path, f) for f in os.listdir(given_path)
-                       if f.lower().endswith(('.jpg', '.jpeg', '.png')))
+        files = get_filenames(given_path)
 
         def batches():
             for i in range(0, len(files) - self.batch_size + 1, self.batch_size):   # drop_last=True

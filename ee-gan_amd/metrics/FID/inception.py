@@ -100,6 +100,12 @@ class InceptionV3(nn.Module):
             blocks.append(lambda x: Fn.GlobalAvgPoolFn.apply(self.Mixed_7c(self.Mixed_7b(self.Mixed_7a(x)))))
         return blocks
 
+    def input_affine(self):
+        """Per-channel (scale, shift) of the input re-normalisation (inception.py:135-138)."""
+        if self.normalize_input:
+            return [s / 0.5 for s in _STD], [(m - 0.5) / 0.5 for m in _MEAN]
+        return [1.0] * 3, [0.0] * 3
+
     def preprocess(self, inp):
         """inception.py:131-138: resize to 299 (bilinear, align_corners=True) and
         re-normalise to the ImageNet statistics, as one HIP pass -> NHWC bf16."""
@@ -108,11 +114,7 @@ class InceptionV3(nn.Module):
         if C != 3:
             raise ValueError('InceptionV3 expects 3-channel input')
         Ho, Wo = (299, 299) if self.resize_input else (H, W)
-        if self.normalize_input:
-            sc = [s / 0.5 for s in _STD]
-            sh = [(m - 0.5) / 0.5 for m in _MEAN]
-        else:
-            sc, sh = [1.0] * 3, [0.0] * 3
+        sc, sh = self.input_affine()
         y = empty_nhwc(N, 3, Ho, Wo, x.device)
         F3 = ctypes.c_float * 3
         ops.fid_preprocess(x.data_ptr(), N, H, W, Ho, Wo, F3(*sc), F3(*sh), y.data_ptr(), 8, stream())
@@ -120,8 +122,13 @@ class InceptionV3(nn.Module):
 
     @torch.no_grad()
     def forward(self, inp):
+        return self.forward_prepared(self.preprocess(inp))
+
+    @torch.no_grad()
+    def forward_prepared(self, x):
+        """The blocks on an input already resized / re-normalised into NHWC bf16
+        (preprocess, or metrics.FID.sampling's generator-sample path)."""
         outp = []
-        x = self.preprocess(inp)
         for idx, block in enumerate(self._blocks()):
             x = block(x)
             if idx in self.output_blocks:

@@ -27,13 +27,14 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 9  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
+#define EEGAN_ABI_VERSION 10  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
                                 4: rectangular (local x global) DAMSM words / sentence blocks on MFMA;
                                 5: GlobalAttentionGeneral (eegan_gag_*), words backward reuses the forward's prep;
                                 6: device input pipeline (eegan_pipe_*);
                                 7: GlobalAttentionGeneral for any source length (eegan_gag_fwd workspace);
                                 8: FID leg (eegan_fid_*);
-                                9: SyncBN peer-write all-reduce (eegan_peer_*) */
+                                9: SyncBN peer-write all-reduce (eegan_peer_*);
+                                10: FID generator-sample input (eegan_fid_samples) */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
@@ -344,6 +345,18 @@ int eegan_pipe_transform(const uint8_t* src, const eegan_img_job* jobs, int B, i
  * eegan_fid_stats_workspace bytes; synchronises the stream once (tile list upload). */
 int eegan_fid_preprocess(const float* x, int N, int H, int W, int Ho, int Wo, const float* scale3,
                          const float* shift3, uint16_t* y, int ldy, hipStream_t s);
+/* samples: the generator's 256 px images as fid_score.py sees them after test.py saved them
+ * (test.py:244-304, miscc/utils.py:11-15: vutils.save_image(normalize=True, scale_each=True) -> uint8 file ->
+ * PIL Resize((299, 299)) -> ToTensor, fid_score.py:106-113) and InceptionV3 renormalised them, without the file:
+ * img NHWC bf16 [N][H][W][ld] -> per-image min/max normalise, uint8 quantise, PIL bilinear H x W -> Ho x Wo with
+ * the host-computed 22-bit weights (hcoef/hbounds along W, vcoef/vbounds along H, PIL Resample.c layout),
+ * x / 255 * scale3[c] + shift3[c] -> y NHWC bf16 [N][Ho][Wo][ldy]; u8_out (optional) [N][Ho][Wo][3] the resized
+ * uint8 image.  ws: eegan_fid_samples_workspace(N, H, Wo) bytes. */
+long eegan_fid_samples_workspace(int N, int H, int Wo);
+int eegan_fid_samples(const uint16_t* img, int N, int H, int W, int ld, int Ho, int Wo, const int* hcoef,
+                      const int* hbounds, int hksize, const int* vcoef, const int* vbounds, int vksize,
+                      const float* scale3, const float* shift3, uint16_t* y, int ldy, uint8_t* u8_out, void* ws,
+                      hipStream_t s);
 long eegan_fid_stats_workspace(int D);
 int eegan_fid_stats(const float* act, int N, int D, double* mu, double* sigma, void* ws, hipStream_t s);
 

@@ -151,15 +151,25 @@ def run_step(rank, world, dev):
 
 
 def main():
-    import torch.distributed as dist
+    """train.py's process shape under torchrun: the drop-in modules are
+    imported first (train.py:22-29), then CUDA_VISIBLE_DEVICES is overwritten
+    with the --gpu argument for every rank alike (train.py:513; here '1', i.e.
+    `--gpu 1`, a device this one-GPU box does not have), then the device is
+    torch.device('cuda') (train.py:114).  No call into torch.distributed or
+    eegan_hip.dist: the import pins this rank's GPU and joins the ranks
+    (eegan_hip.launch)."""
+    import miscc.config  # noqa: F401  (train.py:23-29 import order)
+    import miscc.DAMSM_losses  # noqa: F401
+    import sync_batchnorm  # noqa: F401
+    import models  # noqa: F401
+    import DAMSM  # noqa: F401
+    os.environ['CUDA_VISIBLE_DEVICES'] = os.environ.get('DP_GPU_IDS', '1')   # train.py:513
     rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
-    dist.init_process_group('gloo')   # two ranks share the box's one GPU (RCCL refuses that)
-    dev = torch.device('cuda', 0)
-    torch.cuda.set_device(dev)
+    dev = torch.device('cuda')
     rec, params = run_step(rank, world, dev)
-    torch.save({'rec': rec, 'params': params}, os.path.join(sys.argv[1], 'rank%d.pt' % rank))
-    dist.barrier()
-    dist.destroy_process_group()
+    info = {'device_count': torch.cuda.device_count(), 'rocr': os.environ.get('ROCR_VISIBLE_DEVICES'),
+            'hip': os.environ.get('HIP_VISIBLE_DEVICES')}
+    torch.save({'rec': rec, 'params': params, 'info': info}, os.path.join(sys.argv[1], 'rank%d.pt' % rank))
 
 
 if __name__ == '__main__':

@@ -31,10 +31,17 @@ def test_dropin_train_step_two_ranks(gpu, tmp_path, monkeypatch):
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
            '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
            os.path.join(HERE, 'dp_dropin_worker.py'), str(tmp_path)]
-    env = dict(os.environ, OMP_NUM_THREADS='2')
+    # the worker never calls torch.distributed / eegan_hip.dist: importing the drop-in
+    # modules under torchrun pins each rank's GPU and starts the group (eegan_hip.launch);
+    # gloo because both ranks share this box's one GPU (RCCL refuses that)
+    env = dict(os.environ, OMP_NUM_THREADS='2', EEGAN_DIST_BACKEND='gloo')
+    env.pop('EEGAN_AUTO_DIST', None)
     r = subprocess.run(cmd, env=env, timeout=240, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     ranks = [torch.load(os.path.join(tmp_path, 'rank%d.pt' % i)) for i in range(2)]
+    for rk in ranks:   # train.py:513's CUDA_VISIBLE_DEVICES=1 did not unpin the rank's device
+        print('DP2 rank device pin', rk['info'])
+        assert rk['info']['device_count'] == 1 and rk['info']['hip'] == '0', rk['info']
     p0, p1 = ranks[0]['params'], ranks[1]['params']
     assert set(p0) == set(p1)
     for k in p0:   # averaged gradients -> identical Adam steps on every rank

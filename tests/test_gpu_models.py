@@ -856,3 +856,47 @@ def test_config_step_graph_matches_eager(gpu, cfg):
     assert torch.equal(state['graph'], state['eager'])
     for a, b in zip(fakes['graph'], fakes['eager']):
         assert torch.equal(a, b)
+
+
+def test_damsm_grad_early_trains_attr_enhance(gpu, monkeypatch):
+    """The DAMSM branch differentiated on its own lane (trainer.DAMSM_GRAD_EARLY,
+    the default) must give ATTR_Enhance the same gradient as the joint
+    g_loss.backward() of train.py:493-497: a_loss = sent_loss(cnn_code,
+    attrs_emb) (train.py:432) with attrs_emb the trainable ATTR_Enhance output
+    (train.py:193-194), so part of ATTR_Enhance's gradient arrives through the
+    DAMSM terms, not only through the generator."""
+    import models
+    from eegan_hip import trainer as TR
+    from eegan_hip import functional as Fn
+    from sync_batchnorm import DataParallelWithCallback
+    from oracle.eegan_oracle import STANDIN_SPEC
+    tag = 'step'
+    B, W, ncls, disc_class, stages, sb = STEP_CASES[tag]
+    grads = {}
+    for early in (True, False):
+        monkeypatch.setattr(TR, 'DAMSM_GRAD_EARLY', early)
+        G = _load(models.Gen(W, 100), tag + '_g', sb, gpu)
+        A = _load(models.ATTR_Enhance(), tag + '_a', sb + 1, gpu)
+        makers = [lambda: models.Dis64(W), lambda: models.Dis128(W), lambda: models.Dis256(W, disc_class, ncls)]
+        Ds = [_load(makers[i](), tag + '_d%d' % i, sb + 2 + i, gpu) for i in range(3)]
+        standin = _standin_encoder(seeded_state(STANDIN_SPEC, sb + 10), gpu)
+        T = TR.Trainer(DataParallelWithCallback(G), DataParallelWithCallback(A),
+                       [DataParallelWithCallback(d) for d in Ds], standin, None, B, disc_class=disc_class,
+                       class_nums=ncls, class_coe=10.0, sim_coe=0.05, device=gpu)
+        batch = synthetic_batch(B, seed=7, class_num=ncls, sizes=(64, 128, 256))
+        dbatch = {'imgs': [Fn.ImageToNhwcFn.apply(t.to(gpu)) for t in batch['imgs']],
+                  'cls_ids': batch['cls_ids'].to(gpu), 'cap_lens': batch['cap_lens'].to(gpu)}
+        emb = tuple(seeded_tensor(tag + ':' + k, shp, 1).to(gpu) for k, shp in
+                    (('words', (B, 256, 18)), ('sent', (B, 256)), ('attrs', (B, 3, 256)), ('unpair', (B, 256))))
+        T.train_step(dbatch, noise=batch['noise'].to(gpu), emb=emb)
+        torch.cuda.synchronize()
+        grads[early] = {k: p.grad.detach().float().cpu().clone() for k, p in A.named_parameters()}
+    worst = 0.0
+    for k, g_joint in grads[False].items():
+        if k == 'attr_key.bias':   # true gradient identically zero (softmax shift invariance)
+            continue
+        e = float((grads[True][k] - g_joint).norm() / g_joint.norm().clamp_min(1e-30))
+        worst = max(worst, e)
+    _LOG.append(('damsm_grad_early/attr_enhance worst rel_l2 vs joint backward', worst))
+    print('PARITY damsm_grad_early attr_enhance grads vs joint backward: worst rel_l2 %.3e' % worst)
+    assert worst < 1e-4, worst
