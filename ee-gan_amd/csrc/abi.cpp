@@ -31,53 +31,6 @@ int ee_check_launch(const char* what) {
   return 0;
 }
 
-// Ticket counters for the kernels that finish a reduction in the last
-// arriving workgroup of each tile (split-K convs): one zeroed device ring per
-// GPU, handed out in consecutive runs.  Every counter is reset to 0 by the
-// workgroup that consumed it, so a run is clean again when its launch ends;
-// the ring (4 M counters) is long enough that two launches in flight at once
-// never share a run.  Created on first use, outside graph capture (the eager
-// warm-up); allocation inside a capture fails and the caller takes its
-// separate-reduce path instead.
-namespace {
-constexpr long TICKET_RING = 1L << 22;
-constexpr int TICKET_MAX_DEV = 16;
-std::mutex g_ticket_mu;
-unsigned* g_ticket_base[TICKET_MAX_DEV];
-long g_ticket_next[TICKET_MAX_DEV];
-}  // namespace
-
-unsigned* ee_tickets(long n, hipStream_t s) {
-  int dev = 0;
-  if (n <= 0 || n > TICKET_RING || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= TICKET_MAX_DEV)
-    return nullptr;
-  std::lock_guard<std::mutex> lk(g_ticket_mu);
-  if (!g_ticket_base[dev]) {
-    // never allocate while the launch stream is being captured (an allocation
-    // would invalidate the capture)
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
-      (void)hipGetLastError();
-      return nullptr;
-    }
-    void* p = nullptr;
-    if (hipMalloc(&p, TICKET_RING * sizeof(unsigned)) != hipSuccess) {
-      (void)hipGetLastError();
-      return nullptr;
-    }
-    if (hipMemsetAsync(p, 0, TICKET_RING * sizeof(unsigned), s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
-      (void)hipGetLastError();
-      (void)hipFree(p);
-      return nullptr;
-    }
-    g_ticket_base[dev] = static_cast<unsigned*>(p);
-  }
-  if (g_ticket_next[dev] + n > TICKET_RING) g_ticket_next[dev] = 0;
-  unsigned* r = g_ticket_base[dev] + g_ticket_next[dev];
-  g_ticket_next[dev] += n;
-  return r;
-}
-
 static int ee_hip(hipError_t e, const char* what) {
   if (e != hipSuccess) {
     ee_set_error("%s: %s", what, hipGetErrorString(e));

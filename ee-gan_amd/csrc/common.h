@@ -82,9 +82,6 @@ static inline int ee_round_up(int a, int b) { return (a + b - 1) / b * b; }
 // error reporting (thread-local, no global mutable state shared across threads)
 void ee_set_error(const char* fmt, ...);
 int ee_check_launch(const char* what);
-// n zeroed, self-cleaning device counters for last-workgroup reductions (abi.cpp), or
-// nullptr (first use inside a graph capture, out of memory): take the two-kernel path then
-unsigned* ee_tickets(long n, hipStream_t s);
 
 #define EE_LAUNCH_CHECK(name) return ee_check_launch(name)
 

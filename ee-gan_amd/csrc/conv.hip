@@ -20,6 +20,7 @@
 // a reduce kernel that applies the epilogue).
 // Replaces every nn.Conv2d of models.py:14-403 and DAMSM.py.
 #include <stdlib.h>
+#include <string.h>
 
 #include "common.h"
 #include "../../include/eegan_hip.h"
@@ -70,7 +71,6 @@ struct ConvArgs {
   int Mrows, Kw;                // output channels / packed-weight row stride
   int P;                        // N*OH*OW
   int ncls, nsplit;             // parity classes (BWDD stride>1), K splits
-  int noload;                   // diagnostics only (EEGAN_CONV_NOLOAD): skip steady-state loads
   // BWDD only: multiply dx by act'(gate) of the activation `gate_act` expressed
   // through its output (the activated conv input x): the producer's activation
   // backward fused into this data gradient (x has no other non-gating consumer)
@@ -87,7 +87,6 @@ struct ConvArgs {
   int res_vec;  // res rows 8-byte aligned (ldres % 4 == 0, aligned base): vector residual loads
   int wide;     // conv_fast_kernel pairs: one 64-channel stage of whole 128-B lines per K-step pair
   int stage_epi;  // conv_fast_kernel: LDS-staged epilogue (unsplit bf16 output, 16-B aligned rows; host-checked)
-  unsigned* tickets;  // conv_fast_kernel split-K: per-tile counters, last workgroup reduces (ee_tickets) or null
 };
 
 // K step kt, 8-channel chunk kc -> kernel tap and channel.  Normal mode: the
@@ -295,8 +294,6 @@ EE_DEV void staged_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], flo
 }
 
 // split-K reduction + epilogue: out[p][co] = res + gamma*act(sum_z part[z][p][co] + bias).
-// The per-item bodies are shared by the reduce kernel and the last-workgroup
-// finish of conv_fast_kernel (same arithmetic, same z order: bit-identical).
 //
 // 4 consecutive channels of one pixel: 16-byte slab loads (4 splits in
 // flight), 8-byte residual / gate loads and stores; 32-bit index math (the
@@ -382,43 +379,6 @@ __global__ void conv_splitk_reduce_kernel(ConvArgs a) {
     const long p = e / a.Mrows;
     splitk_item1(a, p, (int)(e - p * a.Mrows), gam);
   }
-}
-
-// Last-workgroup finish of a split-K tile (a.tickets set): every split writes
-// its fp32 partial tile, publishes it (device-scope fence) and takes a ticket
-// on the tile's counter; the workgroup drawing the last ticket sums the slabs
-// of the tile in split order and applies the epilogue -- the reduce kernel's
-// items over this tile only, so the result is bit-identical to it -- then
-// resets the counter for the next launch that is handed this run.
-template <int MODE, int TCO, int TPIX>
-EE_DEV void splitk_finish_tile(const ConvArgs& a, int tid, int pix0, int co0, int Pc, int CH, int CW, int qy, int qx,
-                               int stc, int cls) {
-  __shared__ int s_last;
-  __threadfence();
-  __syncthreads();
-  const int tile = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * cls);
-  if (tid == 0) s_last = atomicAdd(a.tickets + tile, 1u) == (unsigned)(a.nsplit - 1);
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();
-  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
-  const int ncol = min(TCO, a.Mrows - co0);
-  const int per = a.red_vec4 ? 4 : 1, ncv = (ncol + per - 1) / per;
-  for (int item = tid; item < TPIX * ncv; item += 256) {
-    const int pix = item / ncv, c = item - pix * ncv;
-    const int pc = pix0 + pix;
-    if (pc >= Pc) break;   // items are pixel-major: the rest of the tile is past the end too
-    long p = pc;
-    if (MODE == MODE_BWDD && a.ncls > 1) {
-      const int hw = CH * CW;
-      const int n = pc / hw, rem = pc - n * hw;
-      const int yy = rem / CW, xx = rem - yy * CW;
-      p = ((long)n * a.OH + qy + stc * yy) * a.OW + qx + stc * xx;
-    }
-    if (a.red_vec4) splitk_item4(a, (unsigned)p, (unsigned)(co0 + 4 * c), gam);
-    else splitk_item1(a, p, co0 + c, gam);
-  }
-  if (tid == 0) atomicExch(a.tickets + tile, 0u);
 }
 
 // ------------------------------------------------------- FWD / BWDD kernel --
@@ -1099,7 +1059,7 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
     }
 #pragma unroll
     for (int k = 0; k < KS; ++k)
-      if (it + S - KS + k < nk && !(a.noload & 1)) issue((it + S - KS + k) % S);
+      if (it + S - KS + k < nk) issue((it + S - KS + k) % S);
     bf16x8_t fa[KS][FI], fb[KS][FJ];
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
@@ -1127,10 +1087,6 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[k][i], fb[k][j], acc[i][j], 0, 0, 0);
     }
   }
-  if (a.noload & 4) {  // diagnostics (EEGAN_CONV_NOLOAD=4): keep the MFMAs alive, skip the epilogue
-    if (acc[0][0][0] == 123.f) reinterpret_cast<float*>(a.out)[0] = acc[FI - 1][FJ - 1][1];
-    return;
-  }
   static_assert(TPIX * TCO * 4 <= S * STAGE * 2, "staged epilogue tile exceeds the LDS ring");
   if (a.stage_epi) {
     staged_epilogue<MODE, TCO, TPIX, FI, FJ, WT_CO, WT_PIX>(a, acc, reinterpret_cast<float4*>(lds), pix0, co0, wi, wj,
@@ -1138,7 +1094,6 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
     return;
   }
   igemm_epilogue<MODE, FI, FJ, WT_CO, WT_PIX>(a, acc, pix0, co0, wi, wj, lane, split, Pc, CH, CW, qy, qx, stc);
-  if (a.tickets) splitk_finish_tile<MODE, TCO, TPIX>(a, tid, pix0, co0, Pc, CH, CW, qy, qx, stc, cls);
 }
 
 // ---------------------------------------------------------- WGRAD kernel --
@@ -2362,7 +2317,7 @@ __global__ __launch_bounds__(256, 2) void conv_s2bwd_lds_kernel(ConvArgs a, int 
       const int iy = i0 - 1 + pr, ix = j0 - 1 + pq;
       const bool ok = sl < NCHUNK && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
       const int off = (((n * a.IH + iy) * a.IW + ix) * a.lds_src + swz(pix, phys) * 8) * 2;
-      if (!(a.noload & 1)) lds_dma16(rsv, &tile[i * 256 + wv * 64], ok ? (unsigned)off : 0x80000000u);
+      lds_dma16(rsv, &tile[i * 256 + wv * 64], ok ? (unsigned)off : 0x80000000u);
     }
     wait_vmcnt_barrier<0>();
 #pragma unroll 1
@@ -2392,10 +2347,6 @@ __global__ __launch_bounds__(256, 2) void conv_s2bwd_lds_kernel(ConvArgs a, int 
               make_float4(acc[g][t][0], acc[g][t][1], acc[g][t][2], acc[g][t][3]);
         }
       __syncthreads();
-      if (a.noload & 2) {  // diagnostics: skip the global stores
-        if (NSB == 2) sb ^= 1;
-        continue;
-      }
       const int y0 = 2 * (i0 + rr), x0 = 2 * j0;
 #pragma unroll
       for (int k = 0; k < (SPX * 4 + 255) / 256; ++k) {
@@ -2556,17 +2507,27 @@ struct Plan {
   int tco, tpix, nsplit, blocks;
 };
 
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
+// Planner / kernel-path knobs for A/B tests and sweeps, all in one variable:
+// EEGAN_CONV="thin=0,wide=0,target=256" (key = the knob's name below; unset
+// keys keep their defaults).  Read per launch on the host.
+static int knob(const char* key, int dflt) {
+  const char* v = getenv("EEGAN_CONV");
+  if (!v) return dflt;
+  const size_t n = strlen(key);
+  for (const char* p = v; p && *p;) {
+    if (!strncmp(p, key, n) && p[n] == '=') return atoi(p + n + 1);
+    p = strchr(p, ',');
+    if (p) ++p;
+  }
+  return dflt;
 }
 
 Plan plan_igemm(const ConvArgs& a, int Pc_max) {
   // tuning knobs (benchmark sweeps only): grid target, min K-steps per split,
   // and whether 64-row tiles are tried before splitting K
-  const int target = env_int("EEGAN_CONV_TARGET", 512);
-  const int mink = env_int("EEGAN_CONV_MINK", 16);
-  const int small_co = env_int("EEGAN_CONV_SMALLCO", 1);
+  const int target = knob("target", 512);
+  const int mink = knob("mink", 16);
+  const int small_co = knob("smallco", 1);
   const int rows = a.Mrows;
   Plan p;
   p.tco = rows > 64 ? 128 : rows > 32 ? 64 : rows > 16 ? 32 : 16;
@@ -2591,7 +2552,7 @@ Plan plan_igemm(const ConvArgs& a, int Pc_max) {
 // 0 when the shape is not eligible (the tile kernels run), else the launch rc.
 template <int MODE>
 int try_thin(const ConvArgs& a, hipStream_t s, long src_bytes) {
-  if (!env_int("EEGAN_CONV_THIN", 1) || src_bytes >= 0x7fffffffL) return 0;
+  if (!knob("thin", 1) || src_bytes >= 0x7fffffffL) return 0;
   if (a.R != 3 || a.S != 3 || a.st != 1 || a.ncls != 1 || a.res || a.gate || a.out_f32 || a.Mrows > 32) return 0;
   if ((a.ldo & 3) || ((uintptr_t)a.out & 7) || (a.lds_src & 7) || ((uintptr_t)a.src & 15)) return 0;
   const int nt = a.Mrows > 16 ? 2 : 1, slices = ee_cdiv(a.Mrows, 32);
@@ -2601,7 +2562,7 @@ int try_thin(const ConvArgs& a, hipStream_t s, long src_bytes) {
   const long iters = ((a.P + 15L) / 16 + gpi - 1) / gpi;
   const int nb = ee_round_up((int)std::min<long>((iters + 3) / 4, 1024), 8);
   const int ipb = (int)((iters + nb - 1) / nb);
-  if (nks <= 9 && a.OW % 64 == 0 && a.ph <= 1 && a.pw <= 1 && env_int("EEGAN_CONV_THIN_LDS", 1)) {
+  if (nks <= 9 && a.OW % 64 == 0 && a.ph <= 1 && a.pw <= 1 && knob("thin_lds", 1)) {
     const int tiles = a.N * (a.OW / 64) * ((a.OH + 7) / 8);
     const int nbl = ee_round_up(std::min(tiles, nks == 3 ? 2048 : 768), 8), tpb = (tiles + nbl - 1) / nbl;
 #define TL(NT, NKS) ee_launch(conv_thin_lds_kernel<MODE, NT, NKS>, dim3(nbl), dim3(256), 0, s, a, (int)src_bytes, tpb)
@@ -2623,12 +2584,12 @@ int try_thin(const ConvArgs& a, hipStream_t s, long src_bytes) {
 // 4x4 / stride-2 / pad-1 data gradients with <= 32 input channels take
 // conv_s2bwd_lds_kernel (0: not eligible, else the launch rc as try_thin)
 int try_s2bwd(const ConvArgs& a, hipStream_t s, long src_bytes) {
-  if (!env_int("EEGAN_CONV_S2B", 1) || src_bytes >= 0x7fffffffL) return 0;
+  if (!knob("s2b", 1) || src_bytes >= 0x7fffffffL) return 0;
   if (a.R != 4 || a.S != 4 || a.st != 2 || a.ph != 1 || a.pw != 1 || a.ncls != 4 || a.up2 || a.Mrows > 64) return 0;
   if ((a.Cgp != 32 && a.Cgp != 64 && a.Cgp != 128) || a.Cvalid != a.Cgp || (a.lds_src & 7) ||
       ((uintptr_t)a.src & 15))
     return 0;
-  if (a.Mrows > 32 && !env_int("EEGAN_CONV_S2B64", 1)) return 0;
+  if (a.Mrows > 32 && !knob("s2b64", 1)) return 0;
   // LDS-staged epilogue: bf16 output, 16-B runs of 8 channels (output / gate / residual rows 16-B aligned)
   if (a.out_f32 || a.bias || a.act != ACT_NONE || (a.Mrows & 7) || (a.ldo & 7) || ((uintptr_t)a.out & 15)) return 0;
   if (a.gate && ((a.ldgate & 7) || ((uintptr_t)a.gate & 15))) return 0;
@@ -2636,11 +2597,10 @@ int try_s2bwd(const ConvArgs& a, hipStream_t s, long src_bytes) {
   if ((a.OH & 1) || (a.OW & 1) || (a.OW / 2) % S2B_TW || (a.OH / 2) % S2B_TH) return 0;
   if ((long)a.N * a.OH * a.OW >= 0x7fffffffL) return 0;
   const int tiles = a.N * (a.OW / 2 / S2B_TW) * (a.OH / 2 / S2B_TH);
-  const int nbl = ee_round_up(std::min(tiles, env_int("EEGAN_CONV_S2B_BLOCKS", 512)), 8);
+  const int nbl = ee_round_up(std::min(tiles, knob("s2b_blocks", 512)), 8);
   const int tpb = (tiles + nbl - 1) / nbl;
   const int nt = a.Mrows > 16 ? 2 : 1, slices = ee_cdiv(a.Mrows, 32);
   ConvArgs a2 = a;
-  a2.noload = env_int("EEGAN_CONV_NOLOAD", 0);  // diagnostics: 1 no halo DMA, 2 no epilogue
 #define SB(NT, NC) \
   ee_launch(conv_s2bwd_lds_kernel<NT, NC>, dim3(nbl, slices), dim3(256), 0, s, a2, (int)src_bytes, tpb)
   if (a.Cgp == 128) { if (nt == 2) SB(2, 4); else SB(1, 4); }
@@ -2655,7 +2615,7 @@ int try_s2bwd(const ConvArgs& a, hipStream_t s, long src_bytes) {
 // (0: not eligible, else the launch rc as try_thin)
 template <int MODE>
 int try_1x1(const ConvArgs& a, hipStream_t s, long src_bytes) {
-  if (!env_int("EEGAN_CONV_1X1", 1) || src_bytes >= 0x7fffffffL) return 0;
+  if (!knob("1x1", 1) || src_bytes >= 0x7fffffffL) return 0;
   if (a.R != 1 || a.S != 1 || a.st != 1 || a.ph || a.pw || a.ncls != 1 || a.up2 || a.Kw > 256) return 0;
   if ((a.lds_src & 7) || ((uintptr_t)a.src & 15)) return 0;
   const int nks = a.Kw / BK;
@@ -2671,7 +2631,7 @@ int try_1x1(const ConvArgs& a, hipStream_t s, long src_bytes) {
   constexpr int G1 = 1;  // groups per wave iteration (larger: more loads in flight, but the
   const int gpi = G1;    // epilogue unrolled per group costs VGPRs: 247 at NT = 4, GPI = 4)
   const long iters = ((a.P + 15L) / 16 + gpi - 1) / gpi;
-  const int cap = std::max(64, env_int("EEGAN_CONV_1X1_BLOCKS", 1024) / rowblocks);
+  const int cap = std::max(64, knob("1x1_blocks", 1024) / rowblocks);
   const int nb = ee_round_up((int)std::min<long>((iters + 3) / 4, cap), 8);
   const int ipb = (int)((iters + nb - 1) / nb);
   const dim3 grid(nb, rowblocks);
@@ -2704,8 +2664,6 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   if (MODE == MODE_BWDD)
     if (const int sb = try_s2bwd(a, s, src_bytes)) return sb > 0 ? 0 : sb;
   Plan p = plan_igemm(a, Pc_max);
-  a.noload = env_int("EEGAN_CONV_NOLOAD", 0);
-  const int ksv = env_int("EEGAN_CONV_KS", 22);  // 22: pairs, interleaved reads; 2: pairs; 1: single steps
   a.nsplit = p.nsplit;
   a.part = p.nsplit > 1 ? part_ws : nullptr;
   {
@@ -2716,12 +2674,12 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
     if (MODE == MODE_BWDD && a.st > 1) taps_max = ee_cdiv(a.R, a.st) * ee_cdiv(a.S, a.st);
     const int nk_max = taps_max * nc;
     const int kchunk = ee_cdiv(nk_max, p.nsplit);
-    a.wide = p.tco >= 64 && nc % 2 == 0 && kchunk % 2 == 0 && env_int("EEGAN_CONV_WIDE", 1);
+    a.wide = p.tco >= 64 && nc % 2 == 0 && kchunk % 2 == 0 && knob("wide", 1);
   }
   // LDS-staged epilogue (conv_fast_kernel): unsplit bf16 output with 16-B aligned rows
   a.stage_epi = p.nsplit == 1 && !a.out_f32 && a.Mrows % 8 == 0 && a.ldo % 8 == 0 && ((uintptr_t)a.out & 15) == 0 &&
                 (!a.gate || (a.ldgate % 8 == 0 && ((uintptr_t)a.gate & 15) == 0)) &&
-                (!a.res || (a.ldres % 8 == 0 && ((uintptr_t)a.res & 15) == 0)) && env_int("EEGAN_CONV_STAGE_EPI", 1);
+                (!a.res || (a.ldres % 8 == 0 && ((uintptr_t)a.res & 15) == 0)) && knob("stage_epi", 1);
   if (p.nsplit > 1 && !part_ws) {
     ee_set_error("conv: split-K workspace missing");
     return -22;
@@ -2730,34 +2688,23 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   const long total = (long)a.P * a.Mrows;
   if (p.nsplit > 1) {
     const uintptr_t oal = a.out_f32 ? 15 : 7;
-    // EEGAN_CONV_RED_VEC4=0 forces the scalar reduce (A/B and bit-identity tests)
+    // red_vec4=0 forces the scalar reduce (A/B and bit-identity tests)
     a.red_vec4 = a.Mrows % 4 == 0 && total < 0x7fffffffL && a.ldo % 4 == 0 && ((uintptr_t)a.out & oal) == 0 &&
                  ((uintptr_t)a.part & 15) == 0 && (!a.gate || a.gate_vec) && (!a.res || a.res_vec) &&
-                 env_int("EEGAN_CONV_RED_VEC4", 1);
+                 knob("red_vec4", 1);
   }
   const long w_bytes = (long)ee_round_up(a.Mrows, 128) * a.Kw * 2;
 #define GL(TC, TP) ee_launch(conv_glds_kernel<MODE, TC, TP>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
-#define FA(TC, TP)                                                                                          \
-  do {                                                                                                       \
-    if (ksv == 22) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 4, 2>, grid, dim3(256), 0, s, a, src_bytes, w_bytes); \
-    else if (ksv == 2) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 4>, grid, dim3(256), 0, s, a, src_bytes, w_bytes); \
-    else ee_launch(conv_fast_kernel<MODE, TC, TP, 1, 4>, grid, dim3(256), 0, s, a, src_bytes, w_bytes);                     \
-  } while (0)
+#define FA(TC, TP) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 4, 2>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
 #define IG(TC, TP, WC) ee_launch(conv_igemm_kernel<MODE, TC, TP, WC>, grid, dim3(256), 0, s, a)
   // glds: channel chunks fetched whole (C % 8 != 0 masked in the fragments; the
   // fast kernel needs whole valid chunks)
-  const bool glds = ((a.Cvalid % 8) == 0 || a.Cgp == 8 || env_int("EEGAN_CONV_GLDS_RAGGED", 1)) &&
+  const bool glds = ((a.Cvalid % 8) == 0 || a.Cgp == 8 || knob("glds_ragged", 1)) &&
                     src_bytes < 0x7fffffffL && w_bytes < 0x7fffffffL;
   int tr_ = a.R, ts_ = a.S;
   if (MODE == MODE_BWDD && a.st > 1) tr_ = ee_cdiv(a.R, a.st), ts_ = ee_cdiv(a.S, a.st);
-  const bool fast = glds && a.Cgp % BK == 0 && !a.up2 && tr_ * ts_ <= 32 && env_int("EEGAN_CONV_FAST", 1);
+  const bool fast = glds && a.Cgp % BK == 0 && !a.up2 && tr_ * ts_ <= 32 && knob("fast", 1);
   if (fast) {
-    // split-K: the last workgroup of each tile reduces it (EEGAN_CONV_SPLITK_FUSED=1).  Off by
-    // default: the device-scope fences around the tickets (an L2 writeback + invalidate per
-    // workgroup on this multi-XCD part) made the 4x4 / 8x8 deep layers 2.8-6.8x slower than
-    // the separate reduce kernel (profiles/r03_splitk_fused.log)
-    if (p.nsplit > 1 && env_int("EEGAN_CONV_SPLITK_FUSED", 0))
-      a.tickets = ee_tickets((long)grid.x * grid.y * a.ncls, s);
     if (p.tco == 128) { if (p.tpix == 128) FA(128, 128); else FA(128, 64); }
     else if (p.tco == 64) { if (p.tpix == 128) FA(64, 128); else FA(64, 64); }
     else if (p.tco == 32) { if (p.tpix == 256) FA(32, 256); else FA(32, 64); }
@@ -2777,7 +2724,7 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
 #undef GL
 #undef FA
   int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd" : "conv_bwd_data");
-  if (rc || a.nsplit == 1 || a.tickets) return rc;
+  if (rc || a.nsplit == 1) return rc;
   const long work = a.red_vec4 ? total / 4 : total;
   ee_launch(conv_splitk_reduce_kernel<MODE>, dim3((int)std::min<long>((work + 255) / 256, 4096)), dim3(256), 0, s, a);
   return ee_check_launch("conv_splitk_reduce");
@@ -2977,11 +2924,11 @@ static bool wgrad_glds_ok(const eegan_conv_desc* d) {
 
 // blocks of conv_wgrad_thin_kernel for this shape, or 0 when it does not apply
 static int wgrad_thin_blocks(const eegan_conv_desc* d) {
-  if (!env_int("EEGAN_CONV_THIN", 1)) return 0;
+  if (!knob("thin", 1)) return 0;
   if (d->R != 3 || d->S != 3 || d->stride != 1 || d->pad_h != 1 || d->pad_w != 1 || d->up2) return 0;
   const int cg = ee_round_up(d->C, 8);
   // output channels in 8-channel groups on blockIdx.y (each group re-reads the x halo)
-  if (d->K > env_int("EEGAN_WGRAD_THIN_MAXK", 8) || (cg != 32 && cg != 64) || d->Wo % WTH_W || d->Ho % WTH_H) return 0;
+  if (d->K > knob("wgrad_thin_maxk", 8) || (cg != 32 && cg != 64) || d->Wo % WTH_W || d->Ho % WTH_H) return 0;
   if (wgrad_x_bytes(d) >= 0x7fffffffL || wgrad_dy_bytes(d) >= 0x7fffffffL) return 0;
   const int tiles = d->N * (d->Ho / WTH_H) * (d->Wo / WTH_W);
   if (tiles < 8) return 0;
@@ -3005,14 +2952,14 @@ static void wgrad_plan(const eegan_conv_desc* d, int& TCO, int& TK, int& nsplit,
   // ~2 blocks per CU, >= 16 K-steps (512 pixels) per split: the fp32 slab
   // (nsplit x Cout x K) is written once and read once by the column reduce
   // knobs for sweeps: grid target (blocks) and minimum pixels per split
-  int want = std::max(1, env_int("EEGAN_WGRAD_TARGET", 512) / std::max(tiles, 1));
-  const int maxsplit = std::max(1, ee_cdiv(P, env_int("EEGAN_WGRAD_MINP", 512)));
+  int want = std::max(1, knob("wgrad_target", 512) / std::max(tiles, 1));
+  const int maxsplit = std::max(1, ee_cdiv(P, knob("wgrad_minp", 512)));
   nsplit = std::min(want, maxsplit);
   pps = ee_round_up(ee_cdiv(P, nsplit), BK);
   nsplit = ee_cdiv(P, pps);
   // many-split grids: a split count that makes the grid a multiple of 8, so the
   // fast kernel can keep each split's k tiles on one XCD (WgradArgs::xcd_remap)
-  if (nsplit >= 8 && (tiles * nsplit) % 8 && env_int("EEGAN_WGRAD_SPLIT8", 1)) {
+  if (nsplit >= 8 && (tiles * nsplit) % 8 && knob("wgrad_split8", 1)) {
     for (int ns = nsplit + 1; ns < nsplit + 16 && ns <= maxsplit; ++ns) {
       const int pp = ee_round_up(ee_cdiv(P, ns), BK), n2 = ee_cdiv(P, pp);
       if ((tiles * n2) % 8 == 0) {
@@ -3064,8 +3011,8 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
   if (nsplit == 1 && w.P > 0) {
     w.dw = dw;
     w.accumulate = accumulate;
-    // EEGAN_WGRAD_STAGE_EPI: 0 off, 1 unsplit dW only, 2 (default) also the row-major split slabs
-    w.stage = d->C % 4 == 0 && ((uintptr_t)dw & 15) == 0 && env_int("EEGAN_WGRAD_STAGE_EPI", 2);
+    // wgrad_stage_epi: 0 off, 1 unsplit dW only, 2 (default) also the row-major split slabs
+    w.stage = d->C % 4 == 0 && ((uintptr_t)dw & 15) == 0 && knob("wgrad_stage_epi", 2);
   }
   if (w.P > 0 && wgrad_thin_blocks(d)) {
     const int tiles = d->N * (d->Ho / WTH_H) * (d->Wo / WTH_W);
@@ -3080,28 +3027,24 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
     if (rc) return rc;
   } else if (w.P > 0) {
     // co-quad slabs where they measured ahead (K > 1024; at K <= 1024 the quad reduce has too few blocks)
-    w.quad = nsplit > 1 && d->K % 4 == 0 && ((uintptr_t)ws & 15) == 0 && K > env_int("EEGAN_WGRAD_QUAD_MINK", 1024) &&
-             env_int("EEGAN_WGRAD_QUAD", 1);
+    w.quad = nsplit > 1 && d->K % 4 == 0 && ((uintptr_t)ws & 15) == 0 && K > knob("wgrad_quad_mink", 1024) &&
+             knob("wgrad_quad", 1);
     // split slabs through the LDS-staged epilogue too (row-major, 16-B stores) where not co-quad
     if (nsplit > 1 && !w.quad)
-      w.stage = ((uintptr_t)ws & 15) == 0 && env_int("EEGAN_WGRAD_STAGE_EPI", 2) >= 2;
+      w.stage = ((uintptr_t)ws & 15) == 0 && knob("wgrad_stage_epi", 2) >= 2;
     dim3 grid(ee_cdiv(K, TK), ee_cdiv(d->K, TCO), nsplit);
     // (measured ahead on the many-split shapes: 3x3 128-ch 64^2 51 -> 35 us, 4x4/s2 64->128 50 -> 32 us;
     // behind on the few-split deep layers, profiles/r03_wgrad_xcd.txt)
     w.xcd_remap = grid.x > 1 && grid.z >= 8 && ((long)grid.x * grid.y * grid.z) % 8 == 0 &&
-                  env_int("EEGAN_WGRAD_XCD", 1);
+                  knob("wgrad_xcd", 1);
     const long x_bytes = wgrad_x_bytes(d), dy_bytes = wgrad_dy_bytes(d);
 #define WG(TC, TKK, WC) ee_launch(conv_wgrad_kernel<TC, TKK, WC>, grid, dim3(256), 0, stream, w)
 #define WL(TC, TKK) ee_launch(conv_wgrad_glds_kernel<TC, TKK>, grid, dim3(256), 0, stream, w, x_bytes, dy_bytes)
-#define WF(TC, TKK)                                                                                      \
-  do {                                                                                                   \
-    if (wks == 2) ee_launch(conv_wgrad_fast_kernel<TC, TKK, 2>, grid, dim3(256), 0, stream, w, x_bytes, dy_bytes, lw, lhw); \
-    else ee_launch(conv_wgrad_fast_kernel<TC, TKK, 1>, grid, dim3(256), 0, stream, w, x_bytes, dy_bytes, lw, lhw);          \
-  } while (0)
+#define WF(TC, TKK) \
+  ee_launch(conv_wgrad_fast_kernel<TC, TKK, 2>, grid, dim3(256), 0, stream, w, x_bytes, dy_bytes, lw, lhw)
     const int OW = d->Wo, HW = d->Ho * d->Wo;
     const bool pow2 = OW > 0 && (OW & (OW - 1)) == 0 && (HW & (HW - 1)) == 0;
-    const int wks = env_int("EEGAN_WGRAD_KS", 2);
-    if (wgrad_glds_ok(d) && pow2 && !d->up2 && env_int("EEGAN_CONV_FAST", 1)) {
+    if (wgrad_glds_ok(d) && pow2 && !d->up2 && knob("fast", 1)) {
       const int lw = __builtin_ctz(OW), lhw = __builtin_ctz(HW);
       if (TCO == 128) { if (TK == 128) WF(128, 128); else WF(128, 64); }
       else if (TCO == 64) { if (TK == 128) WF(64, 128); else WF(64, 64); }

@@ -115,43 +115,9 @@ __global__ void cat_channels_kernel(const CatParts parts, long P, bf16_t* out, i
   }
 }
 
-// Fixed-order finish of the per-block partials inside the partial kernel (no
-// second launch): every block publishes its partial write-through (agent-scope
-// atomic store), drains it, then draws a ticket; the block that draws the last
-// one sums ws[0..gridDim.x) in a fixed order -- the same value whatever the
-// arrival order -- and resets the ticket for the next launch (the tickets start
-// zeroed, ee_tickets).  Only agent-scope atomic loads read the handed-off
-// partials, so no cache of the reading CU can hold a stale copy.
-struct DotFinish {
-  unsigned* ticket;  // null: the caller launches dot_final_kernel instead
-  float* out;
-  float scale;
-  int accumulate;
-};
-
-EE_DEV void dot_finish(float acc, float* ws, const DotFinish& f, float* red) {
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(ws + blockIdx.x, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(f.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    red[8] = t == gridDim.x - 1 ? 1.f : 0.f;   // the block's one LDS array carries the flag
-  }
-  __syncthreads();
-  if (red[8] == 0.f) return;                   // block-uniform
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the loads below the ticket
-  float a = 0.f;
-  for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x)
-    a += __hip_atomic_load(ws + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  a = block_sum(a, red);
-  if (threadIdx.x == 0) {
-    f.out[0] = f.accumulate ? f.out[0] + a * f.scale : a * f.scale;
-    __hip_atomic_store(f.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // partial sums of x*y (or x when y == null) per block -> ws[block]
 __global__ __launch_bounds__(NT) void dot_partial_kernel(const bf16_t* x, int ldx, const bf16_t* y, int ldy, long P,
-                                                         int C, float* ws, DotFinish fin) {
+                                                         int C, float* ws) {
   __shared__ float red[16];
   const int C8 = (C + 7) / 8;
   float acc = 0.f;
@@ -170,7 +136,6 @@ __global__ __launch_bounds__(NT) void dot_partial_kernel(const bf16_t* x, int ld
     }
   }
   acc = block_sum(acc, red);
-  if (fin.ticket) return dot_finish(acc, ws, fin, red);
   if (threadIdx.x == 0) ws[blockIdx.x] = acc;
 }
 
@@ -179,7 +144,7 @@ __global__ __launch_bounds__(NT) void dot_partial_kernel(const bf16_t* x, int ld
 __global__ __launch_bounds__(NT) void scale_dot_partial_kernel(const bf16_t* g, int ldg, const bf16_t* h, int ldh,
                                                                const float* gamma, float alpha, long P, int C,
                                                                bf16_t* out, int ldo, float* ws, int act,
-                                                               float slope, DotFinish fin) {
+                                                               float slope) {
   __shared__ float red[16];
   const int C8 = (C + 7) / 8;
   const bool vec = (ldg % 8 == 0) && (ldh % 8 == 0) && (ldo % 8 == 0);
@@ -199,7 +164,6 @@ __global__ __launch_bounds__(NT) void scale_dot_partial_kernel(const bf16_t* g, 
     store8(out + p * ldo + c0, a, nv, vec);
   }
   acc = block_sum(acc, red);
-  if (fin.ticket) return dot_finish(acc, ws, fin, red);
   if (threadIdx.x == 0) ws[blockIdx.x] = acc;
 }
 
@@ -605,13 +569,6 @@ __global__ void fill_kernel(float* x, long n, float v) {
   GRID_LOOP(e, n) x[e] = v;
 }
 
-// in-kernel finish (EEGAN_DOT_FUSED=0: the separate dot_final launch, A/B)
-DotFinish dot_finish_args(float* out, float scale, int accumulate, hipStream_t s) {
-  const char* v = getenv("EEGAN_DOT_FUSED");
-  const bool on = v && atoi(v) != 0;   // off by default: 1024 same-address tickets measured slower (profiles/r03_dot_finish_ab.txt)
-  return DotFinish{on ? ee_tickets(1, s) : nullptr, out, scale, accumulate};
-}
-
 }  // namespace
 
 extern "C" {
@@ -654,10 +611,9 @@ long eegan_dot_workspace(void) { return 1024 * sizeof(float); }
 int eegan_dot(const uint16_t* x, int ldx, const uint16_t* y, int ldy, long P, int C, float scale, float* ws,
               float* out, int accumulate, hipStream_t s) {
   const int blocks = std::min(1024, grid_for(P * ((C + 7) / 8)));
-  const DotFinish fin = dot_finish_args(out, scale, accumulate, s);
-  dot_partial_kernel<<<blocks, NT, 0, s>>>(x, ldx, y, ldy, P, C, ws, fin);
+  dot_partial_kernel<<<blocks, NT, 0, s>>>(x, ldx, y, ldy, P, C, ws);
   int rc = ee_check_launch("dot_partial");
-  if (rc || fin.ticket) return rc;
+  if (rc) return rc;
   dot_final_kernel<<<1, 1024, 0, s>>>(ws, blocks, scale, out, accumulate);
   return ee_check_launch("dot_final");
 }
@@ -666,10 +622,9 @@ int eegan_scale_dot(const uint16_t* g, int ldg, const uint16_t* h, int ldh, cons
                     int C, uint16_t* out, int ldo, float* ws, float* dot_out, int accumulate, int act, float slope,
                     hipStream_t s) {
   const int blocks = std::min(1024, grid_for(P * ((C + 7) / 8)));
-  const DotFinish fin = dot_finish_args(dot_out, 1.f, accumulate, s);
-  scale_dot_partial_kernel<<<blocks, NT, 0, s>>>(g, ldg, h, ldh, gamma, alpha, P, C, out, ldo, ws, act, slope, fin);
+  scale_dot_partial_kernel<<<blocks, NT, 0, s>>>(g, ldg, h, ldh, gamma, alpha, P, C, out, ldo, ws, act, slope);
   int rc = ee_check_launch("scale_dot_partial");
-  if (rc || fin.ticket) return rc;
+  if (rc) return rc;
   dot_final_kernel<<<1, 1024, 0, s>>>(ws, blocks, 1.f, dot_out, accumulate);
   return ee_check_launch("dot_final");
 }

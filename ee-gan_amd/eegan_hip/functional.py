@@ -110,62 +110,14 @@ def _sink_of(ctx, i):
     return g
 
 
-# Weight gradients on a side stream (EEGAN_WGRAD_SIDE=1): a direct-sink dW
-# (first-order backward, accumulated straight into the FlatAdam flat gradient)
-# is launched on a side stream of the current one, forked behind the kernels
-# that produced its operands, so it runs beside the data-gradient chain that
-# the next layer's backward waits for.  The owning FlatAdam joins its side
-# streams at step(); the operands are recorded on the side stream so their
-# memory is not reused before it has run.  Side streams are created on first
-# use (outside graph capture: a warm-up step creates them).  Only streams in
-# WGRAD_SIDE_FROM fork them (the trainer puts its step's main stream there):
-# a side stream forked from a stream that is itself forked into a graph
-# capture (a discriminator lane) makes the runtime's capture-end walk recurse
-# without end (stack overflow in hipStreamEndCapture, ROCm 7.0; the same
-# failure as round 2's per-lane side streams and Inception branch streams).
-WGRAD_SIDE = os.environ.get('EEGAN_WGRAD_SIDE', '0') == '1'
-WGRAD_SIDE_FROM = set()
-_SIDES = {}
-
-
-def _side_of(cur):
-    s = _SIDES.get(cur.cuda_stream)
-    if s is None:
-        if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError('weight-gradient side stream first needed during graph capture: run an eager '
-                               'warm-up step first')
-        s = _SIDES[cur.cuda_stream] = T.new_stream(cur.device)
-    return s
-
-
 def _sink_wgrad(ctx, i, x, dz, g, W_shape):
     """dW of input i accumulated into its FlatAdam gradient view; False when
     the gradient has to go through autograd instead."""
-    side = owner = None
-    if WGRAD_SIDE and _sink_of(ctx, i) is not None:
-        owner = getattr(ctx.next_functions[i][0].variable, '_eegan_opt', None)
-        cur = torch.cuda.current_stream()
-        if owner is not None and cur.cuda_stream in WGRAD_SIDE_FROM:
-            side = _side_of(cur)
-            side.wait_stream(cur)
-    with torch.cuda.stream(side) if side is not None else _NullCtx():
-        sink = _grad_sink(ctx, i)
-        if sink is None or not sink.is_contiguous(memory_format=CL):
-            return False
-        conv_bwd_weight_raw(x, dz, g, W_shape, out=sink)
-    if side is not None:
-        x.record_stream(side)
-        dz.record_stream(side)
-        owner._pending_sides.add(side)
-    return True
-
-
-class _NullCtx(object):
-    def __enter__(self):
-        return None
-
-    def __exit__(self, *a):
+    sink = _grad_sink(ctx, i)
+    if sink is None or not sink.is_contiguous(memory_format=CL):
         return False
+    conv_bwd_weight_raw(x, dz, g, W_shape, out=sink)
+    return True
 
 
 # ============================================================== weights ===

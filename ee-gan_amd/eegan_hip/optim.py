@@ -87,7 +87,6 @@ class FlatAdam(torch.optim.Optimizer):
                 p._eegan_gen = self._gen
                 p._eegan_opt = self
                 self._views.append((p, o, k, g))
-        self._pending_sides = set()   # side streams holding weight-gradient writes (functional.WGRAD_SIDE)
         self._pack_sig = None
         self._pack_table = None
         self._pack_total = 0
@@ -259,11 +258,6 @@ class FlatAdam(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
-        if self._pending_sides:
-            cur = torch.cuda.current_stream()
-            for s in self._pending_sides:
-                cur.wait_stream(s)
-            self._pending_sides.clear()
         self._sync_grads()
         self._allreduce()
         g = self.param_groups[0]

@@ -56,33 +56,6 @@ GTERM_GRAD_EARLY = int(os.environ.get('EEGAN_GTERM_GRAD_EARLY', '-1'))   # -1: +
 # first packets of the critical lane then do not queue behind the others' (C2: 678 vs 656 img/s,
 # tools/gpu_env_ab.sh); EEGAN_LANE_ORDER=fwd: D64, D128, D256 after the DAMSM lane
 LANE_ORDER = os.environ.get('EEGAN_LANE_ORDER', 'rev')
-# EEGAN_LATE_JOIN=1: the discriminator lanes are joined into the main stream only
-# after g_update's backward: the backward starts from the per-D terms as roots
-# (their gradients flow lane -> generator, the generator's kernels wait for a
-# lane only where they consume its image gradient), so a lane still busy with
-# its update does not hold up the generator's backward.
-LATE_JOIN = os.environ.get('EEGAN_LATE_JOIN', '0') == '1'
-# EEGAN_DEFER_D=<phase>: the smaller discriminators' lanes start only after the
-# largest D's lane has finished <phase> (a d_update stamp name, e.g. 'loss
-# backward'): they stop competing with the critical lane and fill the GPU
-# during the generator's backward instead (needs LATE_JOIN).
-DEFER_D = os.environ.get('EEGAN_DEFER_D', '').replace('_', ' ')   # underscores stand for spaces
-# EEGAN_TEXT_AHEAD=1: the frozen text encoder (train.py:169-184, no parameter
-# of it is trained) encodes the NEXT batch's captions on its own lane while
-# g_update's backward runs -- a stretch where the generator's small launches
-# leave the GPU mostly idle -- and the step starts from the embeddings the
-# previous step produced, instead of encoding its own batch first on the
-# critical path.  Every step still encodes exactly one batch; the next
-# batch's token tensors come from batch['next'] (the same keys as the batch;
-# absent: the batch itself, the fixed-buffer steady state of bench.py).  The
-# first step of a trainer encodes its own batch up front.
-TEXT_AHEAD = os.environ.get('EEGAN_TEXT_AHEAD', '0') == '1'   # measured -0.6 % (profiles/r03_text_ahead.txt): off
-# EEGAN_EARLY_D0=1: Dis64's whole d_update (and its g_update term) is issued on
-# its lane as soon as the generator has produced img_64 (Gen._image_hook), so it
-# runs beside the generator's stages 2-3 -- a stretch where the generator's
-# small launches leave most of the GPU idle -- instead of beside D256's update.
-EARLY_D0 = os.environ.get('EEGAN_EARLY_D0', '0') == '1'   # measured: G's forward slows by ~1 ms beside it, neutral to -0.7 % (profiles/r03_early_d0.txt)
-
 
 # a g_update term already differentiated w.r.t. its fake image on its lane
 # (GTERM_GRAD_EARLY): its value, the image alias and the gradient there
@@ -132,10 +105,6 @@ class Trainer(object):
             streams = os.environ.get('EEGAN_STREAMS', '1') != '0'
         self.use_streams = bool(streams) and torch.cuda.is_available() and torch.device(device).type == 'cuda'
         self._streams = None
-        self._mark_want = self._mark_ev = None
-        self._early_done = {}
-        self._emb_cur = self._emb_nxt = None   # TEXT_AHEAD buffers: this step's / the next step's embeddings
-        self._text_lane = None
 
     def _side_streams(self, n, fork=True):
         if not self.use_streams:
@@ -165,9 +134,6 @@ class Trainer(object):
         for s in streams:
             if s is not None:
                 main.wait_stream(s)
-
-    def _late_join(self, terms):
-        return LATE_JOIN and self.use_streams and terms is not None
 
     @staticmethod
     def load_optimizers(netG, netDs, attr_enhance):
@@ -283,53 +249,18 @@ class Trainer(object):
         return (w[0] + w[1]) * lam, (s[0] + s[1]) * lam, (a[0] + a[1]) * lam
 
     # ----------------------------------------------------------- updates --
-    def d_update_early(self, i, imgs, fake_img, sent_emb, unpair_sent_emb, class_labels, iter_rec, g_early):
-        """Issue discriminator i's d_update (train.py:439-466) and, when
-        `g_early` is a list, its g_update term on its own lane now -- forked
-        from the caller's stream at this point, so it waits only for the work
-        issued so far (the generator up to `fake_img`).  d_update then skips
-        it and joins its lane with the others.  Returns the g term or None."""
-        lane = self._side_streams(len(self.netsD), fork=False)[i]
-        lane.wait_stream(torch.cuda.current_stream())
-        fakes = [None] * len(self.netsD)
-        fakes[i] = fake_img
-        with self._on(lane):
-            Fn.stamp('D%d start' % i)
-            self._d_update_one(i, imgs, fakes, sent_emb, unpair_sent_emb, class_labels, iter_rec)
-            term = self._g_term(i, fakes, sent_emb, class_labels, iter_rec) if g_early is not None else None
-        self._early_done[i] = term
-        return term
-
     def d_update(self, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec=False, g_early=None,
                  before_join=None):
         """train.py:437-469: per D a hinge(+class) step, then a GP step (each D
         on its own stream).  `g_early` (a list): also run g_update's generator
-        loss term through each D right after that D's update, into the list.
-        Discriminators already issued by d_update_early are only joined."""
+        loss term through each D right after that D's update, into the list."""
         nD = len(self.netsD)
-        done = self._early_done
-        self._early_done = {}
-        streams = self._side_streams(nD, fork=False)
-        if streams[0] is not None:
-            main = torch.cuda.current_stream()
-            for i, s in enumerate(streams):
-                if i not in done:
-                    s.wait_stream(main)
+        streams = self._side_streams(nD)
         g_terms = [None] * nD
-        for i, t in done.items():
-            g_terms[i] = t
         order = range(nD)
         if LANE_ORDER == 'rev':
             order = reversed(order)
-        late = self._late_join(g_early)
-        defer = late and DEFER_D and LANE_ORDER == 'rev' and streams[0] is not None
-        self._mark_want = 'D%d %s' % (nD - 1, DEFER_D) if defer else None
-        self._mark_ev = None
         for i in order:
-            if i in done:
-                continue
-            if defer and i < nD - 1 and self._mark_ev is not None:
-                streams[i].wait_event(self._mark_ev)
             with self._on(streams[i]):
                 Fn.stamp('D%d start' % i)
                 self._d_update_one(i, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec)
@@ -338,23 +269,12 @@ class Trainer(object):
                     # final parameters and the fake images: it runs on the lane as soon as
                     # the update is done, while the larger D's update still runs
                     g_terms[i] = self._g_term(i, fake_imgs, sent_emb, class_labels, iter_rec)
-        self._mark_want = None
         if before_join is not None:
             before_join()
-        if not late:
-            self._join(streams)
-            Fn.stamp('d_update joined')
+        self._join(streams)
+        Fn.stamp('d_update joined')
         if g_early is not None:
             g_early[:] = g_terms
-
-    def _phase(self, name):
-        """Phase boundary of the current lane: a diagnostics stamp, and the
-        event the deferred lanes wait on (EEGAN_DEFER_D)."""
-        Fn.stamp(name)
-        if self._mark_want is not None and name == self._mark_want:
-            ev = torch.cuda.Event()
-            ev.record()
-            self._mark_ev = ev
 
     def _d_update_one(self, i, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec):
         """One D of d_update (train.py:439-466)."""
@@ -367,19 +287,19 @@ class Trainer(object):
         else:
             e_real, e_fake, e_unpair = self.d_loss(real_img, fake_img, sent_emb, unpair_sent_emb, netD)
             d_loss = e_real + (e_fake + e_unpair) / 2.0
-        self._phase('D%d loss forward' % i)
+        Fn.stamp('D%d loss forward' % i)
         optD.zero_grad()
         d_loss.backward(inputs=optD.params)
-        self._phase('D%d loss backward' % i)
+        Fn.stamp('D%d loss backward' % i)
         optD.step()
-        self._phase('D%d adam' % i)
+        Fn.stamp('D%d adam' % i)
         d_loss_gp = self.MA_gradient_penalty(real_img, sent_emb, netD, disc_class)
-        self._phase('D%d gp forward + grad' % i)
+        Fn.stamp('D%d gp forward + grad' % i)
         optD.zero_grad()
         d_loss_gp.backward(inputs=optD.params)
-        self._phase('D%d gp backward' % i)
+        Fn.stamp('D%d gp backward' % i)
         optD.step()
-        self._phase('D%d gp adam' % i)
+        Fn.stamp('D%d gp adam' % i)
         if iter_rec:
             self.records['errD_%d/real_sent' % i] = e_real.detach()
             self.records['errD_%d/fake_sent' % i] = e_fake.detach()
@@ -468,10 +388,6 @@ class Trainer(object):
         """train.py:471-502 (`damsm`: the losses from damsm_early, `terms`: the
         per-D terms from d_update(g_early=...); else computed here)."""
         nD = len(self.netsD)
-        late = self._late_join(terms) and bool(terms) and damsm is not None and len(damsm) > 3 and \
-            damsm[3] is not None
-        if late:
-            return self._g_update_late(fake_imgs, damsm, terms, iter_rec)
         streams = self._side_streams(nD + 1)
         if not terms:
             terms = []
@@ -529,40 +445,6 @@ class Trainer(object):
         Fn.stamp('G adam')
         return g_loss.detach()
 
-    def _g_update_late(self, fake_imgs, damsm, terms, iter_rec):
-        """g_update's backward with the discriminator lanes still unjoined
-        (EEGAN_LATE_JOIN): roots = the per-D terms (on their lanes) and the
-        DAMSM image gradient (its lane is joined first: the seed must be ready
-        on this stream); each lane is joined after the backward.  The same
-        gradients as g_loss.backward() of train.py:493-497, summed at the
-        fake images in another order."""
-        nD = len(self.netsD)
-        streams = self._side_streams(nD + 1, fork=False)
-        w_loss, s_loss, a_loss, dfake = damsm
-        main = torch.cuda.current_stream()
-        main.wait_stream(streams[nD])
-        Fn.stamp('g_update DAMSM joined')
-        if iter_rec:
-            self.records['errG/s_loss'] = s_loss.detach()
-            self.records['errG/w_loss'] = w_loss.detach()
-            self.records['errG/a_loss'] = a_loss.detach()
-        if Fn.STAMPS is not None:
-            for i, f in enumerate(fake_imgs):
-                f.register_hook(lambda g, i=i: (Fn.stamp('dfake%d ready' % i), g)[1])
-        self.optimizerG.zero_grad()
-        roots, grads = _backward_roots(terms)
-        torch.autograd.backward(roots + [al for al, _ in dfake], grads + [g for _, g in dfake],
-                                inputs=self.optimizerG.params)
-        Fn.stamp('G backward (D, DAMSM, G)')
-        self._join(streams)
-        g_loss = _term_value(terms[0]).detach()
-        for t in terms[1:]:
-            g_loss = g_loss + _term_value(t).detach()
-        g_loss = g_loss + self.DAMSM_coe * (s_loss + w_loss + a_loss)
-        self.optimizerG.step()
-        Fn.stamp('G adam')
-        return g_loss
-
     # -------------------------------------------------------- inner step --
     def encode_text(self, batch):
         """train.py:169-184: 5 frozen text-encoder calls (captions, 3 attributes, unpaired)."""
@@ -595,17 +477,8 @@ class Trainer(object):
         """One iteration of train.py:163-206 on a device-resident batch."""
         B = self.batch_size
         dev = self.device
-        if Fn.WGRAD_SIDE and self.use_streams:
-            Fn.WGRAD_SIDE_FROM.add(torch.cuda.current_stream().cuda_stream)
         Fn.stamp('start')
-        ahead = emb is None and TEXT_AHEAD and self.use_streams and self.text_encoder is not None
-        if ahead:
-            if self._emb_cur is None:   # a trainer's first step: its own batch, now
-                self._emb_cur = [t.detach().clone() for t in self.encode_text(batch)]
-                self._emb_nxt = [torch.empty_like(t) for t in self._emb_cur]
-            words, sent, attrs, unpair = self._emb_cur
-        else:
-            words, sent, attrs, unpair = emb if emb is not None else self.encode_text(batch)
+        words, sent, attrs, unpair = emb if emb is not None else self.encode_text(batch)
         Fn.stamp('text encode')
         class_labels = None
         if self.disc_class:
@@ -614,15 +487,7 @@ class Trainer(object):
             noise = torch.randn(B, 100, device=dev)
         _, attn_attr_emb = self.attr_enhance(sent, attrs)
         attn_attr_emb = self.attr_enhance.module.attr_merge(attn_attr_emb)
-        gen = getattr(self.netG, 'module', self.netG)
-        g_early_on = G_EARLY and self.use_streams
-        if EARLY_D0 and self.use_streams and len(self.netsD) == 3 and not LATE_JOIN and not DEFER_D:
-            gen._image_hook = lambda i, img: self.d_update_early(
-                i, batch['imgs'], img, sent, unpair, class_labels, iter_rec, [] if g_early_on else None)
-        try:
-            fake_imgs = self.netG(noise, sent, attn_attr_emb)
-        finally:
-            gen._image_hook = None
+        fake_imgs = self.netG(noise, sent, attn_attr_emb)
         Fn.stamp('ATTR + G forward')
         _, _, match_labels = prepare_labels(B, dev)
         cls_ids = batch.get('cls_ids')  # train.py:490 passes class ids to DAMSM_loss even without USE_CLASS
@@ -638,20 +503,8 @@ class Trainer(object):
         self.d_update(batch['imgs'], fake_imgs, sent, unpair, class_labels, iter_rec, g_early=terms,
                       before_join=issue_damsm if early and LANE_ORDER == 'rev' else None)
         damsm = damsm or None
-        if ahead:   # the next batch's embeddings, beside g_update's backward
-            if self._text_lane is None:
-                self._text_lane = new_stream(self.device)
-            lane = self._text_lane
-            lane.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(lane):
-                for d, t in zip(self._emb_nxt, self.encode_text(batch.get('next', batch))):
-                    d.copy_(t)
         g = self.g_update(fake_imgs, sent, words, attn_attr_emb, cls_ids, B, match_labels, batch['cap_lens'],
                           class_labels, iter_rec, damsm=damsm, terms=terms)
-        if ahead:   # every reader of this step's embeddings is joined into this stream by now
-            torch.cuda.current_stream().wait_stream(lane)
-            for c, n in zip(self._emb_cur, self._emb_nxt):
-                c.copy_(n)
         Fn.stamp('end')
         return fake_imgs, g
 

@@ -198,8 +198,6 @@ class ATTR_Enhance(nn.Module):
 class Gen(nn.Module):
     """models.py:183-256."""
 
-    _image_hook = None   # trainer callback (index, image) once an image is final (not a parameter)
-
     def __init__(self, ngf=cfg.GAN.GF_DIM, nz=cfg.GAN.Z_DIM):
         super().__init__()
         self.ngf = ngf
@@ -261,10 +259,6 @@ class Gen(nn.Module):
         x_64, stage_mask = self.SAGB_progress(x_32, [sent, attrs], stage_mask, 64, self.blocks[4], gb[4])
         cum_x_64 = self.cum_64(x_32, x_64)
         img_64 = self.get_image_64(cum_x_64)
-        if self._image_hook is not None and self.stages > 1:
-            # the trainer issues work that reads only img_64 (Dis64's update) on
-            # its own stream lane here, while stages 2-3 continue on this one
-            self._image_hook(0, img_64)
         if self.stages == 1:
             return [img_64]
         x_128, stage_mask = self.SAGB_progress(x_64, [sent, attrs], stage_mask, 128, self.blocks[5], gb[5])

@@ -73,3 +73,12 @@ def rel_l2(a, b):
     a = a.detach().double().reshape(-1).cpu()
     b = b.detach().double().reshape(-1).cpu()
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def conv_knob(monkeypatch, key, value):
+    """Set one conv planner / kernel-path knob inside EEGAN_CONV ("key=value,...",
+    read per launch by csrc/conv.hip's knob()); monkeypatch restores the variable."""
+    cur = os.environ.get('EEGAN_CONV', '')
+    items = [kv for kv in cur.split(',') if kv and kv.split('=')[0] != key]
+    items.append('%s=%s' % (key, value))
+    monkeypatch.setenv('EEGAN_CONV', ','.join(items))

@@ -12,7 +12,7 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
-from _util import rel_l2  # noqa: E402
+from _util import rel_l2, conv_knob  # noqa: E402
 
 
 def _bf(t):
@@ -61,7 +61,7 @@ CONV_CASES = [
 
 
 def test_conv_fast_path_matches_generic(gpu, monkeypatch):
-    """The hoisted-gather kernels (EEGAN_CONV_FAST=1, default: forward,
+    """The hoisted-gather kernels (EEGAN_CONV fast=1, default: forward,
     backward-data, weight gradient) sum the same products in the same order as
     the generic pipelined kernels: bit-identical."""
     Fn, T, _ = _mods()
@@ -76,7 +76,7 @@ def test_conv_fast_path_matches_generic(gpu, monkeypatch):
         dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
         outs = []
         for fast in ('0', '1'):
-            monkeypatch.setenv('EEGAN_CONV_FAST', fast)
+            conv_knob(monkeypatch, 'fast', fast)
             outs.append((Fn.conv_fwd_raw(x, Wt, None, g).float().cpu(),
                          Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape)).float().cpu(),
                          Fn.conv_bwd_weight_raw(x, dz, g, Wt.shape).cpu()))
@@ -87,7 +87,7 @@ def test_conv_fast_path_matches_generic(gpu, monkeypatch):
 def test_conv_thin_path_matches_tile(gpu, monkeypatch):
     """3x3 stride-1 convs with <= 32 output rows (stem, get_image, 32-channel
     256x256 convs and their data gradients) take the weight-stationary thin
-    kernel (EEGAN_CONV_THIN=1, default): same K steps in the same order as the
+    kernel (EEGAN_CONV thin=1, default): same K steps in the same order as the
     tile kernels, so bit-identical; also checked against torch fp32."""
     Fn, T, _ = _mods()
     for N, Cin, H, W, Cout, pad, up2, bias, act in [
@@ -109,7 +109,7 @@ def test_conv_thin_path_matches_tile(gpu, monkeypatch):
         dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
         outs = []
         for thin in ('0', '1'):
-            monkeypatch.setenv('EEGAN_CONV_THIN', thin)
+            conv_knob(monkeypatch, 'thin', thin)
             o = [Fn.conv_fwd_raw(x, Wt, b, g, act=act).float().cpu()]
             if not up2:
                 o.append(Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape)).float().cpu())
@@ -140,7 +140,7 @@ def test_conv_thin_wgrad(gpu, monkeypatch):
         x, dz = _nhwc(xl, gpu), _nhwc(dzl, gpu)
         outs = []
         for thin in ('0', '1'):
-            monkeypatch.setenv('EEGAN_CONV_THIN', thin)
+            conv_knob(monkeypatch, 'thin', thin)
             outs.append(Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, 3, 3)).cpu())
         wr = torch.zeros(Cout, Cin, 3, 3, requires_grad=True)
         F.conv2d(xl, wr, None, 1, 1).backward(dzl)
@@ -150,11 +150,11 @@ def test_conv_thin_wgrad(gpu, monkeypatch):
 
 def test_conv_thin_wgrad_channel_groups(gpu, monkeypatch):
     """The thin weight-gradient kernel for up to 64 output channels, in
-    8-channel groups on the grid's y axis (EEGAN_WGRAD_THIN_MAXK): against
+    8-channel groups on the grid's y axis (EEGAN_CONV wgrad_thin_maxk): against
     torch fp32 and the tile path; a ragged last group (Cout % 8 != 0) and a
     padded dy row (its channels past Cout are never read into written rows)."""
     Fn, T, _ = _mods()
-    monkeypatch.setenv('EEGAN_WGRAD_THIN_MAXK', '64')
+    conv_knob(monkeypatch, 'wgrad_thin_maxk', '64')
     for N, Cin, H, W, Cout in [(2, 32, 8, 64, 32), (1, 64, 12, 128, 64), (2, 32, 4, 64, 36), (2, 28, 8, 64, 16),
                                (1, 64, 8, 64, 20)]:
         torch.manual_seed(N + Cin + H + Cout)
@@ -164,7 +164,7 @@ def test_conv_thin_wgrad_channel_groups(gpu, monkeypatch):
         x, dz = _nhwc(xl, gpu), _nhwc(dzl, gpu)
         outs = []
         for thin in ('0', '1'):
-            monkeypatch.setenv('EEGAN_CONV_THIN', thin)
+            conv_knob(monkeypatch, 'thin', thin)
             outs.append(Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, 3, 3)).cpu())
         wr = torch.zeros(Cout, Cin, 3, 3, requires_grad=True)
         F.conv2d(xl, wr, None, 1, 1).backward(dzl)
@@ -174,14 +174,14 @@ def test_conv_thin_wgrad_channel_groups(gpu, monkeypatch):
 
 def test_splitk_reduce_vector_path_bit_identical(gpu, monkeypatch):
     """The split-K reduce's 4-channel vector path (default) against the scalar
-    path (EEGAN_CONV_RED_VEC4=0): same summation order, so torch.equal, over
+    path (EEGAN_CONV red_vec4=0): same summation order, so torch.equal, over
     forward (bias, act, residual + gain) and backward-data (activation gate,
     half-resolution residual of resD's pooled shortcut) epilogues; odd channel
-    counts take the scalar path in both runs.  EEGAN_CONV_TARGET forces the
+    counts take the scalar path in both runs.  EEGAN_CONV target= forces the
     K split on these small grids."""
     Fn, T, _ = _mods()
-    monkeypatch.setenv('EEGAN_CONV_TARGET', '4096')
-    monkeypatch.setenv('EEGAN_CONV_MINK', '2')
+    conv_knob(monkeypatch, 'target', '4096')
+    conv_knob(monkeypatch, 'mink', '2')
     lrelu = Fn.ACT_CODES['lrelu']
     for N, Cin, H, W, Cout, k, st, pad in [(2, 256, 4, 4, 128, 3, 1, 1), (2, 96, 8, 8, 64, 4, 2, 1),
                                             (3, 128, 6, 6, 36, 3, 1, 1), (2, 64, 8, 8, 9, 4, 2, 1),
@@ -199,7 +199,7 @@ def test_splitk_reduce_vector_path_bit_identical(gpu, monkeypatch):
         halfres = _nhwc(torch.randn(N, Cin, H // 2, W // 2), gpu)
         outs = []
         for vec in ('0', '1'):
-            monkeypatch.setenv('EEGAN_CONV_RED_VEC4', vec)
+            conv_knob(monkeypatch, 'red_vec4', vec)
             o = [Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, res=res, gamma=gam).float().cpu(),
                  Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, out_f32=True).cpu(),
                  Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), gate=gate, gate_act=lrelu).float().cpu(),
@@ -209,60 +209,17 @@ def test_splitk_reduce_vector_path_bit_identical(gpu, monkeypatch):
             assert torch.equal(a, c)
 
 
-def test_splitk_last_workgroup_finish_bit_identical(gpu, monkeypatch):
-    """Split-K tiles reduced by their last-arriving workgroup (ticket counters,
-    EEGAN_CONV_SPLITK_FUSED=1; off by default, slower) against the separate
-    reduce kernel (=0, default): the same per-item sums in split order, so torch.equal -- vector and
-    scalar items, forward with bias / act / residual + gain and fp32 out,
-    backward-data with gate, the half-resolution residual and stride-2 parity
-    classes.  Each fused call runs three times: the counters reset themselves,
-    so repeated launches on the same ticket runs stay identical."""
-    Fn, T, _ = _mods()
-    monkeypatch.setenv('EEGAN_CONV_TARGET', '4096')
-    monkeypatch.setenv('EEGAN_CONV_MINK', '2')
-    lrelu = Fn.ACT_CODES['lrelu']
-    for N, Cin, H, W, Cout, k, st, pad in [(2, 256, 4, 4, 128, 3, 1, 1), (2, 96, 8, 8, 64, 4, 2, 1),
-                                            (3, 128, 6, 6, 36, 3, 1, 1), (2, 64, 8, 8, 9, 4, 2, 1),
-                                            (16, 512, 4, 4, 512, 3, 1, 1)]:
-        torch.manual_seed(N * Cin + Cout + 1)
-        g = Fn.Geom(Cout, k, k, st, pad, pad, 0)
-        x = _nhwc(torch.randn(N, Cin, H, W), gpu)
-        Wt = (torch.randn(Cout, Cin, k, k) * 0.05).to(gpu)
-        b = torch.randn(Cout).to(gpu)
-        gam = torch.tensor([0.7]).to(gpu)
-        Ho, Wo = g.out_hw(H, W)
-        res = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
-        dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
-        gate = _nhwc(torch.randn(N, Cin, H, W), gpu)
-        halfres = _nhwc(torch.randn(N, Cin, H // 2, W // 2), gpu)
-
-        def run():
-            return [Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, res=res, gamma=gam).float().cpu(),
-                    Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, out_f32=True).cpu(),
-                    Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), gate=gate, gate_act=lrelu).float().cpu(),
-                    Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), res=halfres, res_up2=1,
-                                         res_scale=0.25).float().cpu()]
-        for vec in ('0', '1'):
-            monkeypatch.setenv('EEGAN_CONV_RED_VEC4', vec)
-            monkeypatch.setenv('EEGAN_CONV_SPLITK_FUSED', '0')
-            ref = run()
-            monkeypatch.setenv('EEGAN_CONV_SPLITK_FUSED', '1')
-            for _ in range(3):
-                for a, c in zip(ref, run()):
-                    assert torch.equal(a, c), (N, Cin, Cout, k, vec)
-
-
 @pytest.mark.parametrize('target', ['512', '4096'])
 def test_conv_wide_stages_bit_identical(gpu, monkeypatch, target):
     """Wide pair stages (one 64-channel stage of whole 128-B lines per K-step
-    pair, EEGAN_CONV_WIDE=1, default) against two 32-channel stages (=0): same
+    pair, EEGAN_CONV wide=1, default) against two 32-channel stages (=0): same
     K order and MFMA sequence, so torch.equal -- forward with bias / act /
     residual + gain and fp32 out, backward-data with gate, the
     half-resolution residual and stride-2 parity classes, channel counts with
     padded 64-channel pairs (72, 200), with and without split-K."""
     Fn, T, _ = _mods()
-    monkeypatch.setenv('EEGAN_CONV_TARGET', target)
-    monkeypatch.setenv('EEGAN_CONV_MINK', '2')
+    conv_knob(monkeypatch, 'target', target)
+    conv_knob(monkeypatch, 'mink', '2')
     lrelu = Fn.ACT_CODES['lrelu']
     for N, Cin, H, W, Cout, k, st, pad in [(2, 64, 16, 16, 128, 3, 1, 1), (3, 128, 9, 11, 64, 3, 1, 1),
                                             (2, 96, 16, 16, 256, 4, 2, 1), (2, 64, 12, 12, 200, 1, 1, 0),
@@ -282,7 +239,7 @@ def test_conv_wide_stages_bit_identical(gpu, monkeypatch, target):
         halfres = _nhwc(torch.randn(N, Cin, H // 2, W // 2), gpu) if H % 2 == 0 and W % 2 == 0 else None
         outs = []
         for wide in ('0', '1'):
-            monkeypatch.setenv('EEGAN_CONV_WIDE', wide)
+            conv_knob(monkeypatch, 'wide', wide)
             o = [Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, res=res, gamma=gam).float().cpu(),
                  Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, out_f32=True).cpu(),
                  Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), gate=gate, gate_act=lrelu).float().cpu()]
@@ -297,13 +254,13 @@ def test_conv_wide_stages_bit_identical(gpu, monkeypatch, target):
 def test_conv_s2bwd_halo_bit_identical(gpu, monkeypatch):
     """4x4 / stride-2 / pad-1 data gradients with <= 64 input channels (resD
     block0's and block1's conv_r[0]) take the shared-halo parity-class kernel
-    (EEGAN_CONV_S2B=1, default): same K order as the unsplit tile kernel
-    (EEGAN_CONV_TARGET=1 keeps it unsplit), so torch.equal -- plain, gated and
+    (EEGAN_CONV s2b=1, default): same K order as the unsplit tile kernel
+    (EEGAN_CONV target=1 keeps it unsplit), so torch.equal -- plain, gated and
     with the half-resolution pooled-shortcut residual; 16..64 input (one or two
     32-row slices) and 32/64/128 output channels, one- and multi-tile grids;
     also against torch fp32."""
     Fn, T, _ = _mods()
-    monkeypatch.setenv('EEGAN_CONV_TARGET', '1')
+    conv_knob(monkeypatch, 'target', '1')
     lrelu = Fn.ACT_CODES['lrelu']
     for N, Cin, H, W, Cout in [(2, 32, 64, 64, 64), (3, 16, 8, 64, 32), (1, 24, 16, 128, 64),
                                (2, 32, 24, 192, 32), (5, 32, 8, 64, 64),
@@ -319,7 +276,7 @@ def test_conv_s2bwd_halo_bit_identical(gpu, monkeypatch):
         halfres = _nhwc(torch.randn(N, Cin, H // 2, W // 2), gpu)
         outs = []
         for s2b in ('0', '1'):
-            monkeypatch.setenv('EEGAN_CONV_S2B', s2b)
+            conv_knob(monkeypatch, 's2b', s2b)
             outs.append([Fn.conv_bwd_data_raw(dz, Wt.to(gpu), g, (N, Cin, H, W)).float().cpu(),
                          Fn.conv_bwd_data_raw(dz, Wt.to(gpu), g, (N, Cin, H, W), gate=gate,
                                               gate_act=lrelu).float().cpu(),
@@ -335,14 +292,14 @@ def test_conv_s2bwd_halo_bit_identical(gpu, monkeypatch):
 def test_conv_1x1_stream_bit_identical(gpu, monkeypatch):
     """1x1 convs with <= 256 packed K columns (resD's conv_s, get_mask's
     100 -> 1 projection) and their data gradients take the streaming pointwise
-    kernel (EEGAN_CONV_1X1=1, default): same K order as the unsplit tile kernel
-    (EEGAN_CONV_TARGET=1), so torch.equal -- forward with bias / act / residual
+    kernel (EEGAN_CONV 1x1=1, default): same K order as the unsplit tile kernel
+    (EEGAN_CONV target=1), so torch.equal -- forward with bias / act / residual
     + gain and fp32 out, backward-data plain, gated and with the
     half-resolution residual; channel counts that straddle a 16-B chunk (100),
     one-channel operands (the packed 8-channel K row) and several output-row
     slices per pixel group; also against torch fp32."""
     Fn, T, _ = _mods()
-    monkeypatch.setenv('EEGAN_CONV_TARGET', '1')
+    conv_knob(monkeypatch, 'target', '1')
     lrelu = Fn.ACT_CODES['lrelu']
     for N, Cin, H, W, Cout in [(2, 32, 16, 24, 64), (3, 64, 8, 8, 128), (2, 100, 12, 10, 1), (2, 1, 8, 8, 100),
                                (2, 256, 4, 4, 512), (1, 128, 6, 6, 256), (2, 24, 5, 7, 40), (2, 200, 4, 4, 72)]:
@@ -362,7 +319,7 @@ def test_conv_1x1_stream_bit_identical(gpu, monkeypatch):
         Wd = Wt.to(gpu)
         outs = []
         for on in ('0', '1'):
-            monkeypatch.setenv('EEGAN_CONV_1X1', on)
+            conv_knob(monkeypatch, '1x1', on)
             o = [Fn.conv_fwd_raw(x, Wd, b, g, act=lrelu, res=res, gamma=gam).float().cpu(),
                  Fn.conv_fwd_raw(x, Wd, b, g, act=lrelu, out_f32=True).cpu(),
                  Fn.conv_fwd_raw(x, Wd, None, g).float().cpu(),
@@ -382,7 +339,7 @@ def test_conv_1x1_stream_bit_identical(gpu, monkeypatch):
 
 @pytest.mark.parametrize('target', ['1', '512'])
 def test_conv_staged_epilogue_bit_identical(gpu, monkeypatch, target):
-    """The tile kernel's LDS-staged epilogue (EEGAN_CONV_STAGE_EPI=1, default:
+    """The tile kernel's LDS-staged epilogue (EEGAN_CONV stage_epi=1, default:
     whole 16-B runs of 8 channels per thread) against the direct MFMA-layout
     epilogue (=0): same arithmetic in the same order, so torch.equal --
     forward with bias / act / residual + gain, backward-data with the gate,
@@ -390,7 +347,7 @@ def test_conv_staged_epilogue_bit_identical(gpu, monkeypatch, target):
     shape (16..128 rows x 64..256 pixels), ragged pixel tails; split-K and
     unaligned cases keep the direct epilogue in both runs."""
     Fn, T, _ = _mods()
-    monkeypatch.setenv('EEGAN_CONV_TARGET', target)
+    conv_knob(monkeypatch, 'target', target)
     lrelu = Fn.ACT_CODES['lrelu']
     for N, Cin, H, W, Cout, k, st, pad in [(2, 64, 16, 16, 128, 3, 1, 1), (3, 128, 9, 11, 64, 3, 1, 1),
                                             (2, 96, 16, 16, 256, 4, 2, 1), (2, 64, 12, 12, 200, 1, 1, 0),
@@ -411,7 +368,7 @@ def test_conv_staged_epilogue_bit_identical(gpu, monkeypatch, target):
         halfres = _nhwc(torch.randn(N, Cin, H // 2, W // 2), gpu) if H % 2 == 0 and W % 2 == 0 else None
         outs = []
         for on in ('0', '1'):
-            monkeypatch.setenv('EEGAN_CONV_STAGE_EPI', on)
+            conv_knob(monkeypatch, 'stage_epi', on)
             o = [Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, res=res, gamma=gam).float().cpu(),
                  Fn.conv_fwd_raw(x, Wt, None, g).float().cpu(),
                  Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape)).float().cpu(),
@@ -437,12 +394,12 @@ def _nhwc_nan_padded(x, dev):
 def test_conv_ragged_channels_lds_path(gpu, monkeypatch):
     """Operands whose channel count is not a multiple of 8 (get_mask's 100
     channels, models.py:35-41) take the LDS-DMA kernels (hoisted-gather fast
-    kernel, or conv_glds_kernel with EEGAN_CONV_FAST=0) with the straddling
-    16-B chunk masked per K-step (EEGAN_CONV_GLDS_RAGGED=1, default) instead of
+    kernel, or conv_glds_kernel with EEGAN_CONV fast=0) with the straddling
+    16-B chunk masked per K-step (EEGAN_CONV glds_ragged=1, default) instead of
     the register-staged kernel (=0): same K order, so torch.equal -- even with
     NaN bits in the padding channels -- and against torch fp32."""
     Fn, T, _ = _mods()
-    monkeypatch.setenv('EEGAN_CONV_TARGET', '1')
+    conv_knob(monkeypatch, 'target', '1')
     for N, Cin, H, W, Cout, k, st, pad in [(2, 64, 16, 16, 100, 3, 1, 1), (2, 100, 12, 12, 64, 3, 1, 1),
                                             (2, 20, 16, 16, 36, 4, 2, 1), (1, 128, 8, 8, 100, 3, 1, 1),
                                             (2, 44, 9, 11, 52, 3, 1, 1)]:
@@ -457,8 +414,8 @@ def test_conv_ragged_channels_lds_path(gpu, monkeypatch):
         dz = _nhwc_nan_padded(dzl, gpu)
         outs = []
         for rag, fast in (('0', '1'), ('1', '0'), ('1', '1')):
-            monkeypatch.setenv('EEGAN_CONV_GLDS_RAGGED', rag)
-            monkeypatch.setenv('EEGAN_CONV_FAST', fast)
+            conv_knob(monkeypatch, 'glds_ragged', rag)
+            conv_knob(monkeypatch, 'fast', fast)
             outs.append([Fn.conv_fwd_raw(x, Wd, None, g).float().cpu(),
                          Fn.conv_bwd_data_raw(dz, Wd, g, (N, Cin, H, W)).float().cpu()])
         for other in outs[1:]:
@@ -711,12 +668,12 @@ def test_elementwise_ops(gpu):
 
 def test_wgrad_staged_epilogue_bit_identical(gpu, monkeypatch):
     """Unsplit weight gradients through the LDS-staged dW epilogue
-    (EEGAN_WGRAD_STAGE_EPI=1, default: 16-B read-add-write runs) equal the
+    (EEGAN_CONV wgrad_stage_epi=1, default: 16-B read-add-write runs) equal the
     direct epilogue bit for bit, fresh and accumulated into an existing
     gradient; the DiscCond-head shapes (4x4 grids, 768 / 1024 channels) and
     ragged tiles (Cout, K not multiples of the tile)."""
     Fn, T, _ = _mods()
-    monkeypatch.setenv('EEGAN_WGRAD_TARGET', '1')   # one split: the direct dW path
+    conv_knob(monkeypatch, 'wgrad_target', '1')   # one split: the direct dW path
     for N, Cin, H, W, Cout, k, st, pad in [(8, 768, 4, 4, 1024, 3, 1, 1), (8, 1024, 4, 4, 512, 4, 4, 0),
                                             (4, 96, 8, 8, 72, 3, 1, 1), (2, 64, 16, 16, 200, 4, 2, 1),
                                             (4, 256, 8, 8, 48, 1, 1, 0)]:
@@ -727,7 +684,7 @@ def test_wgrad_staged_epilogue_bit_identical(gpu, monkeypatch):
         dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
         outs = []
         for v in ('0', '1'):
-            monkeypatch.setenv('EEGAN_WGRAD_STAGE_EPI', v)
+            conv_knob(monkeypatch, 'wgrad_stage_epi', v)
             dW = torch.full((Cout, Cin, k, k), 0.5, device=gpu).contiguous(memory_format=torch.channels_last)
             Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, k, k), out=dW)
             outs.append((Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, k, k)).cpu(), dW.cpu()))
@@ -740,7 +697,7 @@ def test_wgrad_staged_epilogue_bit_identical(gpu, monkeypatch):
 
 def test_wgrad_xcd_remap_bit_identical(gpu, monkeypatch):
     """Weight-gradient tiles remapped so one (co tile, split)'s k tiles share an
-    XCD (EEGAN_WGRAD_XCD=1, default) compute the same tiles: torch.equal with
+    XCD (EEGAN_CONV wgrad_xcd=1, default) compute the same tiles: torch.equal with
     the plain block order, split and unsplit, fresh and accumulated."""
     Fn, T, _ = _mods()
     for N, Cin, H, W, Cout, k, st, pad in [(16, 128, 32, 32, 128, 3, 1, 1), (8, 64, 64, 64, 64, 3, 1, 1),
@@ -752,7 +709,7 @@ def test_wgrad_xcd_remap_bit_identical(gpu, monkeypatch):
         dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
         outs = []
         for v in ('0', '1'):
-            monkeypatch.setenv('EEGAN_WGRAD_XCD', v)
+            conv_knob(monkeypatch, 'wgrad_xcd', v)
             dW = torch.full((Cout, Cin, k, k), 0.25, device=gpu).contiguous(memory_format=torch.channels_last)
             Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, k, k), out=dW)
             outs.append((Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, k, k)).cpu(), dW.cpu()))
@@ -761,12 +718,12 @@ def test_wgrad_xcd_remap_bit_identical(gpu, monkeypatch):
 
 
 def test_wgrad_quad_slab_bit_identical(gpu, monkeypatch):
-    """Split weight gradients written as co-quad slabs (EEGAN_WGRAD_QUAD=1,
+    """Split weight gradients written as co-quad slabs (EEGAN_CONV wgrad_quad=1,
     default: one 16-B store per lane) reduce to the same bits as the row-major
     slabs: the column sums visit the same splits in the same order.  Covers
     accumulation into an existing gradient and Cout % 4 != 0 (row-major)."""
     Fn, T, _ = _mods()
-    monkeypatch.setenv('EEGAN_WGRAD_QUAD_MINK', '0')   # quad slabs at every K (default: K > 1024)
+    conv_knob(monkeypatch, 'wgrad_quad_mink', '0')   # quad slabs at every K (default: K > 1024)
     for N, Cin, H, W, Cout, k, st, pad in [(4, 64, 32, 32, 64, 3, 1, 1), (2, 128, 16, 16, 256, 4, 2, 1),
                                             (8, 32, 64, 64, 36, 3, 1, 1), (16, 256, 8, 8, 512, 3, 1, 1)]:
         torch.manual_seed(Cin + H + Cout)
@@ -777,8 +734,8 @@ def test_wgrad_quad_slab_bit_identical(gpu, monkeypatch):
         outs = []
         # row-major slabs with direct stores / co-quad slabs / row-major slabs through the LDS-staged epilogue
         for q, stg in (('0', '1'), ('1', '1'), ('0', '2')):
-            monkeypatch.setenv('EEGAN_WGRAD_STAGE_EPI', stg)
-            monkeypatch.setenv('EEGAN_WGRAD_QUAD', q)
+            conv_knob(monkeypatch, 'wgrad_stage_epi', stg)
+            conv_knob(monkeypatch, 'wgrad_quad', q)
             dW = torch.ones(Cout, Cin, k, k, device=gpu).contiguous(memory_format=torch.channels_last)
             Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, k, k), out=dW)
             outs.append((Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, k, k)).cpu(), dW.cpu()))
@@ -792,36 +749,28 @@ def test_wgrad_quad_slab_bit_identical(gpu, monkeypatch):
 
 
 @pytest.mark.parametrize('P', [64, 4096, 1 << 18])
-def test_dot_in_kernel_finish(gpu, monkeypatch, P):
-    """<g, h> partials finished by the last-arriving block (ticket) == the
-    separate dot_final launch (EEGAN_DOT_FUSED=0) to fp32 rounding of a
-    different summation tree; repeated calls (each launch resets its ticket),
-    the scale-add backward's fused <g, h> accumulated into a sink, and the
-    fp64 sum of the bf16 inputs."""
+def test_dot_partials_finish(gpu, P):
+    """<g, h> from per-block partials and the fixed-order dot_final launch:
+    deterministic over repeated calls, the scale-add backward's fused <g, h>
+    accumulated into a sink, against the fp64 sum of the bf16 inputs."""
     Fn, T, _ = _mods()
     torch.manual_seed(11)
     C = 40
     x = _nhwc(_bf(torch.randn(1, C, P // 64, 64)), gpu)
     y = _nhwc(_bf(torch.randn(1, C, P // 64, 64)), gpu)
     ref = (x.double() * y.double()).sum().item()
-    outs = {}
-    for fused in ('0', '1'):
-        monkeypatch.setenv('EEGAN_DOT_FUSED', fused)
-        vals = [Fn._dot_raw(x, y).item() for _ in range(3)]
-        assert vals[0] == vals[1] == vals[2], vals       # deterministic, tickets reset
-        outs[fused] = vals[0]
-        g = torch.zeros(1, device=gpu)
-        gm = torch.tensor([0.5], device=gpu)
-        d = torch.empty_like(x)
-        ws = T.workspace(Fn.ops.dot_workspace(), gpu)
-        for _ in range(2):   # accumulate twice into the sink
-            Fn.ops.scale_dot(x.data_ptr(), Fn.ld_of(x), y.data_ptr(), Fn.ld_of(y), gm.data_ptr(), 1.0, P, C,
-                             d.data_ptr(), Fn.ld_of(d), ws.data_ptr(), g.data_ptr(), 1, 0, 0.2, Fn.stream())
-        assert abs(g.item() - 2 * ref) <= 1e-5 * abs(2 * ref) + 1e-3, (fused, g.item(), ref)
-        assert rel_l2(d.float().cpu(), 0.5 * x.float().cpu()) < 1e-2
-    scale = max(abs(ref), 1.0)
-    assert abs(outs['1'] - outs['0']) <= 1e-5 * scale, outs
-    assert abs(outs['1'] - ref) <= 1e-5 * scale, (outs, ref)
+    vals = [Fn._dot_raw(x, y).item() for _ in range(3)]
+    assert vals[0] == vals[1] == vals[2], vals
+    g = torch.zeros(1, device=gpu)
+    gm = torch.tensor([0.5], device=gpu)
+    d = torch.empty_like(x)
+    ws = T.workspace(Fn.ops.dot_workspace(), gpu)
+    for _ in range(2):   # accumulate twice into the sink
+        Fn.ops.scale_dot(x.data_ptr(), Fn.ld_of(x), y.data_ptr(), Fn.ld_of(y), gm.data_ptr(), 1.0, P, C,
+                         d.data_ptr(), Fn.ld_of(d), ws.data_ptr(), g.data_ptr(), 1, 0, 0.2, Fn.stream())
+    assert abs(g.item() - 2 * ref) <= 1e-5 * abs(2 * ref) + 1e-3, (g.item(), ref)
+    assert rel_l2(d.float().cpu(), 0.5 * x.float().cpu()) < 1e-2
+    assert abs(vals[0] - ref) <= 1e-5 * max(abs(ref), 1.0), (vals, ref)
 
 
 def test_linear_and_attr(gpu):

@@ -8,7 +8,7 @@ module constants such as EEGAN_DAMSM_EARLY are read at import and cannot be
 switched this way).  The order of the settings rotates every repetition (the
 clock drifts over a run: a fixed order biases the comparison).
 
-    python tools/ab_inproc.py "EEGAN_CONV_MINK=32" ["EEGAN_CONV_MINK=8" ...] [--reps 3] [--steps 20]
+    python tools/ab_inproc.py "EEGAN_CONV=mink=32" ["EEGAN_CONV=mink=8" ...] [--reps 3] [--steps 20]
 """
 import argparse
 import gc
