@@ -34,7 +34,13 @@ namespace {
 
 constexpr int PEER_MAXW = 16;
 constexpr long OFF_CTR = 256, OFF_ERR = 264, OFF_DATA = 512;
-constexpr unsigned long long WAIT_TICKS = 200000000ull;  // 2 s at 100 MHz
+// bounded wait for the peers' slices: long enough for host-side skew between
+// ranks (a checkpoint save or an evaluation on one rank while the others wait
+// in their next step), short enough that a dead peer ends the job: on timeout
+// the error word is set and the result is poisoned with NaN (visible in the BN
+// statistics at once); the trainer checks the error word and raises
+// (eegan_hip.peer.PeerAllReduce.check, Trainer.check_collectives)
+constexpr unsigned long long WAIT_TICKS = 3000000000ull;  // 30 s at 100 MHz
 
 struct PeerSet {
   char* base[PEER_MAXW];
@@ -53,7 +59,11 @@ __global__ __launch_bounds__(256) void peer_allreduce_kernel(double* t, int n, i
   char* own = ps.base[rank];
   unsigned long long* ctr = reinterpret_cast<unsigned long long*>(own + OFF_CTR);
   __shared__ unsigned long long s_ep;
-  if (tid == 0) s_ep = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1ull;
+  __shared__ int s_timeout;
+  if (tid == 0) {
+    s_ep = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1ull;
+    s_timeout = 0;
+  }
   __syncthreads();
   const unsigned long long ep = s_ep;
   const int par = (int)(ep & 1ull);
@@ -76,6 +86,7 @@ __global__ __launch_bounds__(256) void peer_allreduce_kernel(double* t, int n, i
       if (wall_clock64() - t0 > WAIT_TICKS) {
         __hip_atomic_store(reinterpret_cast<unsigned*>(own + OFF_ERR), 1u + (unsigned)tid, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+        s_timeout = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -83,8 +94,10 @@ __global__ __launch_bounds__(256) void peer_allreduce_kernel(double* t, int n, i
   }
   __syncthreads();
 
-  // fixed-order combine: 0 + m_0 + m_1 + ... + m_{world-1}
-  for (int i = tid; i < n; i += 256) {
+  // fixed-order combine: 0 + m_0 + m_1 + ... + m_{world-1}; NaN when a peer never arrived
+  const bool poison = s_timeout != 0;
+  for (int i = tid; i < n && poison; i += 256) t[i] = __builtin_nan("");
+  for (int i = tid; i < n && !poison; i += 256) {
     double acc = 0.0;
     for (int q = 0; q < world; ++q) {
       const unsigned long long* src = reinterpret_cast<const unsigned long long*>(slot_at(own, par, q, cap)) + i;

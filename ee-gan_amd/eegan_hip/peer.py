@@ -116,6 +116,15 @@ class PeerAllReduce(object):
     def timed_out(self):
         return max([r.timed_out() for r in self.regions.values()] or [0])
 
+    def check(self):
+        """Raise when a reduction gave up waiting for a peer since the last
+        check (its output was poisoned with NaN; the ranks' epochs no longer
+        agree, so training cannot continue).  Synchronises the device."""
+        t = self.timed_out()
+        if t:
+            raise RuntimeError('eegan_hip.peer: a SyncBN peer-write all-reduce timed out waiting for rank %d '
+                               '(a rank died or stalled > 30 s); its BN statistics are NaN' % (t - 1))
+
     def close(self):
         for r in self.regions.values():
             r.close()

@@ -350,10 +350,10 @@ class Trainer(object):
             dfake = None
             if grad_early:
                 leaves = (img, attr) if attr is not attr_emb else (img,)
-                grads = torch.autograd.grad(self.DAMSM_coe * (s + w + a), leaves)
+                grads = torch.autograd.grad(self.DAMSM_coe * (s + w + a), leaves, allow_unused=True)
                 w, s, a = w.detach(), s.detach(), a.detach()
                 Fn.stamp('DAMSM backward')
-                dfake = list(zip(leaves, grads))   # (alias, gradient there) pairs
+                dfake = [(al, g) for al, g in zip(leaves, grads) if g is not None]   # (alias, gradient there)
         return w, s, a, dfake
 
     def _g_term(self, i, fake_imgs, sent_emb, class_labels, iter_rec):
@@ -445,6 +445,24 @@ class Trainer(object):
         Fn.stamp('G adam')
         return g_loss.detach()
 
+    # ---------------------------------------------------- failure checks --
+    CHECK_EVERY = 64   # steps between checks of the collectives' error state (each check synchronises)
+
+    @staticmethod
+    def check_collectives():
+        """Raise if a SyncBN peer-write reduction timed out (EEGAN_SYNCBN_PEER):
+        called every CHECK_EVERY steps / replays and before state is saved."""
+        red = Fn.SYNC_BN_ALLREDUCE
+        if red is not None and hasattr(red, 'check'):
+            red.check()
+
+    def state_dict(self):
+        """Optimizer state for checkpoints (collectives checked first: a
+        desynchronised rank must not write a checkpoint)."""
+        self.check_collectives()
+        return {'optimizerG': self.optimizerG.state_dict(),
+                'optimizerDs': [o.state_dict() for o in self.optimizerDs]}
+
     # -------------------------------------------------------- inner step --
     def encode_text(self, batch):
         """train.py:169-184: 5 frozen text-encoder calls (captions, 3 attributes, unpaired)."""
@@ -506,6 +524,9 @@ class Trainer(object):
         g = self.g_update(fake_imgs, sent, words, attn_attr_emb, cls_ids, B, match_labels, batch['cap_lens'],
                           class_labels, iter_rec, damsm=damsm, terms=terms)
         Fn.stamp('end')
+        self._steps = getattr(self, '_steps', 0) + 1
+        if self._steps % self.CHECK_EVERY == 0 and not torch.cuda.is_current_stream_capturing():
+            self.check_collectives()
         return fake_imgs, g
 
 
@@ -593,6 +614,9 @@ class StepGraph(object):
     DEPTH = int(os.environ.get('EEGAN_REPLAY_DEPTH', '1'))
 
     def replay(self):
+        self._n = getattr(self, '_n', 0) + 1
+        if self._n % Trainer.CHECK_EVERY == 0:
+            Trainer.check_collectives()
         if self.DEPTH > 0:
             q = getattr(self, '_inflight', None)
             if q is None:

@@ -873,8 +873,13 @@ def test_damsm_grad_early_trains_attr_enhance(gpu, monkeypatch):
     tag = 'step'
     B, W, ncls, disc_class, stages, sb = STEP_CASES[tag]
     grads = {}
-    for early in (True, False):
-        monkeypatch.setattr(TR, 'DAMSM_GRAD_EARLY', early)
+    orig_loss = TR.Trainer.DAMSM_loss
+
+    def dropped(self, fake_imgs, sent_emb, words_embs, attrs_emb, *a, **k):   # round 3's bug: no a_loss gradient
+        return orig_loss(self, fake_imgs, sent_emb, words_embs, attrs_emb.detach(), *a, **k)
+    for early in (True, False, 'dropped'):
+        monkeypatch.setattr(TR, 'DAMSM_GRAD_EARLY', bool(early))
+        monkeypatch.setattr(TR.Trainer, 'DAMSM_loss', dropped if early == 'dropped' else orig_loss)
         G = _load(models.Gen(W, 100), tag + '_g', sb, gpu)
         A = _load(models.ATTR_Enhance(), tag + '_a', sb + 1, gpu)
         makers = [lambda: models.Dis64(W), lambda: models.Dis128(W), lambda: models.Dis256(W, disc_class, ncls)]
@@ -891,12 +896,16 @@ def test_damsm_grad_early_trains_attr_enhance(gpu, monkeypatch):
         T.train_step(dbatch, noise=batch['noise'].to(gpu), emb=emb)
         torch.cuda.synchronize()
         grads[early] = {k: p.grad.detach().float().cpu().clone() for k, p in A.named_parameters()}
-    worst = 0.0
+    worst = share = 0.0
     for k, g_joint in grads[False].items():
         if k == 'attr_key.bias':   # true gradient identically zero (softmax shift invariance)
             continue
-        e = float((grads[True][k] - g_joint).norm() / g_joint.norm().clamp_min(1e-30))
-        worst = max(worst, e)
+        nrm = g_joint.norm().clamp_min(1e-30)
+        worst = max(worst, float((grads[True][k] - g_joint).norm() / nrm))
+        share = max(share, float((grads['dropped'][k] - g_joint).norm() / nrm))
     _LOG.append(('damsm_grad_early/attr_enhance worst rel_l2 vs joint backward', worst))
-    print('PARITY damsm_grad_early attr_enhance grads vs joint backward: worst rel_l2 %.3e' % worst)
+    _LOG.append(('damsm_grad_early/attr_enhance a_loss share (rel_l2 without it)', share))
+    print('PARITY damsm_grad_early attr_enhance grads vs joint backward: worst rel_l2 %.3e; without the a_loss '
+          'gradient they would differ by %.3e' % (worst, share))
     assert worst < 1e-4, worst
+    assert share > 1e-3, share   # the check is sensitive to the dropped term

@@ -74,3 +74,23 @@ def test_torchrun_ranks_join_at_import(tmp_path, auto):
         assert sorted(x['rank'] for x in res) == [0, 1]
     else:
         assert all(not x['initialized'] and x['raised'] for x in res), res
+
+
+def test_peer_timeout_raises_on_trainer_path(monkeypatch):
+    """A SyncBN peer-write reduction that gave up waiting for a peer (its
+    output poisoned with NaN, csrc/peer.hip) must stop training: the trainer's
+    periodic check and its state_dict raise."""
+    from eegan_hip import functional as Fn
+    from eegan_hip.peer import PeerAllReduce
+    from eegan_hip.trainer import Trainer
+    red = PeerAllReduce.__new__(PeerAllReduce)
+    red.regions = {}
+    monkeypatch.setattr(PeerAllReduce, 'timed_out', lambda self: 0)
+    monkeypatch.setattr(Fn, 'SYNC_BN_ALLREDUCE', red)
+    Trainer.check_collectives()   # healthy: no error
+    monkeypatch.setattr(PeerAllReduce, 'timed_out', lambda self: 1 + 3)   # gave up on rank 3
+    with pytest.raises(RuntimeError, match='timed out waiting for rank 3'):
+        Trainer.check_collectives()
+    T = Trainer.__new__(Trainer)
+    with pytest.raises(RuntimeError, match='timed out'):
+        T.state_dict()
