@@ -2,7 +2,7 @@
 (backend "nccl" = RCCL on ROCm, "gloo" for CPU tests).
 
 Replaces the single-process nn.DataParallel + host-thread SyncBN rendezvous
-of the reference (train.py:220-228, sync_batchnorm/comm.py) with:
+of the reference (train.py:220-228, its sync_batchnorm/comm.py) with:
   * SyncBN statistics all-reduce: a 2C-value fp64 message per BN layer in
     forward (sum, sumsq) and backward (sum dxhat, sum dxhat*xhat);
   * gradient averaging: bucketed all-reduce of each optimizer's flat gradient

@@ -1528,9 +1528,16 @@ class WordsSimFn(torch.autograd.Function):
     `diag_off`: caption index of image 0's own caption (rank * B_local), used
     for the attention maps of the matching pairs."""
 
+    MAX_WORDS = 32   # csrc/damsm.hip NW: one caption's words live in one workgroup's LDS / MFMA tiles
+
     @staticmethod
     def forward(ctx, regions, words, cap_lens, want_att, diag_off=0):
         # regions: (n_img, 256, 17, 17) fp32, NHWC-dense (the Inception projection output) or NCHW
+        if words.shape[2] > WordsSimFn.MAX_WORDS:
+            # the reference takes any words_num (DAMSM_losses.py:287-291); every shipped cfg has
+            # TEXT.WORDS_NUM <= 20, and wider captions are refused rather than truncated
+            raise ValueError('words_loss: captions of up to %d words are supported (got a %d-word batch; '
+                             'cfg.TEXT.WORDS_NUM bounds it)' % (WordsSimFn.MAX_WORDS, words.shape[2]))
         n_img = regions.shape[0]
         if regions.dtype == F32 and T.is_nhwc(regions) and ld_of(regions) == regions.shape[1] \
                 and regions.data_ptr() % 16 == 0:

@@ -1,8 +1,8 @@
 """One-shot peer-write all-reduce for the SyncBN statistics (EEGAN_SYNCBN_PEER=1).
 
 The reference exchanges every BN layer's (sum, ssum) message through a master
-replica (sync_batchnorm/batchnorm.py:90-111 over SyncMaster / SlavePipe,
-sync_batchnorm/comm.py:18-137): gather to GPU0, reduce, broadcast back.  With
+replica (reference sync_batchnorm/batchnorm.py:90-111 over SyncMaster / SlavePipe,
+reference sync_batchnorm/comm.py:18-137): gather to GPU0, reduce, broadcast back.  With
 one process per GPU these messages (2C fp64 values, at most a few KB) are
 latency-bound; a ring all-reduce spends most of its time in protocol steps.
 Here each rank owns a small uncached device region per stream lane, mapped by

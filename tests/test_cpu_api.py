@@ -105,36 +105,6 @@ def test_att_maps_lazy_list():
     assert len(m) == 2 and m[1].shape == (1, 1, 17, 17) and m[0].shape == (1, 3, 17, 17)
 
 
-def test_sync_master_rendezvous():
-    """sync_batchnorm.comm keeps the reference's in-process rendezvous
-    (sync_batchnorm/comm.py:18-137): slaves' messages reach the master's
-    callback after the master's own, each slave gets its own reply, over
-    several rounds."""
-    import threading
-    from sync_batchnorm.comm import SyncMaster
-
-    def callback(msgs):
-        total = sum(m for _, m in msgs)
-        return [(i, (total, m)) for i, m in msgs]
-    master = SyncMaster(callback)
-    pipes = [master.register_slave(i) for i in (1, 2, 3)]
-    for rnd in range(3):
-        got = {}
-
-        def slave(p):
-            got[p.identifier] = p.run_slave(10 * p.identifier + rnd)
-        ts = [threading.Thread(target=slave, args=(p,)) for p in pipes]
-        for t in ts:
-            t.start()
-        mine = master.run_master(rnd)
-        for t in ts:
-            t.join(10)
-        total = rnd + sum(10 * i + rnd for i in (1, 2, 3))
-        assert mine == (total, rnd)
-        assert got == {i: (total, 10 * i + rnd) for i in (1, 2, 3)}
-    assert master.nr_slaves == 3
-
-
 def test_early_term_roots_match_joint_backward():
     """g_update's backward from per-D terms already differentiated at their
     (aliased) fake images (trainer.EarlyTerm, EEGAN_GTERM_GRAD_EARLY) gives the
@@ -167,3 +137,14 @@ def test_early_term_roots_match_joint_backward():
     assert torch.allclose(got, ref, rtol=1e-12, atol=1e-12)
     assert float(_term_value(terms[0]) + _term_value(terms[1])) == pytest.approx(
         float(term(0, f[0]) + term(1, f[1])))
+
+
+def test_words_loss_refuses_wide_captions():
+    """words_loss with captions wider than the kernel's 32 words raises a
+    clear error before any device work (no silent truncation)."""
+    import torch
+    from eegan_hip.functional import WordsSimFn
+    regions = torch.zeros(2, 256, 17, 17)
+    words = torch.zeros(2, 256, 33)
+    with pytest.raises(ValueError, match='up to 32 words'):
+        WordsSimFn.apply(regions, words, torch.tensor([33, 5]), False, 0)
