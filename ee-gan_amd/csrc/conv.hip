@@ -232,28 +232,20 @@ template <int MODE, int TCO, int TPIX, int FI, int FJ, int WT_CO, int WT_PIX>
 EE_DEV void staged_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], float4* st, int pix0, int co0, int wi,
                             int wj, int lane, int tid, int Pc, int CH, int CW, int qy, int qx, int stc) {
   constexpr int NCK = TCO / 4, SWM = NCK >= 8 ? 7 : NCK - 1, E = TCO / 8, ITEMS = TPIX * E;
+  constexpr int NIT = (ITEMS + 255) / 256;
   const int fr = lane & 15, fq = lane >> 4;
-  __syncthreads();  // every wave's last ring reads are done
+  // gate / residual runs of this thread's items loaded first: their latency overlaps the staging
+  uint4 gpre[NIT], rpre[NIT];
+  long ppre[NIT];
 #pragma unroll
-  for (int i = 0; i < FI; ++i)
-#pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-      const int pix = wj * WT_PIX + j * 16 + fr;
-      const int c = (wi * WT_CO + i * 16) / 4 + fq;
-      st[pix * NCK + (c ^ (pix & SWM))] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-    }
-  __syncthreads();
-  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
-#pragma unroll
-  for (int k = 0; k < (ITEMS + 255) / 256; ++k) {
+  for (int k = 0; k < NIT; ++k) {
     const int item = k * 256 + tid;
-    if (ITEMS % 256 && item >= ITEMS) break;
+    gpre[k] = rpre[k] = make_uint4(0, 0, 0, 0);
+    ppre[k] = -1;
+    if (ITEMS % 256 && item >= ITEMS) continue;
     const int pix = item / E, e = item % E;
     const int pc = pix0 + pix, co = co0 + 8 * e;
     if (pc >= Pc || co >= a.Mrows) continue;
-    const float4 lo = st[pix * NCK + ((2 * e) ^ (pix & SWM))];
-    const float4 hi = st[pix * NCK + ((2 * e + 1) ^ (pix & SWM))];
-    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     long p = pc, rpix = pc;
     if (MODE == MODE_BWDD && a.ncls > 1) {
       const int hw = CH * CW;
@@ -268,10 +260,35 @@ EE_DEV void staged_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], flo
       const unsigned y = rem / (unsigned)a.OW, x = rem - y * (unsigned)a.OW;
       rpix = ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
     }
+    ppre[k] = p;
+    if (MODE == MODE_BWDD && a.gate) gpre[k] = *reinterpret_cast<const uint4*>(a.gate + p * a.ldgate + co);
+    if (a.res) rpre[k] = *reinterpret_cast<const uint4*>(a.res + (a.res_up2 ? rpix : p) * a.ldres + co);
+  }
+  __syncthreads();  // every wave's last ring reads are done
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const int pix = wj * WT_PIX + j * 16 + fr;
+      const int c = (wi * WT_CO + i * 16) / 4 + fq;
+      st[pix * NCK + (c ^ (pix & SWM))] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+  __syncthreads();
+  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int item = k * 256 + tid;
+    if (ppre[k] < 0) continue;
+    const int pix = item / E, e = item % E;
+    const int co = co0 + 8 * e;
+    const float4 lo = st[pix * NCK + ((2 * e) ^ (pix & SWM))];
+    const float4 hi = st[pix * NCK + ((2 * e + 1) ^ (pix & SWM))];
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const long p = ppre[k];
 #pragma unroll
     for (int r = 0; r < 8; ++r) v[r] = act_fwd(v[r] + (a.bias ? a.bias[co + r] : 0.f), a.act, a.slope);
     if (MODE == MODE_BWDD && a.gate) {
-      const uint4 gv = *reinterpret_cast<const uint4*>(a.gate + p * a.ldgate + co);
+      const uint4 gv = gpre[k];
       const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -280,7 +297,7 @@ EE_DEV void staged_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], flo
       }
     }
     if (a.res) {
-      const uint4 rv = *reinterpret_cast<const uint4*>(a.res + (a.res_up2 ? rpix : p) * a.ldres + co);
+      const uint4 rv = rpre[k];
       const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1094,6 +1111,196 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
     return;
   }
   igemm_epilogue<MODE, FI, FJ, WT_CO, WT_PIX>(a, acc, pix0, co0, wi, wj, lane, split, Pc, CH, CW, qy, qx, stc);
+}
+
+// ------------------------------------ 3x3 stride-1 convs: LDS halo tiles --
+// FWD / BWDD of 3x3 / stride-1 / pad-1 convs (resD conv_r[1] models.py:270,
+// the SAGB / Cum 3x3 convs models.py:104-143 incl. the nearest-2x upsample, the
+// data gradients of all of them).  The tile kernels gather every source pixel
+// once per tap (9x through L2 -> LDS, 64 B pieces), which bounds them at the
+// per-CU LDS-DMA rate.  Here one workgroup owns 64 output channels x a TH x 32
+// pixel tile of one image; per 32-channel input slice it stages the
+// (TH + 2) x 34 source halo ONCE (LDS-DMA; out-of-image pixels read zeros
+// through the buffer bounds check) together with all 9 taps' 64 x 32 weight
+// slabs, double-buffered per slice, so one barrier covers 9 taps x 16 MFMAs
+// per wave and the next tap's fragments are read while the current tap's
+// MFMAs run.  Halo pixel h's 16-B chunk q sits in LDS slot h * 4 + (q ^ ((h >> 1)
+// & 2)): conflict-free ds_read_b128 for any 16 consecutive halo pixels, i.e. at
+// every tap shift.  BWDD reads the mirrored tap (2 - r, 2 - s) of the same halo
+// with the transposed pack.  Epilogue through LDS (fp32 tile, 16-B runs of 8
+// channels): bias, activation, gate, residual exactly as staged_epilogue.
+// K order: slice-major, tap inner (the tile kernels: tap-major) -- a different
+// fp32 summation order, deterministic.
+constexpr int HALO_TW = 32, HALO_TCO = 64;
+
+EE_DEV int halo_swz(int h) { return (h >> 1) & 2; }
+
+template <int MODE, int TH, int WPX>
+__global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, long src_bytes, long w_bytes) {
+  constexpr int NT = 64 * WPX, TW = HALO_TW, TCO = HALO_TCO, FI = TCO / 16;
+  constexpr int WROWS = TH / WPX, CB = TW / 16, FJ = WROWS * CB;
+  constexpr int HW2 = TW + 2, HP = (TH + 2) * HW2, HOPS = (HP * 4 + NT - 1) / NT, HBUF = HOPS * NT * 16;
+  constexpr int WCH = 9 * TCO * 4, WOPS = (WCH + NT - 1) / NT, WBUF = WOPS * NT * 16;
+  constexpr int TPIX = TH * TW, NCK = TCO / 4;
+  static_assert(WROWS >= 1 && TPIX * TCO * 4 <= 2 * (HBUF + WBUF), "halo tile");
+  __shared__ __attribute__((aligned(16))) char lds[2 * (HBUF + WBUF)];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wj = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_x = a.OW / TW, tiles_y = a.OH / TH;
+  int b = blockIdx.x;
+  const int tx = b % tiles_x;
+  b /= tiles_x;
+  const int ty = b % tiles_y;
+  const int n = b / tiles_y;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int co0 = blockIdx.y * TCO;
+  const int nslice = a.Cgp / BK;
+  const int lds0 = (int)(uintptr_t)(lds_void_t*)lds;
+  const rsrc_t rs_src = make_rsrc(a.src, src_bytes);
+  const rsrc_t rs_w = make_rsrc(a.wp, w_bytes);
+  const int PH = a.IH >> a.up2, PW = a.IW >> a.up2;   // physical source grid (FWD up2: half resolution)
+
+  // this thread's halo pieces (slice 0 offsets; OOB outside the image) and their channel chunk
+  unsigned hoff[HOPS];
+  int hq[HOPS];
+#pragma unroll
+  for (int i = 0; i < HOPS; ++i) {
+    const int L = i * NT + tid, h = L >> 2, q = (L & 3) ^ halo_swz(h);
+    const int hy = h / HW2, hx = h - hy * HW2;
+    const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;   // logical source pixel (pad 1)
+    hq[i] = q;
+    hoff[i] = (h < HP && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW)
+                  ? (unsigned)((((n * PH + (iy >> a.up2)) * PW + (ix >> a.up2)) * a.lds_src + q * 8) * 2)
+                  : OOB;
+  }
+  // weight pieces: stage image [tap][row][4 chunks, swizzled as the tile kernels' rows]
+  unsigned woff[WOPS];
+#pragma unroll
+  for (int i = 0; i < WOPS; ++i) {
+    const int L = i * NT + tid, t = L / (TCO * 4), rem = L - t * (TCO * 4);
+    const int row = rem >> 2, q = (rem & 3) ^ swz_b128((row >> 2) & 3);
+    woff[i] = L < WCH ? (unsigned)(((co0 + row) * a.Kw + t * a.Cgp + q * 8) * 2) : OOB;
+  }
+  auto issue = [&](int cs) {   // slice cs: halo into buffer cs & 1, weights into buffer cs & 1
+    const int buf = cs & 1;
+#pragma unroll
+    for (int i = 0; i < HOPS; ++i) {
+      const bool ok = hoff[i] != OOB && cs * BK + hq[i] * 8 < a.Cvalid;
+      // soffset is wave-uniform (s_ register); an out-of-range lane's OOB voffset stays out of range with it
+      lds_dma16s(rs_src, lds0 + buf * HBUF + (i * NT + wj * 64) * 16, ok ? hoff[i] : OOB, cs * 64);
+    }
+#pragma unroll
+    for (int i = 0; i < WOPS; ++i)
+      lds_dma16s(rs_w, lds0 + 2 * HBUF + buf * WBUF + (i * NT + wj * 64) * 16, woff[i], cs * 64);
+  };
+
+  f32x4_t acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  // C % 8 != 0 is not taken here (whole 16-B chunks valid or zero)
+  auto rd = [&](int cs, int t, bf16x8_t (&fa)[FI], bf16x8_t (&fb)[FJ]) {
+    const int ta = t / 3, tb = t - ta * 3;
+    const int oyh = MODE == MODE_FWD ? ta : 2 - ta, oxh = MODE == MODE_FWD ? tb : 2 - tb;
+    const char* wbase = lds + 2 * HBUF + (cs & 1) * WBUF + t * TCO * 64;
+    const char* hbase = lds + (cs & 1) * HBUF;
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const int row = i * 16 + fr;
+      fa[i] = as_frag(*reinterpret_cast<const uint4*>(wbase + (row * 4 + (fq ^ swz_b128((row >> 2) & 3))) * 16));
+    }
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const int r = wj * WROWS + j / CB, col = (j % CB) * 16 + fr;
+      const int h = (r + oyh) * HW2 + col + oxh;
+      fb[j] = as_frag(*reinterpret_cast<const uint4*>(hbase + (h * 4 + (fq ^ halo_swz(h))) * 16));
+    }
+  };
+  issue(0);
+  for (int cs = 0; cs < nslice; ++cs) {
+    wait_vmcnt_barrier<0>();   // slice cs landed; every wave is done with slice cs - 1's buffers
+    if (cs + 1 < nslice) issue(cs + 1);
+    bf16x8_t fa[2][FI], fb[2][FJ];
+    rd(cs, 0, fa[0], fb[0]);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (t + 1 < 9) rd(cs, t + 1, fa[(t + 1) & 1], fb[(t + 1) & 1]);
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t & 1][i], fb[t & 1][j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // epilogue: the gate / residual runs of this thread's items are loaded first, so their
+  // latency overlaps the LDS staging; fp32 tile [pixel][16 chunks of 4 channels], chunk c
+  // of pixel p at c ^ (p & 15)
+  constexpr int NIT = TPIX * (TCO / 8) / NT;
+  uint4 gpre[NIT], rpre[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int item = k * NT + tid, p = item / (TCO / 8), e = item % (TCO / 8);
+    const int co = co0 + 8 * e;
+    const int y = oy0 + p / TW, x = ox0 + p % TW;
+    const long gp = ((long)n * a.OH + y) * a.OW + x;
+    gpre[k] = rpre[k] = make_uint4(0, 0, 0, 0);
+    if (co < a.Mrows) {
+      if (MODE == MODE_BWDD && a.gate) gpre[k] = *reinterpret_cast<const uint4*>(a.gate + gp * a.ldgate + co);
+      if (a.res) {
+        const long rp = a.res_up2 ? ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1) : gp;
+        rpre[k] = *reinterpret_cast<const uint4*>(a.res + rp * a.ldres + co);
+      }
+    }
+  }
+  __syncthreads();
+  float4* st = reinterpret_cast<float4*>(lds);
+#pragma unroll
+  for (int j = 0; j < FJ; ++j) {
+    const int p = (wj * WROWS + j / CB) * TW + (j % CB) * 16 + fr;
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const int c = i * 4 + fq;
+      st[p * NCK + (c ^ (p & 15))] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+  }
+  __syncthreads();
+  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int item = k * NT + tid, p = item / (TCO / 8), e = item % (TCO / 8);
+    const int co = co0 + 8 * e;
+    if (co >= a.Mrows) continue;
+    const float4 lo = st[p * NCK + ((2 * e) ^ (p & 15))];
+    const float4 hi = st[p * NCK + ((2 * e + 1) ^ (p & 15))];
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const int y = oy0 + p / TW, x = ox0 + p % TW;
+    const long gp = ((long)n * a.OH + y) * a.OW + x;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = act_fwd(v[r] + (a.bias ? a.bias[co + r] : 0.f), a.act, a.slope);
+    if (MODE == MODE_BWDD && a.gate) {
+      const uint4 gv = gpre[k];
+      const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[2 * r] *= act_dgrad_from_y(lo_f(gw[r]), a.gate_act, a.gate_slope);
+        v[2 * r + 1] *= act_dgrad_from_y(hi_f(gw[r]), a.gate_act, a.gate_slope);
+      }
+    }
+    if (a.res) {
+      const uint4 rv = rpre[k];
+      const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[2 * r] = res_combine(a.res_scale, lo_f(rw[r]), gam, v[2 * r]);
+        v[2 * r + 1] = res_combine(a.res_scale, hi_f(rw[r]), gam, v[2 * r + 1]);
+      }
+    }
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + gp * a.ldo + co) =
+        make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+  }
 }
 
 // ---------------------------------------------------------- WGRAD kernel --
@@ -2581,6 +2788,34 @@ int try_thin(const ConvArgs& a, hipStream_t s, long src_bytes) {
   return rc ? rc : 1;
 }
 
+// 3x3 / stride-1 / pad-1 convs with >= 48 output rows on grids of whole 8 x 32
+// tiles take conv_halo3_kernel (0: not eligible, else the launch rc)
+template <int MODE>
+int try_halo3(const ConvArgs& a, hipStream_t s, long src_bytes, long w_bytes) {
+  if (!knob("halo", 1) || src_bytes >= 0x7fffffffL || w_bytes >= 0x7fffffffL) return 0;
+  if (a.R != 3 || a.S != 3 || a.st != 1 || a.ph != 1 || a.pw != 1 || a.ncls != 1 || a.nsplit != 1) return 0;
+  if (MODE == MODE_BWDD && a.up2) return 0;
+  if (a.Mrows < 48 || (a.Mrows & 7) || (a.Cvalid & 7) || a.Cgp % BK || a.out_f32) return 0;
+  if ((a.lds_src & 7) || ((uintptr_t)a.src & 15) || (a.ldo & 7) || ((uintptr_t)a.out & 15)) return 0;
+  if (a.gate && ((a.ldgate & 7) || ((uintptr_t)a.gate & 15))) return 0;
+  if (a.res && ((a.ldres & 7) || ((uintptr_t)a.res & 15))) return 0;
+  if (a.OW % HALO_TW || a.OH % 8 || a.OH != a.IH || a.OW != a.IW) return 0;
+  const int co_t = ee_cdiv(a.Mrows, HALO_TCO);
+  const long tiles16 = a.OH % 16 ? 0 : (long)a.N * (a.OH / 16) * (a.OW / HALO_TW) * co_t;
+  const int big = knob("halo_th", 0);   // 16 / 8: force the tile height (tests, sweeps)
+  const bool th16 = big == 16 || (big != 8 && tiles16 >= 256);
+  if (th16 && !tiles16) return 0;
+  if (th16) {
+    dim3 grid((unsigned)(tiles16 / co_t), co_t);
+    ee_launch(conv_halo3_kernel<MODE, 16, 8>, grid, dim3(512), 0, s, a, src_bytes, w_bytes);
+  } else {
+    dim3 grid((unsigned)((long)a.N * (a.OH / 8) * (a.OW / HALO_TW)), co_t);
+    ee_launch(conv_halo3_kernel<MODE, 8, 4>, grid, dim3(256), 0, s, a, src_bytes, w_bytes);
+  }
+  const int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd(halo3)" : "conv_bwd_data(halo3)");
+  return rc ? rc : 1;
+}
+
 // 4x4 / stride-2 / pad-1 data gradients with <= 32 input channels take
 // conv_s2bwd_lds_kernel (0: not eligible, else the launch rc as try_thin)
 int try_s2bwd(const ConvArgs& a, hipStream_t s, long src_bytes) {
@@ -2663,6 +2898,8 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   if (const int pw = try_1x1<MODE>(a, s, src_bytes)) return pw > 0 ? 0 : pw;
   if (MODE == MODE_BWDD)
     if (const int sb = try_s2bwd(a, s, src_bytes)) return sb > 0 ? 0 : sb;
+  if (const int hl = try_halo3<MODE>(a, s, src_bytes, (long)ee_round_up(a.Mrows, 128) * a.Kw * 2))
+    return hl > 0 ? 0 : hl;
   Plan p = plan_igemm(a, Pc_max);
   a.nsplit = p.nsplit;
   a.part = p.nsplit > 1 ? part_ws : nullptr;

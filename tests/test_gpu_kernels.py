@@ -906,3 +906,53 @@ def test_flat_adam_repacks_conv_weights(gpu):
         for tr, buf, key in ((False, c.fwd, c.fwd_key), (True, c.bwd, c.bwd_key)):
             assert key == Fn.PackCache._key(m.weight)
             assert torch.equal(buf, Fn.pack_weight(m.weight, tr))
+
+
+@pytest.mark.parametrize('th', ['16', '8'])
+def test_conv_halo3_matches_tile_kernel(gpu, monkeypatch, th):
+    """3x3 / stride-1 convs on the LDS halo-tile kernel (conv_halo3_kernel,
+    EEGAN_CONV halo=1, default) against the tile kernels (halo=0) and torch's
+    fp32 conv: forward with bias / act / residual + gain and the fused nearest-2x
+    upsample, backward-data plain / gated / with the half-resolution residual;
+    ragged input channels (40 -> a masked chunk), two output-channel tiles with a
+    partial second one (96), both tile heights.  The halo kernel sums slice-major
+    (the tile kernels tap-major), so the gate is bf16 output rounding: rel-L2
+    <= 5e-3 between the kernels, <= 1e-2 against fp32."""
+    Fn, T, _ = _mods()
+    conv_knob(monkeypatch, 'halo_th', th)
+    lrelu = Fn.ACT_CODES['lrelu']
+    for N, Cin, H, W, Cout, up2 in [(2, 64, 32, 64, 64, 0), (3, 40, 16, 32, 96, 0), (2, 128, 16, 32, 48, 0),
+                                    (2, 64, 16, 32, 64, 1), (1, 256, 32, 32, 128, 0)]:
+        torch.manual_seed(N * Cin + Cout + H + up2)
+        g = Fn.Geom(Cout, 3, 3, 1, 1, 1, up2)
+        xs = torch.randn(N, Cin, H // 2, W // 2) if up2 else torch.randn(N, Cin, H, W)
+        x = _nhwc(xs, gpu)
+        Wt = (torch.randn(Cout, Cin, 3, 3) * (1.0 / (9 * Cin) ** 0.5)).to(gpu)
+        b = torch.randn(Cout).to(gpu) * 0.1
+        gam = torch.tensor([0.7]).to(gpu)
+        res = _nhwc(torch.randn(N, Cout, H, W), gpu)
+        dz = _nhwc(torch.randn(N, Cout, H, W), gpu)
+        gate = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        halfres = _nhwc(torch.randn(N, Cin, H // 2, W // 2), gpu)
+        outs = {}
+        for on in ('0', '1'):
+            conv_knob(monkeypatch, 'halo', on)
+            o = [Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, res=res, gamma=gam).float().cpu(),
+                 Fn.conv_fwd_raw(x, Wt, None, g).float().cpu()]
+            if not up2:
+                o += [Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape)).float().cpu(),
+                      Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), gate=gate, gate_act=lrelu).float().cpu(),
+                      Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), res=halfres, res_up2=1,
+                                           res_scale=0.25).float().cpu()]
+            outs[on] = o
+        for k, (a, c) in enumerate(zip(outs['1'], outs['0'])):
+            e = rel_l2(a, c)
+            assert e <= 5e-3, (N, Cin, H, W, Cout, up2, k, e)
+        xin = xs.to(torch.bfloat16).float()
+        if up2:
+            xin = F.interpolate(xin, scale_factor=2, mode='nearest')
+        ref = F.conv2d(xin, Wt.cpu().to(torch.bfloat16).float(), None, 1, 1)
+        assert rel_l2(outs['1'][1], ref) <= 1e-2
+        if not up2:
+            dref = F.conv_transpose2d(dz.float().cpu(), Wt.cpu().to(torch.bfloat16).float(), None, 1, 1)
+            assert rel_l2(outs['1'][2], dref) <= 1e-2
