@@ -1132,6 +1132,12 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
 // K order: slice-major, tap inner (the tile kernels: tap-major) -- a different
 // fp32 summation order, deterministic.
 constexpr int HALO_TW = 32, HALO_TCO = 64;
+// Diagnostic builds only (tools/gpu_halo_knock.sh compiles copies of the library
+// with -DEEGAN_HALO_KNOCK=bits): 1 = no operand loads, 2 = no output stores,
+// 4 = no MFMAs.  The shipped library is built with 0.
+#ifndef EEGAN_HALO_KNOCK
+#define EEGAN_HALO_KNOCK 0
+#endif
 
 EE_DEV int halo_swz(int h) { return (h >> 1) & 2; }
 
@@ -1190,6 +1196,7 @@ __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, lon
   // slice cs of tile T into buffer buf: the (TH + 2) x 34 halo (pixel h's chunk q at slot
   // h * 4 + (q ^ halo_swz(h)); out-of-image pixels read zeros) and the 9 taps' 64 x 32 weights
   auto issue = [&](const Tile& T, int cs, int buf) {
+    if (EEGAN_HALO_KNOCK & 1) return;
 #pragma unroll
     for (int i = 0; i < HOPS; ++i) {
       const int hy = hpk[i] >> 16, hx = (hpk[i] >> 4) & 0xfff, q = hpk[i] & 15;
@@ -1254,6 +1261,7 @@ __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, lon
 #pragma unroll
       for (int k = 0; k < 9; ++k) {
         if (k + 1 < 9) rd(buf, k + 1, z, fa[(k + 1) & 1], fb[(k + 1) & 1]);
+        if (EEGAN_HALO_KNOCK & 4) continue;
 #pragma unroll
         for (int i = 0; i < FI; ++i)
 #pragma unroll
@@ -1304,7 +1312,7 @@ __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, lon
       const int item = k * NT + tid, p = item / NCK, e = item % NCK;
       const uint4 v = *reinterpret_cast<const uint4*>(stg + p * TCO * 2 + ((e ^ (p & 7)) << 4));
       const long gp = ((long)T.n * a.OH + T.oy0 + p / TW) * a.OW + T.ox0 + p % TW;
-      if (T.co0 + 8 * e < a.Mrows)
+      if (T.co0 + 8 * e < a.Mrows && (!(EEGAN_HALO_KNOCK & 2) || v.x == 0x7fc17fc1u))
         *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + gp * a.ldo + T.co0 + 8 * e) = v;
     }
   }
