@@ -1124,10 +1124,11 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
 // through the buffer bounds check) together with all 9 taps' 64 x 32 weight
 // slabs, double-buffered per slice, so one barrier covers 9 taps x 16 MFMAs
 // per wave and the next tap's fragments are read while the current tap's
-// MFMAs run.  Halo pixel h's 16-B chunk q sits in LDS slot h * 4 + (q ^ ((h >> 1)
-// & 2)): conflict-free ds_read_b128 for any 16 consecutive halo pixels, i.e. at
-// every tap shift.  BWDD reads the mirrored tap (2 - r, 2 - s) of the same halo
-// with the transposed pack.  Epilogue through LDS (fp32 tile, 16-B runs of 8
+// MFMAs run.  Halo pixel h = (hy, hx)'s 16-B chunk q sits in LDS slot h * 4 +
+// (q ^ ((hx >> 1) & 2)): conflict-free ds_read_b128 for any 16 consecutive
+// pixels of a halo row, i.e. at every tap shift, and a tap's row shift is an
+// immediate offset.  BWDD reads the mirrored tap (2 - r, 2 - s) of the same
+// halo with the transposed pack.  Epilogue through LDS (fp32 tile, 16-B runs of 8
 // channels): bias, activation, gate, residual exactly as staged_epilogue.
 // K order: slice-major, tap inner (the tile kernels: tap-major) -- a different
 // fp32 summation order, deterministic.
@@ -1139,7 +1140,7 @@ constexpr int HALO_TW = 32, HALO_TCO = 64;
 #define EEGAN_HALO_KNOCK 0
 #endif
 
-EE_DEV int halo_swz(int h) { return (h >> 1) & 2; }
+EE_DEV int halo_swz(int hx) { return (hx >> 1) & 2; }
 
 template <int MODE, int TH, int WPX>
 __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, long src_bytes, long w_bytes) {
@@ -1147,176 +1148,180 @@ __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, lon
   constexpr int WROWS = TH / WPX, CB = TW / 16, FJ = WROWS * CB;
   constexpr int HW2 = TW + 2, HP = (TH + 2) * HW2, HOPS = (HP * 4 + NT - 1) / NT, HBUF = HOPS * NT * 16;
   constexpr int WCH = 9 * TCO * 4, WOPS = (WCH + NT - 1) / NT, WBUF = WOPS * NT * 16;
-  constexpr int TPIX = TH * TW, NCK = TCO / 8, NIT = TPIX * NCK / NT;
-  constexpr int BUF = HBUF + WBUF;   // one slice buffer: halo, then the weights
-  static_assert(WROWS >= 1 && TPIX * TCO * 2 <= BUF, "halo tile");
+  constexpr int TPIX = TH * TW, NCK = TCO / 4;
+  static_assert(WROWS >= 1 && TPIX * TCO * 4 <= 2 * (HBUF + WBUF), "halo tile");
   __shared__ __attribute__((aligned(16))) char lds[2 * (HBUF + WBUF)];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wj = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tiles_x = a.OW / TW, tiles_y = a.OH / TH;
-  const int ptiles = a.N * tiles_y * tiles_x, ntiles = ptiles * ((a.Mrows + TCO - 1) / TCO);
+  int b = blockIdx.x;
+  const int tx = b % tiles_x;
+  b /= tiles_x;
+  const int ty = b % tiles_y;
+  const int n = b / tiles_y;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int co0 = blockIdx.y * TCO;
   const int nslice = a.Cgp / BK;
   const int lds0 = (int)(uintptr_t)(lds_void_t*)lds;
   const rsrc_t rs_src = make_rsrc(a.src, src_bytes);
   const rsrc_t rs_w = make_rsrc(a.wp, w_bytes);
   const int PH = a.IH >> a.up2, PW = a.IW >> a.up2;   // physical source grid (FWD up2: half resolution)
 
-  // persistent: this workgroup's tiles are blockIdx.x, + gridDim.x, ...; tile t = co tile
-  // (outermost: neighbouring workgroups share a weight slab) x image x row x column
-  struct Tile { int n, oy0, ox0, co0; };
-  auto tile_of = [&](int t) {
-    Tile r;
-    const int ct = t / ptiles;
-    int q = t - ct * ptiles;
-    const int tx = q % tiles_x;
-    q /= tiles_x;
-    r.oy0 = (q % tiles_y) * TH;
-    r.n = q / tiles_y;
-    r.ox0 = tx * TW;
-    r.co0 = ct * TCO;
-    return r;
-  };
-  // this thread's pieces, tile-independent parts: halo (hy, hx, chunk) packed, weight offsets
-  // without the tile's channel offset (that and the slice go into the uniform soffset)
-  int hpk[HOPS];
-  unsigned wpk[WOPS];
+  // this thread's halo pieces (slice 0 offsets; OOB outside the image) and their channel chunk
+  unsigned hoff[HOPS];
+  int hq[HOPS];
 #pragma unroll
   for (int i = 0; i < HOPS; ++i) {
-    const int L = i * NT + tid, h = L >> 2, q = (L & 3) ^ halo_swz(h);
-    const int hy = h / HW2, hx = h - hy * HW2;
-    hpk[i] = h < HP ? (hy << 16) | (hx << 4) | q : -1;
+    const int L = i * NT + tid, h = L >> 2;
+    const int hy = h / HW2, hx = h - hy * HW2, q = (L & 3) ^ halo_swz(hx);
+    const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;   // logical source pixel (pad 1)
+    hq[i] = q;
+    hoff[i] = (h < HP && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW)
+                  ? (unsigned)((((n * PH + (iy >> a.up2)) * PW + (ix >> a.up2)) * a.lds_src + q * 8) * 2)
+                  : OOB;
   }
+  // weight pieces: stage image [tap][row][4 chunks, swizzled as the tile kernels' rows]
+  unsigned woff[WOPS];
 #pragma unroll
   for (int i = 0; i < WOPS; ++i) {
     const int L = i * NT + tid, t = L / (TCO * 4), rem = L - t * (TCO * 4);
     const int row = rem >> 2, q = (rem & 3) ^ swz_b128((row >> 2) & 3);
-    wpk[i] = L < WCH ? (unsigned)((row * a.Kw + t * a.Cgp + q * 8) * 2) : OOB;
+    woff[i] = L < WCH ? (unsigned)(((co0 + row) * a.Kw + t * a.Cgp + q * 8) * 2) : OOB;
   }
-  // slice cs of tile T into buffer buf: the (TH + 2) x 34 halo (pixel h's chunk q at slot
-  // h * 4 + (q ^ halo_swz(h)); out-of-image pixels read zeros) and the 9 taps' 64 x 32 weights
-  auto issue = [&](const Tile& T, int cs, int buf) {
+  auto issue = [&](int cs) {   // slice cs: halo into buffer cs & 1, weights into buffer cs & 1
     if (EEGAN_HALO_KNOCK & 1) return;
+    const int buf = cs & 1;
 #pragma unroll
     for (int i = 0; i < HOPS; ++i) {
-      const int hy = hpk[i] >> 16, hx = (hpk[i] >> 4) & 0xfff, q = hpk[i] & 15;
-      const int iy = T.oy0 - 1 + hy, ix = T.ox0 - 1 + hx;   // logical source pixel (pad 1)
-      const bool ok = hpk[i] >= 0 && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW &&
-                      cs * BK + q * 8 < a.Cvalid;
-      const unsigned off = ok ? (unsigned)((((T.n * PH + (iy >> a.up2)) * PW + (ix >> a.up2)) * a.lds_src + q * 8) * 2)
-                              : OOB;
-      // soffset is wave-uniform (an s_ register); an out-of-range lane's OOB offset stays out of range with it
-      lds_dma16s(rs_src, lds0 + buf * BUF + (i * NT + wj * 64) * 16, off, cs * 64);
+      const bool ok = hoff[i] != OOB && cs * BK + hq[i] * 8 < a.Cvalid;
+      // soffset is wave-uniform (s_ register); an out-of-range lane's OOB voffset stays out of range with it
+      lds_dma16s(rs_src, lds0 + buf * HBUF + (i * NT + wj * 64) * 16, ok ? hoff[i] : OOB, cs * 64);
     }
 #pragma unroll
     for (int i = 0; i < WOPS; ++i)
-      lds_dma16s(rs_w, lds0 + buf * BUF + HBUF + (i * NT + wj * 64) * 16, wpk[i], T.co0 * a.Kw * 2 + cs * 64);
+      lds_dma16s(rs_w, lds0 + 2 * HBUF + buf * WBUF + (i * NT + wj * 64) * 16, woff[i], cs * 64);
   };
 
+  f32x4_t acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fq = lane >> 4;
-  // `z` is an opaque zero per slice: the fragment addresses depend on it, so the compiler
-  // recomputes them per tap instead of hoisting all 9 x (FI + FJ) of them out of the slice
-  // loop (which spilled the 512-thread form)
-  auto rd = [&](int buf, int t, int z, bf16x8_t (&fa)[FI], bf16x8_t (&fb)[FJ]) {
+  // fragment addresses: a per-slice base register + an immediate for every tap.  Weights:
+  // row i * 16 + fr of tap t at woff + t * 4096 + i * 1024 (the chunk swizzle of rows
+  // i * 16 + fr is i-independent).  Halo: pixel column hx's swizzle depends on hx only (and
+  // is the same for hx + 16), so B fragment j = (row jr, 16-column block jc) at tap shift
+  // (oyh, oxh) is fhoff[oxh] + (oyh + jr) * HW2 * 64 + jc * 1024: 3 base registers.
+  // C % 8 != 0 is not taken here (whole 16-B chunks valid or zero)
+  const int fwoff = 2 * HBUF + fr * 64 + ((fq ^ swz_b128((fr >> 2) & 3)) << 4);
+  int fhoff[3];
+#pragma unroll
+  for (int sx = 0; sx < 3; ++sx)
+    fhoff[sx] = ((wj * WROWS * HW2 + fr + sx) << 6) + ((fq ^ halo_swz(fr + sx)) << 4);
+  auto rd = [&](int cs, int t, bf16x8_t (&fa)[FI], bf16x8_t (&fb)[FJ]) {
     const int ta = t / 3, tb = t - ta * 3;
-    const int oyh = (MODE == MODE_FWD ? ta : 2 - ta) + z, oxh = MODE == MODE_FWD ? tb : 2 - tb;
-    const char* hbase = lds + buf * BUF;
-    const char* wbase = hbase + HBUF + t * TCO * 64;
-#pragma unroll
-    for (int i = 0; i < FI; ++i) {
-      const int row = i * 16 + fr;
-      fa[i] = as_frag(*reinterpret_cast<const uint4*>(wbase + (row * 4 + (fq ^ swz_b128((row >> 2) & 3))) * 16));
-    }
-#pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-      const int r = wj * WROWS + j / CB, col = (j % CB) * 16 + fr;
-      const int h = (r + oyh) * HW2 + col + oxh;
-      fb[j] = as_frag(*reinterpret_cast<const uint4*>(hbase + (h * 4 + (fq ^ halo_swz(h))) * 16));
-    }
-  };
-
-  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
-  int g = 0;   // slices computed so far (buffer parity)
-  int t = blockIdx.x;
-  if (t < ntiles) issue(tile_of(t), 0, 0);
-  for (; t < ntiles; t += gridDim.x) {
-    const Tile T = tile_of(t);
-    f32x4_t acc[FI][FJ];
+    const int oyh = MODE == MODE_FWD ? ta : 2 - ta, oxh = MODE == MODE_FWD ? tb : 2 - tb;
+    const char* wbase = lds + (cs & 1) * WBUF + fwoff;
+    const char* hbase = lds + (cs & 1) * HBUF;
 #pragma unroll
     for (int i = 0; i < FI; ++i)
+      fa[i] = as_frag(*reinterpret_cast<const uint4*>(wbase + t * TCO * 64 + i * 1024));
 #pragma unroll
-      for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    for (int cs = 0; cs < nslice; ++cs, ++g) {
-      // slice cs landed (younger: only the previous tile's NIT epilogue stores, which
-      // drain while this tile computes); every wave is done with the other buffer
-      if (cs == 0 && t != (int)blockIdx.x) wait_vmcnt_barrier<NIT>();
-      else wait_vmcnt_barrier<0>();
-      if (cs + 1 < nslice) issue(T, cs + 1, (g + 1) & 1);
-      else if (t + (int)gridDim.x < ntiles) issue(tile_of(t + gridDim.x), 0, (g + 1) & 1);
-      const int buf = g & 1;
-      int z;
-      asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-      bf16x8_t fa[2][FI], fb[2][FJ];
-      rd(buf, 0, z, fa[0], fb[0]);
+    for (int j = 0; j < FJ; ++j)
+      fb[j] = as_frag(*reinterpret_cast<const uint4*>(hbase + fhoff[oxh] + (oyh + j / CB) * HW2 * 64 + (j % CB) * 1024));
+  };
+  issue(0);
+  for (int cs = 0; cs < nslice; ++cs) {
+    wait_vmcnt_barrier<0>();   // slice cs landed; every wave is done with slice cs - 1's buffers
+    if (cs + 1 < nslice) issue(cs + 1);
+    bf16x8_t fa[2][FI], fb[2][FJ];
+    rd(cs, 0, fa[0], fb[0]);
 #pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        if (k + 1 < 9) rd(buf, k + 1, z, fa[(k + 1) & 1], fb[(k + 1) & 1]);
-        if (EEGAN_HALO_KNOCK & 4) continue;
+    for (int t = 0; t < 9; ++t) {
+      // tap t + 1's fragments are requested before tap t's MFMAs (the compiler sinks each
+      // read to its first use; pinning them ahead with scheduling fences measured the same,
+      // within 1 %: the LDS latency is not what bounds this loop)
+      if (t + 1 < 9) rd(cs, t + 1, fa[(t + 1) & 1], fb[(t + 1) & 1]);
+      if (EEGAN_HALO_KNOCK & 4) continue;
 #pragma unroll
-        for (int i = 0; i < FI; ++i)
+      for (int i = 0; i < FI; ++i)
 #pragma unroll
-          for (int j = 0; j < FJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[k & 1][i], fb[k & 1][j], acc[i][j], 0, 0, 0);
-      }
-    }
-    // epilogue in the MFMA layout (4 channels of one pixel per lane): bias, activation, gate,
-    // residual in fp32 with one final rounding, then the bf16 tile through the LDS buffer the
-    // last slice used ([pixel][8 chunks of 8 channels], chunk c of pixel p at c ^ (p & 7)) and
-    // out as whole 16-B runs; the stores drain during the next tile's slices
-    __syncthreads();
-    char* stg = lds + ((g - 1) & 1) * BUF;
-#pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-      const int p = (wj * WROWS + j / CB) * TW + (j % CB) * 16 + fr;
-      const int y = T.oy0 + p / TW, x = T.ox0 + p % TW;
-      const long gp = ((long)T.n * a.OH + y) * a.OW + x;
-#pragma unroll
-      for (int i = 0; i < FI; ++i) {
-        const int cl = i * 16 + fq * 4, co = T.co0 + cl;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          v[r] = act_fwd(acc[i][j][r] + ((a.bias && co + r < a.Mrows) ? a.bias[co + r] : 0.f), a.act, a.slope);
-        if (co < a.Mrows) {
-          if (MODE == MODE_BWDD && a.gate) {
-            const uint2 gv = *reinterpret_cast<const uint2*>(a.gate + gp * a.ldgate + co);
-            const float gg[4] = {lo_f(gv.x), hi_f(gv.x), lo_f(gv.y), hi_f(gv.y)};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] *= act_dgrad_from_y(gg[r], a.gate_act, a.gate_slope);
-          }
-          if (a.res) {
-            const long rp = a.res_up2 ? ((long)T.n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1) : gp;
-            const uint2 rv = *reinterpret_cast<const uint2*>(a.res + rp * a.ldres + co);
-            const float rr[4] = {lo_f(rv.x), hi_f(rv.x), lo_f(rv.y), hi_f(rv.y)};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = res_combine(a.res_scale, rr[r], gam, v[r]);
-          }
-        }
-        *reinterpret_cast<uint2*>(stg + p * TCO * 2 + (((cl >> 3) ^ (p & 7)) << 4) + (cl & 4) * 2) =
-            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < NIT; ++k) {
-      const int item = k * NT + tid, p = item / NCK, e = item % NCK;
-      const uint4 v = *reinterpret_cast<const uint4*>(stg + p * TCO * 2 + ((e ^ (p & 7)) << 4));
-      const long gp = ((long)T.n * a.OH + T.oy0 + p / TW) * a.OW + T.ox0 + p % TW;
-      if (T.co0 + 8 * e < a.Mrows && (!(EEGAN_HALO_KNOCK & 2) || v.x == 0x7fc17fc1u))
-        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + gp * a.ldo + T.co0 + 8 * e) = v;
+        for (int j = 0; j < FJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t & 1][i], fb[t & 1][j], acc[i][j], 0, 0, 0);
     }
   }
+  // epilogue: the gate / residual runs of this thread's items are loaded first, so their
+  // latency overlaps the LDS staging; fp32 tile [pixel][16 chunks of 4 channels], chunk c
+  // of pixel p at c ^ (p & 15)
+  constexpr int NIT = TPIX * (TCO / 8) / NT;
+  uint4 gpre[NIT], rpre[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int item = k * NT + tid, p = item / (TCO / 8), e = item % (TCO / 8);
+    const int co = co0 + 8 * e;
+    const int y = oy0 + p / TW, x = ox0 + p % TW;
+    const long gp = ((long)n * a.OH + y) * a.OW + x;
+    gpre[k] = rpre[k] = make_uint4(0, 0, 0, 0);
+    if (co < a.Mrows) {
+      if (MODE == MODE_BWDD && a.gate) gpre[k] = *reinterpret_cast<const uint4*>(a.gate + gp * a.ldgate + co);
+      if (a.res) {
+        const long rp = a.res_up2 ? ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1) : gp;
+        rpre[k] = *reinterpret_cast<const uint4*>(a.res + rp * a.ldres + co);
+      }
+    }
+  }
+  __syncthreads();
+  float4* st = reinterpret_cast<float4*>(lds);
+#pragma unroll
+  for (int j = 0; j < FJ; ++j) {
+    const int p = (wj * WROWS + j / CB) * TW + (j % CB) * 16 + fr;
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const int c = i * 4 + fq;
+      st[p * NCK + (c ^ (p & 15))] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+  }
+  __syncthreads();
+  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int item = k * NT + tid, p = item / (TCO / 8), e = item % (TCO / 8);
+    const int co = co0 + 8 * e;
+    if (co >= a.Mrows) continue;
+    const float4 lo = st[p * NCK + ((2 * e) ^ (p & 15))];
+    const float4 hi = st[p * NCK + ((2 * e + 1) ^ (p & 15))];
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const int y = oy0 + p / TW, x = ox0 + p % TW;
+    const long gp = ((long)n * a.OH + y) * a.OW + x;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = act_fwd(v[r] + (a.bias ? a.bias[co + r] : 0.f), a.act, a.slope);
+    if (MODE == MODE_BWDD && a.gate) {
+      const uint4 gv = gpre[k];
+      const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[2 * r] *= act_dgrad_from_y(lo_f(gw[r]), a.gate_act, a.gate_slope);
+        v[2 * r + 1] *= act_dgrad_from_y(hi_f(gw[r]), a.gate_act, a.gate_slope);
+      }
+    }
+    if (a.res) {
+      const uint4 rv = rpre[k];
+      const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[2 * r] = res_combine(a.res_scale, lo_f(rw[r]), gam, v[2 * r]);
+        v[2 * r + 1] = res_combine(a.res_scale, hi_f(rw[r]), gam, v[2 * r + 1]);
+      }
+    }
+    const uint4 o = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+    if (!(EEGAN_HALO_KNOCK & 2) || o.x == 0x7fc17fc1u)
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + gp * a.ldo + co) = o;
+  }
 }
+
+
 
 // ---------------------------------------------------------- WGRAD kernel --
 struct WgradArgs {
@@ -2820,15 +2825,12 @@ int try_halo3(const ConvArgs& a, hipStream_t s, long src_bytes, long w_bytes) {
   const int big = knob("halo_th", 0);   // 16 / 8: force the tile height (tests, sweeps)
   const bool th16 = big == 16 || (big != 8 && tiles16 >= 256);
   if (th16 && !tiles16) return 0;
-  // persistent: one workgroup per CU (160 KB / 120 KB of LDS), each walks tiles blockIdx.x + k * grid
-  const int cus = knob("halo_grid", 256);
   if (th16) {
-    ee_launch(conv_halo3_kernel<MODE, 16, 8>, dim3((unsigned)std::min<long>(tiles16, cus)), dim3(512), 0, s, a,
-              src_bytes, w_bytes);
+    dim3 grid((unsigned)(tiles16 / co_t), co_t);
+    ee_launch(conv_halo3_kernel<MODE, 16, 8>, grid, dim3(512), 0, s, a, src_bytes, w_bytes);
   } else {
-    const long tiles8 = (long)a.N * (a.OH / 8) * (a.OW / HALO_TW) * co_t;
-    ee_launch(conv_halo3_kernel<MODE, 8, 4>, dim3((unsigned)std::min<long>(tiles8, cus)), dim3(256), 0, s, a,
-              src_bytes, w_bytes);
+    dim3 grid((unsigned)((long)a.N * (a.OH / 8) * (a.OW / HALO_TW)), co_t);
+    ee_launch(conv_halo3_kernel<MODE, 8, 4>, grid, dim3(256), 0, s, a, src_bytes, w_bytes);
   }
   const int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd(halo3)" : "conv_bwd_data(halo3)");
   return rc ? rc : 1;

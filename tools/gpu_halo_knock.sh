@@ -20,3 +20,13 @@ for k in ${KNOCKS:-1 2 3 4 6}; do
   step 200 ${TAG}_k$k env EEGAN_HIP_LIB=$PWD/tools/ab_lib/libeegan_hip_knock$k.so python3 tools/conv_bench.py --shapes $S --dirs fwd,bwdd --device-time
 done
 for k in 0 ${KNOCKS:-1 2 3 4 6}; do echo "== knock $k"; grep -h 'TF/s' gpurun_out/${TAG}_k$k.log; done
+# D256's d_update alone, kernel by kernel (rocprofv3 kernel trace, one stream)
+if [ -n "$LANE" ]; then
+  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+  step 300 ${TAG}_lt_d2 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${TAG}_lt_d2 -o run -- python3 tools/lane_trace.py --d 2
+  LANE_TOP=40 python3 tools/lane_trace.py --report gpurun_out/${TAG}_lt_d2 > gpurun_out/${TAG}_lt_d2_report.txt
+  find gpurun_out/${TAG}_lt_d2 -name '*.csv' -delete
+  step 300 ${TAG}_lt_all rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${TAG}_lt_all -o run -- python3 tools/lane_trace.py --d -1
+  LANE_TOP=40 python3 tools/lane_trace.py --report gpurun_out/${TAG}_lt_all > gpurun_out/${TAG}_lt_all_report.txt
+  find gpurun_out/${TAG}_lt_all -name '*.csv' -delete
+fi
