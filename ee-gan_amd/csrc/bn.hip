@@ -32,20 +32,33 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(const bf16_t* __restrict
   if (row < rows) {
     const int c = cg * 8;
     const bool vec = (ld % 8) == 0;
-    for (long p = p0 + row; p < p1; p += rows) {
-      const bf16_t* src = x + p * ld + c;
-      if (vec) {
-        uint4 v = *reinterpret_cast<const uint4*>(src);
-        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    long p = p0 + row;
+    if (vec) {
+      // SU pixels' loads in flight per thread, summed in pixel order (as one at a time)
+      constexpr int SU = 4;
+      for (; p < p1; p += SU * rows) {
+        uint4 v[SU];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float a = lo_f(w4[j]), b = hi_f(w4[j]);
-          s[2 * j] += a;
-          q[2 * j] += a * a;
-          s[2 * j + 1] += b;
-          q[2 * j + 1] += b * b;
+        for (int u = 0; u < SU; ++u)
+          if (p + u * rows < p1) v[u] = *reinterpret_cast<const uint4*>(x + (p + u * rows) * ld + c);
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          if (p + u * rows >= p1) break;
+          const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float a = lo_f(w4[j]), b = hi_f(w4[j]);
+            s[2 * j] += a;
+            q[2 * j] += a * a;
+            s[2 * j + 1] += b;
+            q[2 * j + 1] += b * b;
+          }
         }
-      } else {
+      }
+    }
+    for (; p < p1; p += rows) {
+      const bf16_t* src = x + p * ld + c;
+      {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (c + j < C) {
@@ -227,6 +240,10 @@ __global__ __launch_bounds__(NT) void bnmod_fwd_kernel(ModArgs a, bf16_t* __rest
 }
 
 // ------------------------------------------------------ backward, pass 1 --
+// RU pixels' loads per thread are issued before their arithmetic (2 left the
+// reduce at ~3 TB/s on the generator's 128^2 / 256^2 layers)
+constexpr int RU = 4;
+
 // grid: (chunks, N). Each block reduces a pixel range of ONE sample into
 // ws[n][chunk][4][C]:  S0 = sum g*m*xhat, S1 = sum g*m (ssa: dgamma/dbeta
 // partials; affine: sum g*xhat / sum g), S2 = sum dxhat, S3 = sum dxhat*xhat.
@@ -258,11 +275,11 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_reduce_kernel(ModArgs a, const b
   // power of two <= 64: its dmask is then a shuffle reduction (no LDS, no barriers)
   const bool wave_red = (C8 & (C8 - 1)) == 0 && C8 <= 64;
   // base of the pixel loop must be block-uniform for the dmask reduction
-  for (int qb = q0; qb < q1; qb += 2 * rows) {
-    uint4 xr[2], gr[2];
-    float mr[2];
+  for (int qb = q0; qb < q1; qb += RU * rows) {
+    uint4 xr[RU], gr[RU];
+    float mr[RU];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < RU; ++u) {
       const int q = qb + u * rows + row;
       if (row < rows && q < q1) {
         const int oy = (unsigned)q / (unsigned)Wo, ox = q - oy * Wo;
@@ -274,7 +291,7 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_reduce_kernel(ModArgs a, const b
       }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < RU; ++u) {
       const int q = qb + u * rows + row;
       float dm = 0.f;
       if (row < rows && q < q1) {
@@ -386,40 +403,25 @@ __global__ void bnmod_bwd_sums_kernel(const double* __restrict__ tmp, int N, int
 // dx (physical input grid) = istd * (dxhat - mean(dxhat) - xhat*mean(dxhat*xhat)), summed
 // over the 2x2 children when the forward upsampled.  grid (chunks, N) over
 // input pixels of sample n.
-__global__ __launch_bounds__(NT) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_t* __restrict__ dt, int lddt,
-                                                          const double* __restrict__ chan, double count,
-                                                          bf16_t* __restrict__ dx, int lddx, int ppc) {
-  const int C8 = (a.C + 7) / 8, rows = NT / C8;
-  const int row = threadIdx.x / C8, cg = threadIdx.x - row * C8;
-  if (row >= rows) return;
-  const int n = blockIdx.y, c0 = cg * 8, nv = a.C - c0;
+// DXU input pixels x NCH (1, or the 4 upsampled) output children per iteration, loads first
+template <int DXU, int NCH>
+EE_DEV void bwd_dx_body(const ModArgs& a, const bf16_t* __restrict__ dt, int lddt, bf16_t* __restrict__ dx, int lddx,
+                        int ppc, const ChanParams& P, const float (&vg)[8], const float (&m1)[8], const float (&m2)[8],
+                        int n, int c0, int nv, int row, int rows, int q1) {
   const int Ho = a.H << a.up2, Wo = a.W << a.up2;
   const int HW = a.H * a.W;
-  const int q1 = min(HW, ((int)blockIdx.x + 1) * ppc);
-  const int nch = a.up2 ? 4 : 1;
-  ChanParams P;
-  load_params(a, n, c0, P);
-  float vg[8], m1[8], m2[8];
+  for (int qb = (int)blockIdx.x * ppc + row; qb < q1; qb += DXU * rows) {
+    uint4 xr[DXU], gr[DXU][NCH];
+    float mr[DXU][NCH];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = min(c0 + j, a.C - 1);
-    vg[j] = a.stats[2 * a.C + c];
-    m1[j] = (float)(chan[c] / count);
-    m2[j] = (float)(chan[a.C + c] / count);
-  }
-  for (int qb = (int)blockIdx.x * ppc + row; qb < q1; qb += 2 * rows) {
-    // two input pixels x (1 or 4) output children per iteration, loads first
-    uint4 xr[2], gr[2][4];
-    float mr[2][4];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < DXU; ++u) {
       const int q = qb + u * rows;
       if (q < q1) {
         const int iy = (unsigned)q / (unsigned)a.W, ix = q - iy * a.W;
         xr[u] = *reinterpret_cast<const uint4*>(a.x + ((long)n * HW + q) * a.ldx + c0);
 #pragma unroll
-        for (int ch = 0; ch < 4; ++ch) {
-          if (ch < nch) {
+        for (int ch = 0; ch < NCH; ++ch) {
+          {
             const int oy = (iy << a.up2) + (ch >> 1), ox = (ix << a.up2) + (ch & 1);
             const long op = ((long)n * Ho + oy) * Wo + ox;
             gr[u][ch] = *reinterpret_cast<const uint4*>(dt + op * lddt + c0);
@@ -429,7 +431,7 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_
       }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < DXU; ++u) {
       const int q = qb + u * rows;
       if (q >= q1) break;
       float xh[8], o[8];
@@ -440,8 +442,7 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_
         o[j] = 0.f;
       }
 #pragma unroll
-      for (int ch = 0; ch < 4; ++ch) {
-        if (ch >= nch) break;
+      for (int ch = 0; ch < NCH; ++ch) {
         float gv[8];
         unpack8(gr[u][ch], gv);
 #pragma unroll
@@ -458,6 +459,28 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_
       store8(dx + ((long)n * HW + q) * lddx + c0, o, nv);
     }
   }
+}
+
+__global__ __launch_bounds__(NT) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_t* __restrict__ dt, int lddt,
+                                                          const double* __restrict__ chan, double count,
+                                                          bf16_t* __restrict__ dx, int lddx, int ppc) {
+  const int C8 = (a.C + 7) / 8, rows = NT / C8;
+  const int row = threadIdx.x / C8, cg = threadIdx.x - row * C8;
+  if (row >= rows) return;
+  const int n = blockIdx.y, c0 = cg * 8, nv = a.C - c0;
+  const int q1 = min(a.H * a.W, ((int)blockIdx.x + 1) * ppc);
+  ChanParams P;
+  load_params(a, n, c0, P);
+  float vg[8], m1[8], m2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = min(c0 + j, a.C - 1);
+    vg[j] = a.stats[2 * a.C + c];
+    m1[j] = (float)(chan[c] / count);
+    m2[j] = (float)(chan[a.C + c] / count);
+  }
+  if (a.up2) bwd_dx_body<2, 4>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
+  else bwd_dx_body<4, 1>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
 }
 
 ModArgs make_args(const eegan_bnmod_desc* d) {
