@@ -312,33 +312,16 @@ EE_DEV void staged_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], flo
 
 // split-K reduction + epilogue: out[p][co] = res + gamma*act(sum_z part[z][p][co] + bias).
 //
-// 4 consecutive channels of one pixel: 16-byte slab loads (4 splits in
-// flight), 8-byte residual / gate loads and stores; 32-bit index math (the
-// host enables this path only for P * Mrows < 2^31)
+// 4 consecutive channels of one pixel: the residual / gate / bias loads are
+// issued first, then the 16-byte slab loads 8 splits at a time (one memory
+// round trip for the usual 8-way split), summed in split order (bit-identical
+// to the scalar path); 32-bit index math (the host enables this path only for
+// P * Mrows < 2^31)
 EE_DEV void splitk_item4(const ConvArgs& a, unsigned p, unsigned co, float gam) {
   const unsigned total4 = (unsigned)(((long)a.P * a.Mrows) >> 2);
   const unsigned i = (p * (unsigned)a.Mrows + co) >> 2;
-  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-  const f32x4_t* src = reinterpret_cast<const f32x4_t*>(a.part) + i;
-  int z = 0;
-  for (; z + 4 <= a.nsplit; z += 4) {
-    const f32x4_t v0 = src[(long)z * total4], v1 = src[(long)(z + 1) * total4];
-    const f32x4_t v2 = src[(long)(z + 2) * total4], v3 = src[(long)(z + 3) * total4];
-    acc += v0;  // same order as the scalar path: bit-identical sums
-    acc += v1;
-    acc += v2;
-    acc += v3;
-  }
-  for (; z < a.nsplit; ++z) acc += src[(long)z * total4];
-  float v[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = act_fwd(acc[r] + (a.bias ? a.bias[co + r] : 0.f), a.act, a.slope);
-  if (a.gate) {
-    const uint2 gv = *reinterpret_cast<const uint2*>(a.gate + (long)p * a.ldgate + co);
-    const float gg[4] = {lo_f(gv.x), hi_f(gv.x), lo_f(gv.y), hi_f(gv.y)};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] *= act_dgrad_from_y(gg[r], a.gate_act, a.gate_slope);
-  }
+  uint2 gv = make_uint2(0, 0), rv = make_uint2(0, 0);
+  if (a.gate) gv = *reinterpret_cast<const uint2*>(a.gate + (long)p * a.ldgate + co);
   if (a.res) {
     long rpix = p;
     if (a.res_up2) {
@@ -347,7 +330,30 @@ EE_DEV void splitk_item4(const ConvArgs& a, unsigned p, unsigned co, float gam) 
       const unsigned y = rem / (unsigned)a.OW, x = rem - y * (unsigned)a.OW;
       rpix = ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
     }
-    const uint2 rv = *reinterpret_cast<const uint2*>(a.res + rpix * a.ldres + co);
+    rv = *reinterpret_cast<const uint2*>(a.res + rpix * a.ldres + co);
+  }
+  f32x4_t bv = {0.f, 0.f, 0.f, 0.f};
+  if (a.bias) bv = f32x4_t{a.bias[co], a.bias[co + 1], a.bias[co + 2], a.bias[co + 3]};
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  const f32x4_t* src = reinterpret_cast<const f32x4_t*>(a.part) + i;
+  int z = 0;
+  for (; z + 8 <= a.nsplit; z += 8) {
+    f32x4_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = src[(long)(z + k) * total4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += v[k];   // split order, as the scalar path
+  }
+  for (; z < a.nsplit; ++z) acc += src[(long)z * total4];
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = act_fwd(acc[r] + bv[r], a.act, a.slope);
+  if (a.gate) {
+    const float gg[4] = {lo_f(gv.x), hi_f(gv.x), lo_f(gv.y), hi_f(gv.y)};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] *= act_dgrad_from_y(gg[r], a.gate_act, a.gate_slope);
+  }
+  if (a.res) {
     const float rr[4] = {lo_f(rv.x), hi_f(rv.x), lo_f(rv.y), hi_f(rv.y)};
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = res_combine(a.res_scale, rr[r], gam, v[r]);
