@@ -128,13 +128,13 @@ __global__ __launch_bounds__(COLS * RG) void colsum_rows_kernel(const float* __r
   Acc s = 0;
   if (c < ncols) {
     int r = g;
-    for (; r + 3 * RG < nrows; r += 4 * RG) {
-      const float a0 = in[(long)r * stride + c], a1 = in[(long)(r + RG) * stride + c];
-      const float a2 = in[(long)(r + 2 * RG) * stride + c], a3 = in[(long)(r + 3 * RG) * stride + c];
-      s += (Acc)a0;
-      s += (Acc)a1;
-      s += (Acc)a2;
-      s += (Acc)a3;
+    // 8 rows' loads per round trip, summed in row order (as one at a time)
+    for (; r + 7 * RG < nrows; r += 8 * RG) {
+      float a[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] = in[(long)(r + k * RG) * stride + c];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += (Acc)a[k];
     }
     for (; r < nrows; r += RG) s += (Acc)in[(long)r * stride + c];
   }

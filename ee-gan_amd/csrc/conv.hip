@@ -1376,13 +1376,13 @@ __global__ __launch_bounds__(COLS * RG) void wgrad_quad_reduce_kernel(const floa
   f32x4_t s = {0.f, 0.f, 0.f, 0.f};
   if (ok) {
     int r = g;
-    for (; r + 3 * RG < nrows; r += 4 * RG) {
-      const f32x4_t a0 = src[(long)r * st4], a1 = src[(long)(r + RG) * st4];
-      const f32x4_t a2 = src[(long)(r + 2 * RG) * st4], a3 = src[(long)(r + 3 * RG) * st4];
-      s += a0;
-      s += a1;
-      s += a2;
-      s += a3;
+    // 8 rows' loads per round trip, summed in row order (colsum_rows_kernel's)
+    for (; r + 7 * RG < nrows; r += 8 * RG) {
+      f32x4_t a[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] = src[(long)(r + k * RG) * st4];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += a[k];
     }
     for (; r < nrows; r += RG) s += src[(long)r * st4];
   }
