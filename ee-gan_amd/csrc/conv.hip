@@ -2814,14 +2814,16 @@ int try_thin(const ConvArgs& a, hipStream_t s, long src_bytes) {
   return rc ? rc : 1;
 }
 
-// 3x3 / stride-1 / pad-1 convs with >= 48 output rows on grids of whole 8 x 32
+// 3x3 / stride-1 / pad-1 convs with >= 32 output rows on grids of whole 8 x 32
 // tiles take conv_halo3_kernel (0: not eligible, else the launch rc)
 template <int MODE>
 int try_halo3(const ConvArgs& a, hipStream_t s, long src_bytes, long w_bytes) {
   if (!knob("halo", 1) || src_bytes >= 0x7fffffffL || w_bytes >= 0x7fffffffL) return 0;
   if (a.R != 3 || a.S != 3 || a.st != 1 || a.ph != 1 || a.pw != 1 || a.ncls != 1 || a.nsplit != 1) return 0;
   if (MODE == MODE_BWDD && a.up2) return 0;
-  if (a.Mrows < 48 || (a.Mrows & 7) || (a.Cvalid & 7) || a.Cgp % BK || a.out_f32) return 0;
+  // >= 32 rows: at 32 the 64-row tile idles half its MFMAs, and still beats the tile
+  // kernels by 17-19 % (fetch-bound; 3x3 64 -> 32 at 256^2 143 -> 118 us)
+  if (a.Mrows < 32 || (a.Mrows & 7) || (a.Cvalid & 7) || a.Cgp % BK || a.out_f32) return 0;
   if ((a.lds_src & 7) || ((uintptr_t)a.src & 15) || (a.ldo & 7) || ((uintptr_t)a.out & 15)) return 0;
   if (a.gate && ((a.ldgate & 7) || ((uintptr_t)a.gate & 15))) return 0;
   if (a.res && ((a.ldres & 7) || ((uintptr_t)a.res & 15))) return 0;

@@ -915,14 +915,14 @@ def test_conv_halo3_matches_tile_kernel(gpu, monkeypatch, th):
     fp32 conv: forward with bias / act / residual + gain and the fused nearest-2x
     upsample, backward-data plain / gated / with the half-resolution residual;
     ragged input channels (40 -> a masked chunk), two output-channel tiles with a
-    partial second one (96), both tile heights.  The halo kernel sums slice-major
+    partial second one (96), 32 output channels (half a tile), both tile heights.  The halo kernel sums slice-major
     (the tile kernels tap-major), so the gate is bf16 output rounding: rel-L2
     <= 5e-3 between the kernels, <= 1e-2 against fp32."""
     Fn, T, _ = _mods()
     conv_knob(monkeypatch, 'halo_th', th)
     lrelu = Fn.ACT_CODES['lrelu']
     for N, Cin, H, W, Cout, up2 in [(2, 64, 32, 64, 64, 0), (3, 40, 16, 32, 96, 0), (2, 128, 16, 32, 48, 0),
-                                    (2, 64, 16, 32, 64, 1), (1, 256, 32, 32, 128, 0)]:
+                                    (2, 64, 16, 32, 64, 1), (1, 256, 32, 32, 128, 0), (2, 64, 16, 32, 32, 0)]:
         torch.manual_seed(N * Cin + Cout + H + up2)
         g = Fn.Geom(Cout, 3, 3, 1, 1, 1, up2)
         xs = torch.randn(N, Cin, H // 2, W // 2) if up2 else torch.randn(N, Cin, H, W)

@@ -47,6 +47,7 @@ SHAPES = {
     'c3x3_128_100_64': (16, 128, 64, 64, 100, 3, 1, 1),
     'c3x3_64_32_128': (16, 64, 128, 128, 32, 3, 1, 1),
     'c3x3_32_16_256': (16, 32, 256, 256, 16, 3, 1, 1),
+    'c3x3_64_32_256': (16, 64, 256, 256, 32, 3, 1, 1),
     # Dis256 at N = 32 (real + fake batched), models.py resD blocks 0-5
     'd256_b0_s2': (32, 32, 256, 256, 64, 4, 2, 1),
     'd256_b0_3x3': (32, 64, 128, 128, 64, 3, 1, 1),
