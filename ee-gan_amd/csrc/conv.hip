@@ -286,7 +286,7 @@ EE_DEV void staged_epilogue(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], flo
     float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     const long p = ppre[k];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = act_fwd(v[r] + (a.bias ? a.bias[co + r] : 0.f), a.act, a.slope);
+    for (int r = 0; r < 8; ++r) v[r] = act_fwd(v[r] + ((a.bias && co + r < a.Mrows) ? a.bias[co + r] : 0.f), a.act, a.slope);
     if (MODE == MODE_BWDD && a.gate) {
       const uint4 gv = gpre[k];
       const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
@@ -1148,7 +1148,11 @@ constexpr int HALO_TW = 32, HALO_TCO = 64;
 
 EE_DEV int halo_swz(int hx) { return (hx >> 1) & 2; }
 
-template <int MODE, int TH, int WPX>
+// RAG: Cvalid % 8 != 0 -- the 16-B chunk straddling Cvalid carries the row's padding
+// channels (any bits): masked in the B fragments of that slice (as the tile kernels'
+// rag_mask).  Output rows Mrows % 8 != 0: the straddling chunk's valid channels are
+// stored one by one, nothing past Mrows is written.
+template <int MODE, int TH, int WPX, bool RAG = false>
 __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, long src_bytes, long w_bytes) {
   constexpr int NT = 64 * WPX, TW = HALO_TW, TCO = HALO_TCO, FI = TCO / 16;
   constexpr int WROWS = TH / WPX, CB = TW / 16, FJ = WROWS * CB;
@@ -1220,12 +1224,12 @@ __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, lon
   // i * 16 + fr is i-independent).  Halo: pixel column hx's swizzle depends on hx only (and
   // is the same for hx + 16), so B fragment j = (row jr, 16-column block jc) at tap shift
   // (oyh, oxh) is fhoff[oxh] + (oyh + jr) * HW2 * 64 + jc * 1024: 3 base registers.
-  // C % 8 != 0 is not taken here (whole 16-B chunks valid or zero)
   const int fwoff = 2 * HBUF + fr * 64 + ((fq ^ swz_b128((fr >> 2) & 3)) << 4);
   int fhoff[3];
 #pragma unroll
   for (int sx = 0; sx < 3; ++sx)
     fhoff[sx] = ((wj * WROWS * HW2 + fr + sx) << 6) + ((fq ^ halo_swz(fr + sx)) << 4);
+  uint4 rmsk = make_uint4(~0u, ~0u, ~0u, ~0u);   // RAG: this lane's chunk mask in the current slice
   auto rd = [&](int cs, int t, bf16x8_t (&fa)[FI], bf16x8_t (&fb)[FJ]) {
     const int ta = t / 3, tb = t - ta * 3;
     const int oyh = MODE == MODE_FWD ? ta : 2 - ta, oxh = MODE == MODE_FWD ? tb : 2 - tb;
@@ -1235,13 +1239,17 @@ __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, lon
     for (int i = 0; i < FI; ++i)
       fa[i] = as_frag(*reinterpret_cast<const uint4*>(wbase + t * TCO * 64 + i * 1024));
 #pragma unroll
-    for (int j = 0; j < FJ; ++j)
-      fb[j] = as_frag(*reinterpret_cast<const uint4*>(hbase + fhoff[oxh] + (oyh + j / CB) * HW2 * 64 + (j % CB) * 1024));
+    for (int j = 0; j < FJ; ++j) {
+      uint4 v = *reinterpret_cast<const uint4*>(hbase + fhoff[oxh] + (oyh + j / CB) * HW2 * 64 + (j % CB) * 1024);
+      if (RAG) v = make_uint4(v.x & rmsk.x, v.y & rmsk.y, v.z & rmsk.z, v.w & rmsk.w);
+      fb[j] = as_frag(v);
+    }
   };
   issue(0);
   for (int cs = 0; cs < nslice; ++cs) {
     wait_vmcnt_barrier<0>();   // slice cs landed; every wave is done with slice cs - 1's buffers
     if (cs + 1 < nslice) issue(cs + 1);
+    if (RAG) rmsk = mask_chunk(make_uint4(~0u, ~0u, ~0u, ~0u), cs * BK + 8 * fq, a.Cvalid);
     bf16x8_t fa[2][FI], fb[2][FJ];
     rd(cs, 0, fa[0], fb[0]);
 #pragma unroll
@@ -1302,7 +1310,7 @@ __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, lon
     const int y = oy0 + p / TW, x = ox0 + p % TW;
     const long gp = ((long)n * a.OH + y) * a.OW + x;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = act_fwd(v[r] + (a.bias ? a.bias[co + r] : 0.f), a.act, a.slope);
+    for (int r = 0; r < 8; ++r) v[r] = act_fwd(v[r] + ((a.bias && co + r < a.Mrows) ? a.bias[co + r] : 0.f), a.act, a.slope);
     if (MODE == MODE_BWDD && a.gate) {
       const uint4 gv = gpre[k];
       const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
@@ -1321,9 +1329,13 @@ __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, lon
         v[2 * r + 1] = res_combine(a.res_scale, hi_f(rw[r]), gam, v[2 * r + 1]);
       }
     }
+    bf16_t* dst = reinterpret_cast<bf16_t*>(a.out) + gp * a.ldo + co;
+    if (co + 8 > a.Mrows) {   // the output row's last, partial chunk
+      for (int r = 0; r < a.Mrows - co; ++r) dst[r] = f2bf(v[r]);
+      continue;
+    }
     const uint4 o = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
-    if (!(EEGAN_HALO_KNOCK & 2) || o.x == 0x7fc17fc1u)
-      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + gp * a.ldo + co) = o;
+    if (!(EEGAN_HALO_KNOCK & 2) || o.x == 0x7fc17fc1u) *reinterpret_cast<uint4*>(dst) = o;
   }
 }
 
@@ -2823,7 +2835,8 @@ int try_halo3(const ConvArgs& a, hipStream_t s, long src_bytes, long w_bytes) {
   if (MODE == MODE_BWDD && a.up2) return 0;
   // >= 32 rows: at 32 the 64-row tile idles half its MFMAs, and still beats the tile
   // kernels by 17-19 % (fetch-bound; 3x3 64 -> 32 at 256^2 143 -> 118 us)
-  if (a.Mrows < 32 || (a.Mrows & 7) || (a.Cvalid & 7) || a.Cgp % BK || a.out_f32) return 0;
+  if (a.Mrows < 32 || a.Cgp % BK || a.out_f32) return 0;
+  if ((a.Cvalid & 7) && MODE != MODE_BWDD) return 0;   // ragged inputs: data gradients only (get_mask's 100-ch)
   if ((a.lds_src & 7) || ((uintptr_t)a.src & 15) || (a.ldo & 7) || ((uintptr_t)a.out & 15)) return 0;
   if (a.gate && ((a.ldgate & 7) || ((uintptr_t)a.gate & 15))) return 0;
   if (a.res && ((a.ldres & 7) || ((uintptr_t)a.res & 15))) return 0;
@@ -2833,13 +2846,17 @@ int try_halo3(const ConvArgs& a, hipStream_t s, long src_bytes, long w_bytes) {
   const int big = knob("halo_th", 0);   // 16 / 8: force the tile height (tests, sweeps)
   const bool th16 = big == 16 || (big != 8 && tiles16 >= 256);
   if (th16 && !tiles16) return 0;
-  if (th16) {
-    dim3 grid((unsigned)(tiles16 / co_t), co_t);
-    ee_launch(conv_halo3_kernel<MODE, 16, 8>, grid, dim3(512), 0, s, a, src_bytes, w_bytes);
-  } else {
-    dim3 grid((unsigned)((long)a.N * (a.OH / 8) * (a.OW / HALO_TW)), co_t);
-    ee_launch(conv_halo3_kernel<MODE, 8, 4>, grid, dim3(256), 0, s, a, src_bytes, w_bytes);
+  const dim3 grid16((unsigned)(tiles16 / co_t), co_t), grid8((unsigned)((long)a.N * (a.OH / 8) * (a.OW / HALO_TW)), co_t);
+  if constexpr (MODE == MODE_BWDD) {
+    if (a.Cvalid & 7) {
+      if (th16) ee_launch(conv_halo3_kernel<MODE, 16, 8, true>, grid16, dim3(512), 0, s, a, src_bytes, w_bytes);
+      else ee_launch(conv_halo3_kernel<MODE, 8, 4, true>, grid8, dim3(256), 0, s, a, src_bytes, w_bytes);
+      const int rc = ee_check_launch("conv_bwd_data(halo3)");
+      return rc ? rc : 1;
+    }
   }
+  if (th16) ee_launch(conv_halo3_kernel<MODE, 16, 8>, grid16, dim3(512), 0, s, a, src_bytes, w_bytes);
+  else ee_launch(conv_halo3_kernel<MODE, 8, 4>, grid8, dim3(256), 0, s, a, src_bytes, w_bytes);
   const int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd(halo3)" : "conv_bwd_data(halo3)");
   return rc ? rc : 1;
 }

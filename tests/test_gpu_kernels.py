@@ -956,3 +956,36 @@ def test_conv_halo3_matches_tile_kernel(gpu, monkeypatch, th):
         if not up2:
             dref = F.conv_transpose2d(dz.float().cpu(), Wt.cpu().to(torch.bfloat16).float(), None, 1, 1)
             assert rel_l2(outs['1'][2], dref) <= 1e-2
+
+
+@pytest.mark.gpu
+def test_conv_halo3_ragged_channels(gpu, monkeypatch):
+    """The halo kernel on get_mask's 100-channel conv (models.py:34-41): the
+    forward's 100 output rows end in a partial 8-channel chunk (its valid
+    channels stored one by one, nothing past 100 written), the data gradient
+    reads a 100-channel dy whose padding channels hold NaN bits (masked in the
+    B fragments).  Against the tile kernels (halo=0) and torch fp32."""
+    Fn, T, _ = _mods()
+    N, Cin, H, W, Cout = 2, 64, 16, 32, 100
+    torch.manual_seed(7)
+    g = Fn.Geom(Cout, 3, 3, 1, 1, 1, 0)
+    xs = torch.randn(N, Cin, H, W)
+    x = _nhwc(xs, gpu)
+    Wt = (torch.randn(Cout, Cin, 3, 3) * (1.0 / (9 * Cin) ** 0.5)).to(gpu)
+    b = torch.randn(Cout).to(gpu) * 0.1
+    dzs = torch.randn(N, Cout, H, W)
+    dz = _nhwc_nan_padded(dzs, gpu)
+    outs = {}
+    for on in ('0', '1'):
+        conv_knob(monkeypatch, 'halo', on)
+        y = Fn.conv_fwd_raw(x, Wt, b, g, act=Fn.ACT_CODES['relu'])
+        dx = Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape))
+        outs[on] = (y.float().cpu(), dx.float().cpu())
+    for a, c in zip(outs['1'], outs['0']):
+        assert torch.isfinite(a).all()
+        assert rel_l2(a, c) <= 5e-3
+    wb = Wt.cpu().to(torch.bfloat16).float()
+    yref = F.relu(F.conv2d(xs.to(torch.bfloat16).float(), wb, b.cpu(), 1, 1))
+    assert rel_l2(outs['1'][0], yref) <= 1e-2
+    dref = F.conv_transpose2d(dzs.to(torch.bfloat16).float(), wb, None, 1, 1)
+    assert rel_l2(outs['1'][1], dref) <= 1e-2
