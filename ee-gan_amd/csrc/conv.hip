@@ -1152,15 +1152,18 @@ EE_DEV int halo_swz(int hx) { return (hx >> 1) & 2; }
 // channels (any bits): masked in the B fragments of that slice (as the tile kernels'
 // rag_mask).  Output rows Mrows % 8 != 0: the straddling chunk's valid channels are
 // stored one by one, nothing past Mrows is written.
-template <int MODE, int TH, int WPX, bool RAG = false>
-__global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, long src_bytes, long w_bytes) {
+template <int MODE, int TH, int WPX, bool RAG = false, int NBUF = 2>
+__global__ __launch_bounds__(64 * WPX, NBUF == 1 ? 2 : 1) void conv_halo3_kernel(ConvArgs a, long src_bytes,
+                                                                               long w_bytes) {
   constexpr int NT = 64 * WPX, TW = HALO_TW, TCO = HALO_TCO, FI = TCO / 16;
   constexpr int WROWS = TH / WPX, CB = TW / 16, FJ = WROWS * CB;
   constexpr int HW2 = TW + 2, HP = (TH + 2) * HW2, HOPS = (HP * 4 + NT - 1) / NT, HBUF = HOPS * NT * 16;
   constexpr int WCH = 9 * TCO * 4, WOPS = (WCH + NT - 1) / NT, WBUF = WOPS * NT * 16;
   constexpr int TPIX = TH * TW, NCK = TCO / 4;
-  static_assert(WROWS >= 1 && TPIX * TCO * 4 <= 2 * (HBUF + WBUF), "halo tile");
-  __shared__ __attribute__((aligned(16))) char lds[2 * (HBUF + WBUF)];
+  // NBUF = 1: one slice buffer, two workgroups per CU (one's loads under the other's MFMAs)
+  constexpr int LDSB = NBUF * (HBUF + WBUF) > TPIX * TCO * 4 ? NBUF * (HBUF + WBUF) : TPIX * TCO * 4;
+  static_assert(WROWS >= 1 && (NBUF == 1 || NBUF == 2), "halo tile");
+  __shared__ __attribute__((aligned(16))) char lds[LDSB];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wj = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1201,7 +1204,7 @@ __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, lon
   }
   auto issue = [&](int cs) {   // slice cs: halo into buffer cs & 1, weights into buffer cs & 1
     if (EEGAN_HALO_KNOCK & 1) return;
-    const int buf = cs & 1;
+    const int buf = NBUF == 2 ? cs & 1 : 0;
 #pragma unroll
     for (int i = 0; i < HOPS; ++i) {
       const bool ok = hoff[i] != OOB && cs * BK + hq[i] * 8 < a.Cvalid;
@@ -1210,7 +1213,7 @@ __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, lon
     }
 #pragma unroll
     for (int i = 0; i < WOPS; ++i)
-      lds_dma16s(rs_w, lds0 + 2 * HBUF + buf * WBUF + (i * NT + wj * 64) * 16, woff[i], cs * 64);
+      lds_dma16s(rs_w, lds0 + NBUF * HBUF + buf * WBUF + (i * NT + wj * 64) * 16, woff[i], cs * 64);
   };
 
   f32x4_t acc[FI][FJ];
@@ -1224,7 +1227,7 @@ __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, lon
   // i * 16 + fr is i-independent).  Halo: pixel column hx's swizzle depends on hx only (and
   // is the same for hx + 16), so B fragment j = (row jr, 16-column block jc) at tap shift
   // (oyh, oxh) is fhoff[oxh] + (oyh + jr) * HW2 * 64 + jc * 1024: 3 base registers.
-  const int fwoff = 2 * HBUF + fr * 64 + ((fq ^ swz_b128((fr >> 2) & 3)) << 4);
+  const int fwoff = NBUF * HBUF + fr * 64 + ((fq ^ swz_b128((fr >> 2) & 3)) << 4);
   int fhoff[3];
 #pragma unroll
   for (int sx = 0; sx < 3; ++sx)
@@ -1233,8 +1236,8 @@ __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, lon
   auto rd = [&](int cs, int t, bf16x8_t (&fa)[FI], bf16x8_t (&fb)[FJ]) {
     const int ta = t / 3, tb = t - ta * 3;
     const int oyh = MODE == MODE_FWD ? ta : 2 - ta, oxh = MODE == MODE_FWD ? tb : 2 - tb;
-    const char* wbase = lds + (cs & 1) * WBUF + fwoff;
-    const char* hbase = lds + (cs & 1) * HBUF;
+    const char* wbase = lds + (NBUF == 2 ? cs & 1 : 0) * WBUF + fwoff;
+    const char* hbase = lds + (NBUF == 2 ? cs & 1 : 0) * HBUF;
 #pragma unroll
     for (int i = 0; i < FI; ++i)
       fa[i] = as_frag(*reinterpret_cast<const uint4*>(wbase + t * TCO * 64 + i * 1024));
@@ -1248,7 +1251,7 @@ __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, lon
   issue(0);
   for (int cs = 0; cs < nslice; ++cs) {
     wait_vmcnt_barrier<0>();   // slice cs landed; every wave is done with slice cs - 1's buffers
-    if (cs + 1 < nslice) issue(cs + 1);
+    if (NBUF == 2 && cs + 1 < nslice) issue(cs + 1);
     if (RAG) rmsk = mask_chunk(make_uint4(~0u, ~0u, ~0u, ~0u), cs * BK + 8 * fq, a.Cvalid);
     bf16x8_t fa[2][FI], fb[2][FJ];
     rd(cs, 0, fa[0], fb[0]);
@@ -1264,6 +1267,10 @@ __global__ __launch_bounds__(64 * WPX, 1) void conv_halo3_kernel(ConvArgs a, lon
 #pragma unroll
         for (int j = 0; j < FJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t & 1][i], fb[t & 1][j], acc[i][j], 0, 0, 0);
+    }
+    if (NBUF == 1 && cs + 1 < nslice) {
+      __syncthreads();   // every wave is done with the one buffer
+      issue(cs + 1);
     }
   }
   // epilogue: the gate / residual runs of this thread's items are loaded first, so their
@@ -2855,7 +2862,15 @@ int try_halo3(const ConvArgs& a, hipStream_t s, long src_bytes, long w_bytes) {
       return rc ? rc : 1;
     }
   }
-  if (th16) ee_launch(conv_halo3_kernel<MODE, 16, 8>, grid16, dim3(512), 0, s, a, src_bytes, w_bytes);
+  // default: two single-buffered 8-row workgroups per CU (one's slice loads, first-slice wait and
+  // epilogue run under the other's MFMAs; 64 KB of LDS each, so other lanes' kernels still fit
+  // beside them).  Per kernel it wins on 2-slice layers (D256 b0 66 -> 58 us) and loses on 8-slice
+  // ones (25.7 -> 28.7 us); on the replayed step +0.4 / +0.6 % against halo_nb=2 (the double-
+  // buffered one-workgroup-per-CU forms) and +0.4 % against choosing it for <= 2 slices only
+  const int nb = knob("halo_nb", 1);
+  if (!big && nb == 1)
+    ee_launch(conv_halo3_kernel<MODE, 8, 4, false, 1>, grid8, dim3(256), 0, s, a, src_bytes, w_bytes);
+  else if (th16) ee_launch(conv_halo3_kernel<MODE, 16, 8>, grid16, dim3(512), 0, s, a, src_bytes, w_bytes);
   else ee_launch(conv_halo3_kernel<MODE, 8, 4>, grid8, dim3(256), 0, s, a, src_bytes, w_bytes);
   const int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd(halo3)" : "conv_bwd_data(halo3)");
   return rc ? rc : 1;

@@ -908,14 +908,16 @@ def test_flat_adam_repacks_conv_weights(gpu):
             assert torch.equal(buf, Fn.pack_weight(m.weight, tr))
 
 
-@pytest.mark.parametrize('th', ['16', '8'])
+@pytest.mark.parametrize('th', ['16', '8', '0'])
 def test_conv_halo3_matches_tile_kernel(gpu, monkeypatch, th):
     """3x3 / stride-1 convs on the LDS halo-tile kernel (conv_halo3_kernel,
     EEGAN_CONV halo=1, default) against the tile kernels (halo=0) and torch's
     fp32 conv: forward with bias / act / residual + gain and the fused nearest-2x
     upsample, backward-data plain / gated / with the half-resolution residual;
     ragged input channels (40 -> a masked chunk), two output-channel tiles with a
-    partial second one (96), 32 output channels (half a tile), both tile heights.  The halo kernel sums slice-major
+    partial second one (96), 32 output channels (half a tile), both tile heights
+    double-buffered (halo_th 16 / 8) and the default single-buffered 8-row form
+    that runs two workgroups per CU (halo_th 0).  The halo kernel sums slice-major
     (the tile kernels tap-major), so the gate is bf16 output rounding: rel-L2
     <= 5e-3 between the kernels, <= 1e-2 against fp32."""
     Fn, T, _ = _mods()
