@@ -55,6 +55,8 @@ _FAMILIES = [
     (re.compile(r'conv_1x1_kernel<0,'), 'conv_fwd', True),
     (re.compile(r'conv_1x1_kernel<1,'), 'conv_bwd_data', True),
     (re.compile(r'conv_s2bwd_lds_kernel<'), 'conv_bwd_data', True),
+    (re.compile(r'conv_halo3_kernel<0,'), 'conv_fwd', True),
+    (re.compile(r'conv_halo3_kernel<1,'), 'conv_bwd_data', True),
     (re.compile(r'colsum_rows_kernel<.*WgradMap'), 'conv_bwd_weight', False),
 ]
 
