@@ -91,38 +91,57 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(const bf16_t* __restrict
   }
 }
 
-// stats[0..C) mean, [C..2C) inv_std, [2C..3C) 1 if d(inv_std)/d(var) != 0
-__global__ void bn_finalize_kernel(const double* __restrict__ sums, int C, double count, double sum_scale, float eps,
-                                   float mom, int clamp_mode, float* __restrict__ rmean, float* __restrict__ rvar,
-                                   float* __restrict__ stats) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// BN finalize parameters (the statistics of one BN call)
+struct FinArgs {
+  const double* sums;   // [2C] sum, sum of squares (after any cross-rank all-reduce)
+  double count, sum_scale;
+  float eps, mom;
+  int clamp_mode;
+  float* rmean;         // running statistics (null: not tracked)
+  float* rvar;
+  float* stats;         // out: [3C] mean, inv_std, d(inv_std)/d(var) != 0
+};
+
+// mean / inv_std / variance-gradient flag of channel c (bit-identical wherever it runs);
+// `commit` writes stats[] and updates the running statistics (once per channel per call)
+EE_DEV void bn_finalize_channel(const FinArgs& f, int C, int c, float& mean_o, float& istd_o, bool commit) {
   // sum_scale: replication factor of the statistics tensor (4 when x is read
   // through the nearest-2x upsample: every low-res element appears 4 times)
-  const double s1 = sums[c] * sum_scale, s2 = sums[C + c] * sum_scale;
-  const double mean = s1 / count;
+  const double s1 = f.sums[c] * f.sum_scale, s2 = f.sums[C + c] * f.sum_scale;
+  const double mean = s1 / f.count;
   double sumvar = s2 - s1 * mean;
   if (sumvar < 0) sumvar = 0;
-  const double var_b = sumvar / count;
+  const double var_b = sumvar / f.count;
   float istd, vg = 1.f;
-  if (clamp_mode) {  // batchnorm.py:125  clamp(var, eps) ** -0.5
-    if (var_b < eps) {
-      istd = (float)(1.0 / sqrt((double)eps));
+  if (f.clamp_mode) {  // batchnorm.py:125  clamp(var, eps) ** -0.5
+    if (var_b < f.eps) {
+      istd = (float)(1.0 / sqrt((double)f.eps));
       vg = 0.f;
     } else {
       istd = (float)(1.0 / sqrt(var_b));
     }
   } else {           // F.batch_norm: 1/sqrt(var + eps)
-    istd = (float)(1.0 / sqrt(var_b + (double)eps));
+    istd = (float)(1.0 / sqrt(var_b + (double)f.eps));
   }
-  stats[c] = (float)mean;
-  stats[C + c] = istd;
-  stats[2 * C + c] = vg;
-  if (rmean) {
-    const double unb = count > 1 ? sumvar / (count - 1) : sumvar;
-    rmean[c] = (float)((1.0 - mom) * rmean[c] + mom * mean);
-    rvar[c] = (float)((1.0 - mom) * rvar[c] + mom * unb);
+  mean_o = (float)mean;
+  istd_o = istd;
+  if (!commit) return;
+  f.stats[c] = (float)mean;
+  f.stats[C + c] = istd;
+  f.stats[2 * C + c] = vg;
+  if (f.rmean) {
+    const double unb = f.count > 1 ? sumvar / (f.count - 1) : sumvar;
+    f.rmean[c] = (float)((1.0 - f.mom) * f.rmean[c] + f.mom * mean);
+    f.rvar[c] = (float)((1.0 - f.mom) * f.rvar[c] + f.mom * unb);
   }
+}
+
+// stats[0..C) mean, [C..2C) inv_std, [2C..3C) 1 if d(inv_std)/d(var) != 0
+__global__ void bn_finalize_kernel(FinArgs f, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float m, i;
+  bn_finalize_channel(f, C, c, m, i, true);
 }
 
 // ---------------------------------------------------------------- apply --
@@ -148,12 +167,16 @@ struct ChanParams {
   float mean[8], istd[8], pm[8], pa[8];  // mode 0: w, b ; mode 1: gam[n], bet[n]
 };
 
-EE_DEV void load_params(const ModArgs& a, int n, int c0, ChanParams& q) {
+EE_DEV void load_params(const ModArgs& a, int n, int c0, ChanParams& q, const FinArgs* fin = nullptr) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = min(c0 + j, a.C - 1);
-    q.mean[j] = a.stats[c];
-    q.istd[j] = a.stats[a.C + c];
+    if (fin) {   // statistics straight from the sums (the forward's fused finalize)
+      bn_finalize_channel(*fin, a.C, c, q.mean[j], q.istd[j], false);
+    } else {
+      q.mean[j] = a.stats[c];
+      q.istd[j] = a.stats[a.C + c];
+    }
     if (a.mode == 0) {
       q.pm[j] = a.w ? a.w[c] : 1.f;
       q.pa[j] = a.b ? a.b[c] : 0.f;
@@ -199,7 +222,18 @@ EE_DEV void store8(bf16_t* dst, const float (&o)[8], int nvalid) {
 // (a single 16-byte load per iteration left these kernels latency-bound).
 constexpr int FUNR = 4;
 
-__global__ __launch_bounds__(NT) void bnmod_fwd_kernel(ModArgs a, bf16_t* __restrict__ y, int ldy, int ppc) {
+// FIN: the statistics come from the sums (the finalize kernel folded in: every block
+// recomputes its channels' mean / inv_std, block (0, 0) also writes stats[] and the
+// running statistics -- one launch less per BN call on the generator's serial chain)
+template <bool FIN>
+__global__ __launch_bounds__(NT) void bnmod_fwd_kernel(ModArgs a, bf16_t* __restrict__ y, int ldy, int ppc,
+                                                       FinArgs fin) {
+  if (FIN && blockIdx.x == 0 && blockIdx.y == 0) {
+    for (int c = threadIdx.x; c < a.C; c += NT) {
+      float m, i;
+      bn_finalize_channel(fin, a.C, c, m, i, true);
+    }
+  }
   const int C8 = (a.C + 7) / 8, rows = NT / C8;
   const int row = threadIdx.x / C8, cg = threadIdx.x - row * C8;
   if (row >= rows) return;
@@ -208,7 +242,7 @@ __global__ __launch_bounds__(NT) void bnmod_fwd_kernel(ModArgs a, bf16_t* __rest
   const int HWo = Ho * Wo;  // per-sample pixel counts fit 32 bits
   const int q1 = min(HWo, ((int)blockIdx.x + 1) * ppc);
   ChanParams P;
-  load_params(a, n, c0, P);
+  load_params(a, n, c0, P, FIN ? &fin : nullptr);
   for (int qb = (int)blockIdx.x * ppc + row; qb < q1; qb += FUNR * rows) {
     uint4 xr[FUNR];
     float mr[FUNR];
@@ -560,8 +594,8 @@ int eegan_bn_stats(const uint16_t* x, long P, int C, int ld, float* ws, double* 
 
 int eegan_bn_finalize(const double* sums, int C, double count, double sum_scale, float eps, float momentum,
                       int clamp_mode, float* running_mean, float* running_var, float* stats, hipStream_t stream) {
-  bn_finalize_kernel<<<ee_cdiv(C, 256), 256, 0, stream>>>(sums, C, count, sum_scale, eps, momentum, clamp_mode,
-                                                           running_mean, running_var, stats);
+  const FinArgs f{sums, count, sum_scale, eps, momentum, clamp_mode, running_mean, running_var, stats};
+  bn_finalize_kernel<<<ee_cdiv(C, 256), 256, 0, stream>>>(f, C);
   return ee_check_launch("bn_finalize");
 }
 
@@ -570,8 +604,25 @@ int eegan_bnmod_fwd(const eegan_bnmod_desc* d, uint16_t* y, int ldy, hipStream_t
   if (!vec_ok(d, ldy, y, "bnmod_fwd")) return -22;
   int ppc;
   const int chunks = pix_chunks(d->N, (long)(d->H << d->up2) * (d->W << d->up2), d->C, ppc);
-  bnmod_fwd_kernel<<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc);
+  bnmod_fwd_kernel<false><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, FinArgs{});
   return ee_check_launch("bnmod_fwd");
+}
+
+int eegan_bnmod_fwd_fin(const eegan_bnmod_desc* d, const double* sums, double count, double sum_scale, float eps,
+                        float momentum, int clamp_mode, float* running_mean, float* running_var, uint16_t* y,
+                        int ldy, hipStream_t stream) {
+  ModArgs a = make_args(d);
+  if (!vec_ok(d, ldy, y, "bnmod_fwd_fin")) return -22;
+  if (!d->stats) {
+    ee_set_error("bnmod_fwd_fin: the descriptor's stats buffer (written here) is missing");
+    return -22;
+  }
+  int ppc;
+  const int chunks = pix_chunks(d->N, (long)(d->H << d->up2) * (d->W << d->up2), d->C, ppc);
+  const FinArgs f{sums, count, sum_scale, eps, momentum, clamp_mode, running_mean, running_var,
+                  const_cast<float*>(d->stats)};
+  bnmod_fwd_kernel<true><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, f);
+  return ee_check_launch("bnmod_fwd_fin");
 }
 
 long eegan_bnmod_bwd_workspace(const eegan_bnmod_desc* d) {

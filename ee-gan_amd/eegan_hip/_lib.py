@@ -74,6 +74,7 @@ _SIGS = {
     'eegan_bn_stats': ([P, L, I, I, P, P, P], I),
     'eegan_bn_finalize': ([P, I, D, D, F, F, I, P, P, P, P], I),
     'eegan_bnmod_fwd': ([BD, P, I, P], I),
+    'eegan_bnmod_fwd_fin': ([BD, P, D, D, F, F, I, P, P, P, I, P], I),
     'eegan_bnmod_bwd_workspace': ([BD], L),
     'eegan_bnmod_bwd': ([BD, P, I, P, P, P, P, P, P], I),
     'eegan_bnmod_bwd_dx': ([BD, P, I, P, D, P, I, P], I),
@@ -163,7 +164,7 @@ def _load():
 
 LIB = _load()
 ABI_VERSION = LIB.eegan_abi_version()
-EXPECTED_ABI = 10
+EXPECTED_ABI = 11
 if ABI_VERSION != EXPECTED_ABI:
     raise ImportError('%s has ABI %d, these bindings need %d: rebuild (make -C ee-gan_amd/csrc)'
                       % (LIB_PATH, ABI_VERSION, EXPECTED_ABI))

@@ -27,14 +27,15 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 10  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
+#define EEGAN_ABI_VERSION 11  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
                                 4: rectangular (local x global) DAMSM words / sentence blocks on MFMA;
                                 5: GlobalAttentionGeneral (eegan_gag_*), words backward reuses the forward's prep;
                                 6: device input pipeline (eegan_pipe_*);
                                 7: GlobalAttentionGeneral for any source length (eegan_gag_fwd workspace);
                                 8: FID leg (eegan_fid_*);
                                 9: SyncBN peer-write all-reduce (eegan_peer_*);
-                                10: FID generator-sample input (eegan_fid_samples) */
+                                10: FID generator-sample input (eegan_fid_samples);
+                                11: BN forward with the finalize folded in (eegan_bnmod_fwd_fin) */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
@@ -143,6 +144,12 @@ typedef struct eegan_bnmod_desc {
 } eegan_bnmod_desc;
 
 int eegan_bnmod_fwd(const eegan_bnmod_desc* d, uint16_t* y, int ldy, hipStream_t stream);
+/* eegan_bn_finalize + eegan_bnmod_fwd in one launch (replaces the pair at sync_batchnorm/batchnorm.py:
+ * 48-78 + models.py:69-86): the statistics are computed from sums[2C] (same arguments as
+ * eegan_bn_finalize) and written to d->stats (with the running statistics) for the backward */
+int eegan_bnmod_fwd_fin(const eegan_bnmod_desc* d, const double* sums, double count, double sum_scale, float eps,
+                        float momentum, int clamp_mode, float* running_mean, float* running_var, uint16_t* y,
+                        int ldy, hipStream_t stream);
 long eegan_bnmod_bwd_workspace(const eegan_bnmod_desc* d);
 /* pass 1: dparam0/1 = (dw, db) [C] (mode 0) or (dgam, dbet) [N][C] (mode 1); dmask [N][Ho*Wo];
  * chan[2C] (fp64) = (sum dxhat, sum dxhat*xhat) -- all-reduce these across ranks for SyncBN */
