@@ -1153,7 +1153,7 @@ EE_DEV int halo_swz(int hx) { return (hx >> 1) & 2; }
 // rag_mask).  Output rows Mrows % 8 != 0: the straddling chunk's valid channels are
 // stored one by one, nothing past Mrows is written.
 template <int MODE, int TH, int WPX, bool RAG = false, int NBUF = 2>
-__global__ __launch_bounds__(64 * WPX, NBUF == 1 ? 2 : 1) void conv_halo3_kernel(ConvArgs a, long src_bytes,
+__global__ __launch_bounds__(64 * WPX, NBUF == 1 ? (TH == 4 ? 3 : 2) : 1) void conv_halo3_kernel(ConvArgs a, long src_bytes,
                                                                                long w_bytes) {
   constexpr int NT = 64 * WPX, TW = HALO_TW, TCO = HALO_TCO, FI = TCO / 16;
   constexpr int WROWS = TH / WPX, CB = TW / 16, FJ = WROWS * CB;
@@ -2854,21 +2854,26 @@ int try_halo3(const ConvArgs& a, hipStream_t s, long src_bytes, long w_bytes) {
   const bool th16 = big == 16 || (big != 8 && tiles16 >= 256);
   if (th16 && !tiles16) return 0;
   const dim3 grid16((unsigned)(tiles16 / co_t), co_t), grid8((unsigned)((long)a.N * (a.OH / 8) * (a.OW / HALO_TW)), co_t);
+  // default: three single-buffered 4-row workgroups per CU (52 KB of LDS each): one's slice
+  // loads, first-slice wait and epilogue run under the others' MFMAs, and other lanes' kernels
+  // still fit beside them.  Per kernel it wins on small-spatial / few-slice layers (3x3 256-ch
+  // 32^2 28.5 -> 24.8 us, D256 b0 60.7 -> 58.0) and loses on others (128-ch 64^2 24.4 -> 29.0);
+  // on the replayed step +0.8 / +0.9 % against two 8-row workgroups per CU (halo_nb=1), which
+  // was +0.4 / +0.6 % against the double-buffered one-workgroup-per-CU forms (halo_nb=2)
+  const int nb = knob("halo_nb", 3);
+  const dim3 grid4((unsigned)((long)a.N * (a.OH / 4) * (a.OW / HALO_TW)), co_t);
   if constexpr (MODE == MODE_BWDD) {
     if (a.Cvalid & 7) {
-      if (th16) ee_launch(conv_halo3_kernel<MODE, 16, 8, true>, grid16, dim3(512), 0, s, a, src_bytes, w_bytes);
-      else ee_launch(conv_halo3_kernel<MODE, 8, 4, true>, grid8, dim3(256), 0, s, a, src_bytes, w_bytes);
+      if (big == 16) ee_launch(conv_halo3_kernel<MODE, 16, 8, true>, grid16, dim3(512), 0, s, a, src_bytes, w_bytes);
+      else if (big == 8) ee_launch(conv_halo3_kernel<MODE, 8, 4, true>, grid8, dim3(256), 0, s, a, src_bytes, w_bytes);
+      else ee_launch(conv_halo3_kernel<MODE, 4, 4, true, 1>, grid4, dim3(256), 0, s, a, src_bytes, w_bytes);
       const int rc = ee_check_launch("conv_bwd_data(halo3)");
       return rc ? rc : 1;
     }
   }
-  // default: two single-buffered 8-row workgroups per CU (one's slice loads, first-slice wait and
-  // epilogue run under the other's MFMAs; 64 KB of LDS each, so other lanes' kernels still fit
-  // beside them).  Per kernel it wins on 2-slice layers (D256 b0 66 -> 58 us) and loses on 8-slice
-  // ones (25.7 -> 28.7 us); on the replayed step +0.4 / +0.6 % against halo_nb=2 (the double-
-  // buffered one-workgroup-per-CU forms) and +0.4 % against choosing it for <= 2 slices only
-  const int nb = knob("halo_nb", 1);
-  if (!big && nb == 1)
+  if (!big && nb == 3)
+    ee_launch(conv_halo3_kernel<MODE, 4, 4, false, 1>, grid4, dim3(256), 0, s, a, src_bytes, w_bytes);
+  else if (!big && nb == 1)
     ee_launch(conv_halo3_kernel<MODE, 8, 4, false, 1>, grid8, dim3(256), 0, s, a, src_bytes, w_bytes);
   else if (th16) ee_launch(conv_halo3_kernel<MODE, 16, 8>, grid16, dim3(512), 0, s, a, src_bytes, w_bytes);
   else ee_launch(conv_halo3_kernel<MODE, 8, 4>, grid8, dim3(256), 0, s, a, src_bytes, w_bytes);

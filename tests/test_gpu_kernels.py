@@ -916,8 +916,8 @@ def test_conv_halo3_matches_tile_kernel(gpu, monkeypatch, th):
     upsample, backward-data plain / gated / with the half-resolution residual;
     ragged input channels (40 -> a masked chunk), two output-channel tiles with a
     partial second one (96), 32 output channels (half a tile), both tile heights
-    double-buffered (halo_th 16 / 8) and the default single-buffered 8-row form
-    that runs two workgroups per CU (halo_th 0).  The halo kernel sums slice-major
+    double-buffered (halo_th 16 / 8) and the default single-buffered 4-row form
+    that runs three workgroups per CU (halo_th 0).  The halo kernel sums slice-major
     (the tile kernels tap-major), so the gate is bf16 output rounding: rel-L2
     <= 5e-3 between the kernels, <= 1e-2 against fp32."""
     Fn, T, _ = _mods()
