@@ -1348,6 +1348,111 @@ __global__ __launch_bounds__(64 * WPX, NBUF == 1 ? (TH == 4 ? 3 : 2) : 1) void c
 
 
 
+// ----------------------------- 4x4 / stride-2 forward convs on 32 channels --
+// FWD of the first resD block's 4x4 / stride-2 / pad-1 conv of every D (32 -> 64
+// channels, models.py:267; D256 at 256^2, N = 32: the largest conv of the D256
+// lane).  The tile kernels gather every input pixel once per overlapping 4x4
+// window (16 taps through L2, 64-B pieces).  Here a persistent workgroup keeps
+// its wave's 16 output channels x 16 taps of weights in VGPRs (one A fragment
+// per tap, loaded once) and walks 2 x 32-pixel output tiles, staging each
+// tile's 6 x 66-pixel input halo ONCE in LDS by LDS-DMA (out-of-image pixels
+// read zeros through the buffer bounds check).  Stride-2 taps read every other
+// halo column, so each halo row is stored as its even- then its odd-column
+// plane (33 pixels each): a tap's 16 consecutive output pixels are 16
+// consecutive plane pixels, chunk-swizzled q ^ ((idx >> 1) & 2) -> conflict-free
+// ds_read_b128 (brute-forced over all rows, planes and tap shifts).  Single
+// halo buffer (28 KB); two workgroups per CU hide each other's loads.  K
+// order = the tile kernels' (tap-major, one 32-channel step per tap): the same
+// MFMA sequence per output, bit-identical results.  Epilogue through LDS
+// (fp32 tile, 16-B runs of 8 channels): bias and activation.
+constexpr int S2F_TH = 2, S2F_TW = 32;
+
+EE_DEV int s2f_swz(int idx) { return (idx >> 1) & 2; }
+
+__global__ __launch_bounds__(256, 2) void conv_s2fwd_kernel(ConvArgs a, long src_bytes) {
+  constexpr int NT = 256, TH = S2F_TH, TW = S2F_TW, HC = 2 * TW + 2, PL = TW + 1, HR = 2 * TH + 2;
+  constexpr int HP = HR * HC, HOPS = (HP * 4 + NT - 1) / NT, HBUF = HOPS * NT * 16;
+  constexpr int TPIX = TH * TW, FJ = TPIX / 16, NCK = 16, NIT = TPIX * 8 / NT;
+  static_assert(TPIX * 64 * 4 <= HBUF && NIT * NT == TPIX * 8, "s2fwd tile");
+  __shared__ __attribute__((aligned(16))) char lds[HBUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, fr = lane & 15, fq = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_x = a.OW / TW, tiles_y = a.OH / TH, ntiles = a.N * tiles_y * tiles_x;
+  const int lds0 = (int)(uintptr_t)(lds_void_t*)lds;
+  const rsrc_t rs_src = make_rsrc(a.src, src_bytes);
+
+  // this wave's weights: rows 16 w + fr, tap t's 32 channels, chunk fq (rows past Mrows are zero in the pack)
+  bf16x8_t wa[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t)
+    wa[t] = as_frag(*reinterpret_cast<const uint4*>(a.wp + (long)(16 * w + fr) * a.Kw + t * BK + fq * 8));
+  // this thread's halo pieces: slot L >> 2 = (row hy, plane p, index idx) <-> column 2 idx + p
+  int hpk[HOPS];
+#pragma unroll
+  for (int i = 0; i < HOPS; ++i) {
+    const int L = i * NT + tid, slot = L >> 2;
+    const int hy = slot / HC, rem = slot - hy * HC, pl = rem >= PL, idx = rem - pl * PL;
+    const int q = (L & 3) ^ s2f_swz(idx);
+    hpk[i] = slot < HP ? (hy << 16) | ((2 * idx + pl) << 4) | q : -1;
+  }
+  const int PH = a.IH, PW = a.IW;
+  const int fbase[2] = {(fr << 6) + ((fq ^ s2f_swz(fr)) << 4), ((fr + 1) << 6) + ((fq ^ s2f_swz(fr + 1)) << 4)};
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    int b = t;
+    const int tx = b % tiles_x;
+    b /= tiles_x;
+    const int ty = b % tiles_y, n = b / tiles_y;
+    const int oy0 = ty * TH, ox0 = tx * TW;
+#pragma unroll
+    for (int i = 0; i < HOPS; ++i) {
+      const int hy = hpk[i] >> 16, hx = (hpk[i] >> 4) & 0xfff, q = hpk[i] & 15;
+      const int iy = 2 * oy0 - 1 + hy, ix = 2 * ox0 - 1 + hx;
+      const bool ok = hpk[i] >= 0 && (unsigned)iy < (unsigned)PH && (unsigned)ix < (unsigned)PW;
+      const unsigned off = ok ? (unsigned)((((n * PH + iy) * PW + ix) * a.lds_src + q * 8) * 2) : OOB;
+      lds_dma16s(rs_src, lds0 + (i * NT + (tid & ~63)) * 16, off, 0);
+    }
+    wait_vmcnt_barrier<0>();
+    f32x4_t acc[FJ];
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 16; ++tap) {
+      const int r = tap >> 2, sx = tap & 3;
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) {
+        // plane index fr + (sx >> 1) + 16 jc: its swizzle is jc-independent, so every read is one of
+        // two base registers + an immediate
+        const int jr = j / (TW / 16), jc = j % (TW / 16);
+        const int imm = ((2 * jr + r) * HC + (sx & 1) * PL + jc * 16) * 64;
+        const bf16x8_t fb = as_frag(*reinterpret_cast<const uint4*>(lds + fbase[sx >> 1] + imm));
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[tap], fb, acc[j], 0, 0, 0);
+      }
+    }
+    __syncthreads();   // every wave is done with the halo: the fp32 tile goes through the same LDS
+    float4* st = reinterpret_cast<float4*>(lds);
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const int p = (j / (TW / 16)) * TW + (j % (TW / 16)) * 16 + fr, c = w * 4 + fq;
+      st[p * NCK + (c ^ (p & 15))] = make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int item = k * NT + tid, p = item / 8, e = item % 8, co = 8 * e;
+      const float4 lo = st[p * NCK + ((2 * e) ^ (p & 15))];
+      const float4 hi = st[p * NCK + ((2 * e + 1) ^ (p & 15))];
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = act_fwd(v[r] + (a.bias ? a.bias[co + r] : 0.f), a.act, a.slope);
+      const long gp = ((long)n * a.OH + oy0 + p / TW) * a.OW + ox0 + p % TW;
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + gp * a.ldo + co) =
+          make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+    }
+    __syncthreads();   // the staged tile is read before the next halo lands on it
+  }
+}
+
 // ---------------------------------------------------------- WGRAD kernel --
 struct WgradArgs {
   const bf16_t* x;     // [N][IH>>up2][IW>>up2][ldx]
@@ -2833,6 +2938,25 @@ int try_thin(const ConvArgs& a, hipStream_t s, long src_bytes) {
   return rc ? rc : 1;
 }
 
+// 4x4 / stride-2 / pad-1 forward convs, 32 -> 64 channels, bias / activation only, on
+// whole 2 x 32 output tiles take conv_s2fwd_kernel (0: not eligible, else the launch rc)
+int try_s2fwd(const ConvArgs& a, hipStream_t s, long src_bytes) {
+  if (!knob("s2f", 1) || src_bytes >= 0x7fffffffL) return 0;
+  if (a.R != 4 || a.S != 4 || a.st != 2 || a.ph != 1 || a.pw != 1 || a.ncls != 1 || a.nsplit != 1 || a.up2) return 0;
+  if (a.Cgp != BK || a.Cvalid != BK || a.Mrows != 64 || a.Kw != 16 * BK) return 0;
+  if (a.res || a.gate || a.out_f32 || (a.ldo & 7) || ((uintptr_t)a.out & 15)) return 0;
+  if ((a.lds_src & 7) || ((uintptr_t)a.src & 15)) return 0;
+  if (a.OW % S2F_TW || a.OH % S2F_TH || a.IH != 2 * a.OH || a.IW != 2 * a.OW) return 0;
+  const long tiles = (long)a.N * (a.OH / S2F_TH) * (a.OW / S2F_TW);
+  if (tiles >= 0x7fffffffL) return 0;
+  // persistent: two workgroups per CU (VGPR-bound: 64 of a wave's registers hold its weights,
+  // loaded once per workgroup)
+  const unsigned grid = (unsigned)std::min<long>(tiles, 2 * 256);
+  ee_launch(conv_s2fwd_kernel, dim3(grid), dim3(256), 0, s, a, src_bytes);
+  const int rc = ee_check_launch("conv_fwd(s2-halo)");
+  return rc ? rc : 1;
+}
+
 // 3x3 / stride-1 / pad-1 convs with >= 32 output rows on grids of whole 8 x 32
 // tiles take conv_halo3_kernel (0: not eligible, else the launch rc)
 template <int MODE>
@@ -2963,6 +3087,8 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   if (const int pw = try_1x1<MODE>(a, s, src_bytes)) return pw > 0 ? 0 : pw;
   if (MODE == MODE_BWDD)
     if (const int sb = try_s2bwd(a, s, src_bytes)) return sb > 0 ? 0 : sb;
+  if (MODE == MODE_FWD)
+    if (const int sf = try_s2fwd(a, s, src_bytes)) return sf > 0 ? 0 : sf;
   if (const int hl = try_halo3<MODE>(a, s, src_bytes, (long)ee_round_up(a.Mrows, 128) * a.Kw * 2))
     return hl > 0 ? 0 : hl;
   Plan p = plan_igemm(a, Pc_max);

@@ -991,3 +991,30 @@ def test_conv_halo3_ragged_channels(gpu, monkeypatch):
     assert rel_l2(outs['1'][0], yref) <= 1e-2
     dref = F.conv_transpose2d(dzs.to(torch.bfloat16).float(), wb, None, 1, 1)
     assert rel_l2(outs['1'][1], dref) <= 1e-2
+
+
+@pytest.mark.gpu
+def test_conv_s2fwd_matches_tile_kernel(gpu, monkeypatch):
+    """4x4 / stride-2 / pad-1 forward convs with 32 input and 64 output channels
+    on conv_s2fwd_kernel (resD conv_r[0] of each D's first block, models.py:267):
+    the same K order as the tile kernels, so bit-identical to them (EEGAN_CONV
+    s2f=0), and against torch's fp32 conv; a grid with more tiles than the
+    persistent workgroups (each walks several), bias + leaky ReLU."""
+    Fn, T, _ = _mods()
+    lrelu = Fn.ACT_CODES['lrelu']
+    for N, H, W in [(2, 32, 64), (16, 128, 128)]:
+        torch.manual_seed(N + H)
+        g = Fn.Geom(64, 4, 4, 2, 1, 1, 0)
+        xs = torch.randn(N, 32, H, W)
+        x = _nhwc(xs, gpu)
+        Wt = (torch.randn(64, 32, 4, 4) * (1.0 / (16 * 32) ** 0.5)).to(gpu)
+        b = torch.randn(64).to(gpu) * 0.1
+        outs = {}
+        for on in ('0', '1'):
+            conv_knob(monkeypatch, 's2f', on)
+            outs[on] = (Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu).float().cpu(),
+                        Fn.conv_fwd_raw(x, Wt, None, g).float().cpu())
+        for a, c in zip(outs['1'], outs['0']):
+            assert torch.equal(a, c), (N, H, W, float((a - c).abs().max()))
+        ref = F.conv2d(xs.to(torch.bfloat16).float(), Wt.cpu().to(torch.bfloat16).float(), None, 2, 1)
+        assert rel_l2(outs['1'][1], ref) <= 1e-2
