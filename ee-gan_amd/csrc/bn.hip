@@ -374,37 +374,24 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_reduce_kernel(ModArgs a, const b
       }
     }
   }
-  // reduce acc over rows -> ws
-  float* sacc = sh + rows * C8;  // [rows][4][C8*8]
-  const int W8 = C8 * 8;
-  int nrows = rows;
-  if (wave_red) {
-    // the rows of one wave first, by shuffles (lanes l, l^C8, l^2C8, ... share
-    // channels); then one partial row per wave goes through LDS
-    for (int off = C8; off < 64; off <<= 1)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] += __shfl_xor(acc[i][j], off);
-    nrows = NT / 64;
-    if ((t & 63) < C8) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sacc[((t >> 6) * 4 + i) * W8 + c0 + j] = acc[i][j];
-    }
-  } else if (row < rows) {
+  // reduce acc over rows -> ws: every row's partials through LDS (a row stride of
+  // 4 * W8 + 1 floats spreads a wave's rows over the banks), then one thread per
+  // output sums the rows in order.  (Reducing a wave's rows by shuffles first took
+  // 4 x 32 lane exchanges per thread at C = 32.)
+  float* sacc = sh + rows * C8;  // [rows][4 * W8 + 1]
+  const int W8 = C8 * 8, RS = 4 * W8 + 1;
+  if (row < rows) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sacc[(row * 4 + i) * W8 + c0 + j] = acc[i][j];
+      for (int j = 0; j < 8; ++j) sacc[row * RS + i * W8 + c0 + j] = acc[i][j];
   }
   __syncthreads();
   float* out = ws + ((long)n * gridDim.x + blockIdx.x) * 4 * C;
   for (int e = t; e < 4 * C; e += NT) {
     const int i = e / C, c = e - i * C;
     float s = 0.f;
-    for (int r = 0; r < nrows; ++r) s += sacc[(r * 4 + i) * W8 + c];
+    for (int r = 0; r < rows; ++r) s += sacc[r * RS + i * W8 + c];
     out[e] = s;
   }
 }
@@ -644,7 +631,7 @@ int eegan_bnmod_bwd(const eegan_bnmod_desc* d, const uint16_t* dt, int lddt, flo
     return -22;
   }
   const int rows = NT / C8;
-  const size_t shm = (rows * C8 + rows * 4 * C8 * 8) * sizeof(float);
+  const size_t shm = (rows * C8 + rows * (4 * C8 * 8 + 1)) * sizeof(float);
   dim3 grid(chunks, d->N);
   bnmod_bwd_reduce_kernel<<<grid, NT, shm, stream>>>(a, dt, lddt, ppc, ws, dmask);
   int rc = ee_check_launch("bnmod_bwd_reduce");

@@ -1,5 +1,6 @@
 #!/bin/bash
-# PMC counters of conv_halo3_kernel on one conv_bench shape (diagnostic), one pass per group
+# PMC counters of one kernel (KF, default conv_halo3_kernel) under CMD (default: conv_bench on
+# one shape), one pass per counter group (diagnostic)
 source ./run_gpu_steps.sh
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=${1:-hp}
@@ -10,16 +11,16 @@ i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
   step 120 ${TAG}_p$i timeout -s KILL 100 rocprofv3 --pmc $P --output-format csv -d gpurun_out/${TAG}_p$i -o run -- \
-    python3 tools/conv_bench.py --shapes $SH --dirs fwd --iters 5
+    ${CMD:-python3 tools/conv_bench.py --shapes $SH --dirs fwd --iters 5}
 done
-python3 - "$TAG" <<'PY'
+python3 - "$TAG" "${KF:-halo3}" <<'PY'
 import csv, glob, sys, collections
-tag = sys.argv[1]
+tag, kf = sys.argv[1], sys.argv[2]
 for i in (1, 2):
     acc = collections.defaultdict(list)
     for f in glob.glob('gpurun_out/%s_p%d/**/*counter_collection.csv' % (tag, i), recursive=True):
         for r in csv.DictReader(open(f)):
-            if 'halo3' in r['Kernel_Name']:
+            if kf in r['Kernel_Name']:
                 acc[(r['Dispatch_Id'], r['Counter_Name'])].append(float(r['Counter_Value']))
     per = collections.defaultdict(list)
     for (d, c), v in acc.items():
