@@ -139,15 +139,16 @@ __global__ __launch_bounds__(NT) void dot_partial_kernel(const bf16_t* x, int ld
   if (threadIdx.x == 0) ws[blockIdx.x] = acc;
 }
 
-// ScaleAdd backward in one pass over g: out = s * g (the residual-branch
-// gradient) and the per-block partials of <g, h> (the gain's gradient)
+// ScaleAdd backward in one pass over g: out = (r ? r : 0) + s * g (the
+// residual-branch gradient; r = a second gradient summed into it) and the
+// per-block partials of <g, h> (the gain's gradient)
 __global__ __launch_bounds__(NT) void scale_dot_partial_kernel(const bf16_t* g, int ldg, const bf16_t* h, int ldh,
                                                                const float* gamma, float alpha, long P, int C,
-                                                               bf16_t* out, int ldo, float* ws, int act,
-                                                               float slope) {
+                                                               const bf16_t* r, int ldr, bf16_t* out, int ldo,
+                                                               float* ws, int act, float slope) {
   __shared__ float red[16];
   const int C8 = (C + 7) / 8;
-  const bool vec = (ldg % 8 == 0) && (ldh % 8 == 0) && (ldo % 8 == 0);
+  const bool vec = (ldg % 8 == 0) && (ldh % 8 == 0) && (ldo % 8 == 0) && (!r || ldr % 8 == 0);
   const float s = alpha * (gamma ? *gamma : 1.f);
   float acc = 0.f;
   GRID_LOOP(e, P * C8) {
@@ -160,6 +161,11 @@ __global__ __launch_bounds__(NT) void scale_dot_partial_kernel(const bf16_t* g, 
     for (int j = 0; j < 8; ++j) {
       acc += a.v[j] * b.v[j];
       a.v[j] *= act ? s * act_dgrad_from_y(b.v[j], act, slope) : s;
+    }
+    if (r) {
+      V8 c = load8(r + p * ldr + c0, nv, vec);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a.v[j] += c.v[j];
     }
     store8(out + p * ldo + c0, a, nv, vec);
   }
@@ -622,7 +628,19 @@ int eegan_scale_dot(const uint16_t* g, int ldg, const uint16_t* h, int ldh, cons
                     int C, uint16_t* out, int ldo, float* ws, float* dot_out, int accumulate, int act, float slope,
                     hipStream_t s) {
   const int blocks = std::min(1024, grid_for(P * ((C + 7) / 8)));
-  scale_dot_partial_kernel<<<blocks, NT, 0, s>>>(g, ldg, h, ldh, gamma, alpha, P, C, out, ldo, ws, act, slope);
+  scale_dot_partial_kernel<<<blocks, NT, 0, s>>>(g, ldg, h, ldh, gamma, alpha, P, C, nullptr, 0, out, ldo, ws, act,
+                                                 slope);
+  int rc = ee_check_launch("scale_dot_partial");
+  if (rc) return rc;
+  dot_final_kernel<<<1, 1024, 0, s>>>(ws, blocks, 1.f, dot_out, accumulate);
+  return ee_check_launch("dot_final");
+}
+
+int eegan_scale_dot_res(const uint16_t* g, int ldg, const uint16_t* h, int ldh, const float* gamma, float alpha, long P,
+                        int C, const uint16_t* r, int ldr, uint16_t* out, int ldo, float* ws, float* dot_out,
+                        int accumulate, hipStream_t s) {
+  const int blocks = std::min(1024, grid_for(P * ((C + 7) / 8)));
+  scale_dot_partial_kernel<<<blocks, NT, 0, s>>>(g, ldg, h, ldh, gamma, alpha, P, C, r, ldr, out, ldo, ws, 0, 0.f);
   int rc = ee_check_launch("scale_dot_partial");
   if (rc) return rc;
   dot_final_kernel<<<1, 1024, 0, s>>>(ws, blocks, 1.f, dot_out, accumulate);

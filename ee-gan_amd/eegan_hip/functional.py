@@ -476,6 +476,8 @@ class PoolConvFn(torch.autograd.Function):
             if fused and gp is not None and dz is not None:
                 dx = conv_bwd_data_raw(dz, W, g, ctx.x_shape, ctx.cache, res=_as_bf16_grad(gp), res_up2=1,
                                        res_scale=0.25)
+            elif FUSE_GP_ADDS and gp is not None and dz is not None:
+                dx = PoolConvBwdDataFn.apply(dz, _as_bf16_grad(gp), W, g, ctx.x_shape, ctx.cache)
             else:
                 parts = []
                 if dz is not None:
@@ -496,6 +498,37 @@ class PoolConvFn(torch.autograd.Function):
             else:
                 db = ChanSumFn.apply(dz)
         return dx, dW, db, None, None, None, None, None
+
+
+# EEGAN_FUSE_GP_ADDS=0: the gradient penalty's create_graph backward sums resD's
+# two input gradients and ScaleAdd's two output gradients with separate passes
+FUSE_GP_ADDS = os.environ.get('EEGAN_FUSE_GP_ADDS', '1') != '0'
+
+
+class PoolConvBwdDataFn(torch.autograd.Function):
+    """PoolConvFn's dx under create_graph (the gradient penalty's first
+    backward): conv^T(dz) + avg_pool2d adjoint(gp) in one data-gradient launch
+    (the pooled branch's gradient added in the epilogue, as in the first-order
+    path), differentiable: its backward is ConvBwdDataFn's and AvgPool2AdjFn's."""
+
+    @staticmethod
+    def forward(ctx, dz, gp, W, g, x_shape, cache):
+        ctx.g, ctx.cache = g, cache
+        ctx.save_for_backward(dz, W)
+        return conv_bwd_data_raw(dz, W, g, x_shape, cache, res=gp, res_up2=1, res_scale=0.25)
+
+    @staticmethod
+    def backward(ctx, gdx):
+        dz, W = ctx.saved_tensors
+        gdx = _as_bf16_grad(gdx)
+        g_dz = g_gp = g_W = None
+        if ctx.needs_input_grad[0]:
+            g_dz = Conv2dFn.apply(gdx, W, None, ctx.g, 0, 0.0, False, ctx.cache)
+        if ctx.needs_input_grad[1]:
+            g_gp = AvgPool2Fn.apply(gdx)
+        if ctx.needs_input_grad[2] and _needed(ctx, 2) and not _sink_wgrad(ctx, 2, gdx, dz, ctx.g, W.shape):
+            g_W = ConvBwdWeightFn.apply(gdx, dz, ctx.g)
+        return g_dz, g_gp, g_W, None, None, None
 
 
 class ConvBwdDataFn(torch.autograd.Function):
@@ -728,9 +761,53 @@ class ScaleAddFn(torch.autograd.Function):
             if not _needed(ctx, 2):
                 d_g = None
             return d_res, d_h, d_g, None, None
-        d_h = ScaleFn.apply(g, gamma) if ctx.needs_input_grad[1] else None
-        d_g = DotFn.apply(g, h) if ctx.needs_input_grad[2] else None
+        if FUSE_GP_ADDS and d_res is not None and ctx.needs_input_grad[1]:
+            d_res, d_h = ScaleAddBwdFn.apply(g, gamma)
+        else:
+            d_h = ScaleFn.apply(g, gamma) if ctx.needs_input_grad[1] else None
+        d_g = DotFn.apply(g, h) if _needed(ctx, 2) else None
         return d_res, d_h, d_g, None, None
+
+
+class ScaleAddBwdFn(torch.autograd.Function):
+    """(g, gamma * g): ScaleAddFn's gradients of (res, h) under create_graph as
+    ONE node, so the double backward sums the two paths' gradients, scales one
+    and takes gamma's <gg_h, g> in a single pass (eegan_scale_dot_res) instead
+    of ScaleFn's backward, DotFn and autograd's add.  The first output is g
+    itself (autograd returns it as a view attached to this node)."""
+
+    @staticmethod
+    def forward(ctx, g, gamma):
+        ctx.save_for_backward(g, gamma)
+        return g, _scale_raw(g, gamma)
+
+    @staticmethod
+    def backward(ctx, gg_res, gg_h):
+        g, gamma = ctx.saved_tensors
+        if gg_h is None:
+            return gg_res, None
+        gg_h = _as_bf16_grad(gg_h)
+        if gg_res is not None:
+            gg_res = _as_bf16_grad(gg_res)
+        need_gamma = _needed(ctx, 1)
+        if torch.is_grad_enabled():   # a third-order pass: composed of differentiable Functions
+            out = ScaleFn.apply(gg_h, gamma)
+            if gg_res is not None:
+                out = out + gg_res
+            return out, (DotFn.apply(gg_h, g) if need_gamma else None)
+        N, C, H, W = gg_h.shape
+        out = empty_nhwc(N, C, H, W, gg_h.device)
+        if not need_gamma:
+            ops.scale_add(ptr(gg_res), ld_of(gg_res) if gg_res is not None else 0, gg_h.data_ptr(), ld_of(gg_h),
+                          gamma.data_ptr(), 1.0, N * H * W, C, out.data_ptr(), ld_of(out), stream())
+            return out, None
+        sink = _grad_sink(ctx, 1)
+        d_g = torch.empty(1, dtype=F32, device=g.device) if sink is None else None
+        ws = workspace(ops.dot_workspace(), g.device)
+        ops.scale_dot_res(gg_h.data_ptr(), ld_of(gg_h), g.data_ptr(), ld_of(g), gamma.data_ptr(), 1.0, N * H * W, C,
+                          ptr(gg_res), ld_of(gg_res) if gg_res is not None else 0, out.data_ptr(), ld_of(out),
+                          ws.data_ptr(), (sink if d_g is None else d_g).data_ptr(), int(d_g is None), stream())
+        return out, d_g
 
 
 class ScaleFn(torch.autograd.Function):

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 11  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
+#define EEGAN_ABI_VERSION 12  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
                                 4: rectangular (local x global) DAMSM words / sentence blocks on MFMA;
                                 5: GlobalAttentionGeneral (eegan_gag_*), words backward reuses the forward's prep;
                                 6: device input pipeline (eegan_pipe_*);
@@ -35,7 +35,8 @@ extern "C" {
                                 8: FID leg (eegan_fid_*);
                                 9: SyncBN peer-write all-reduce (eegan_peer_*);
                                 10: FID generator-sample input (eegan_fid_samples);
-                                11: BN forward with the finalize folded in (eegan_bnmod_fwd_fin) */
+                                11: BN forward with the finalize folded in (eegan_bnmod_fwd_fin);
+                                12: ScaleAdd double backward in one pass (eegan_scale_dot_res) */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
@@ -180,6 +181,12 @@ int eegan_cat_channels(const uint16_t* const* parts, const int* lds, const int* 
 int eegan_scale_dot(const uint16_t* g, int ldg, const uint16_t* h, int ldh, const float* gamma, float alpha, long P,
                     int C, uint16_t* out, int ldo, float* ws, float* dot_out, int accumulate, int act, float slope,
                     hipStream_t stream);
+/* The gradient penalty's double backward through ScaleAdd (models.py:278 under create_graph): out = r +
+ * alpha*gamma*g (the two gradients of the first backward's (g, gamma*g) summed) and dot_out (+)= <g, h>
+ * (gamma's gradient, h = the first backward's g), one pass; ws = eegan_dot_workspace() bytes */
+int eegan_scale_dot_res(const uint16_t* g, int ldg, const uint16_t* h, int ldh, const float* gamma, float alpha, long P,
+                        int C, const uint16_t* r, int ldr, uint16_t* out, int ldo, float* ws, float* dot_out,
+                        int accumulate, hipStream_t stream);
 long eegan_dot_workspace(void);
 int eegan_dot(const uint16_t* x, int ldx, const uint16_t* y, int ldy, long P, int C, float scale, float* ws,
               float* out, int accumulate, hipStream_t s);

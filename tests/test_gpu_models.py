@@ -443,6 +443,38 @@ def test_fused_activation_backward_matches_separate(gpu, monkeypatch):
         assert rel_l2(gp1[n], gp0[n]) < 2e-2, n
 
 
+def test_gradient_penalty_fused_adds_match_separate(gpu, monkeypatch):
+    """The gradient penalty's create_graph backward with resD's two input
+    gradients summed in the conv epilogue (PoolConvBwdDataFn) and ScaleAdd's
+    double backward in one pass (ScaleAddBwdFn) against the separate passes
+    plus autograd adds (EEGAN_FUSE_GP_ADDS=0): the same sums, rounded to bf16
+    once instead of twice, so gradients agree to bf16 rounding."""
+    import models
+    from eegan_hip import functional as Fn
+    from eegan_hip.trainer import Trainer
+    from sync_batchnorm import DataParallelWithCallback
+    from _util import rel_l2
+    D = _load(models.Dis256(8, True, 10), 'dis256', 30 + 256, gpu)
+    with torch.no_grad():
+        for i, b in enumerate((D.block0, D.block1, D.block2, D.block3, D.block4, D.block5)):
+            b.gamma.fill_(0.25 + 0.1 * i)    # non-zero gains: both ScaleAdd paths carry gradient
+    netD = DataParallelWithCallback(D)
+    x = seeded_tensor('gpf:x', (2, 3, 256, 256), 1, 'uniform').to(gpu)
+    s = seeded_tensor('gpf:s', (2, 256), 1).to(gpu)
+    res = []
+    for fuse in (False, True):
+        monkeypatch.setattr(Fn, 'FUSE_GP_ADDS', fuse)
+        D.zero_grad(set_to_none=True)
+        gp = Trainer.MA_gradient_penalty(Fn.ImageToNhwcFn.apply(x), s, netD, True)
+        gp.backward()
+        res.append((gp.detach().cpu(), {n: p.grad.cpu() for n, p in D.named_parameters() if p.grad is not None}))
+    (v0, g0), (v1, g1) = res
+    assert torch.allclose(v0, v1, rtol=2e-2)
+    assert set(g0) == set(g1) and any('gamma' in n for n in g0)
+    for n in g0:
+        assert rel_l2(g1[n], g0[n]) < 3e-2, n
+
+
 def test_inception_stacked_1x1_matches_separate(gpu, monkeypatch):
     """Inception blocks' shared-input 1x1 branches as one stacked conv
     (DAMSM._Stacked1x1) vs separate convs: identical forward (same K order per

@@ -9,6 +9,7 @@ switched this way).  The order of the settings rotates every repetition (the
 clock drifts over a run: a fixed order biases the comparison).
 
     python tools/ab_inproc.py "EEGAN_CONV=mink=32" ["EEGAN_CONV=mink=8" ...] [--reps 3] [--steps 20]
+    python tools/ab_inproc.py "py:eegan_hip.functional.FUSE_GP_ADDS=False"   (a module constant)
 """
 import argparse
 import gc
@@ -21,6 +22,12 @@ sys.path.insert(0, os.path.join(REPO, 'ee-gan_amd'))
 sys.path.insert(0, REPO)
 
 import torch  # noqa: E402
+
+
+def _py_attr(path):
+    import importlib
+    modname, attr = path.rsplit('.', 1)
+    return importlib.import_module(modname), attr
 
 
 def main():
@@ -40,14 +47,26 @@ def main():
     settings = ['base'] + args.settings
     res = {s: [] for s in settings}
     base_env = dict(os.environ)
+    py_base = []
+    for s in args.settings:
+        for kv in s.split():
+            if kv.startswith('py:'):
+                mod, attr = _py_attr(kv.split('=', 1)[0][3:])
+                py_base.append((mod, attr, getattr(mod, attr)))
     for rep in range(args.reps):
         for s in settings[rep % len(settings):] + settings[:rep % len(settings)]:
             os.environ.clear()
             os.environ.update(base_env)
+            for mod, attr, v in py_base:
+                setattr(mod, attr, v)
             if s != 'base':
                 for kv in s.split():
                     k, v = kv.split('=', 1)
-                    os.environ[k] = v
+                    if k.startswith('py:'):   # py:package.module.ATTR=value (module constants)
+                        mod, attr = _py_attr(k[3:])
+                        setattr(mod, attr, eval(v))
+                    else:
+                        os.environ[k] = v
             sg = StepGraph(T, batch, warmup=1)
             sg.replay()
             torch.cuda.synchronize()
