@@ -388,6 +388,18 @@ def _as_bf16_grad(g):
 
 # EEGAN_FUSE_ACT_BWD=0: every activation backward runs as its own pass (A/B switch).
 FUSE_ACT_BWD = os.environ.get('EEGAN_FUSE_ACT_BWD', '1') != '0'
+# EEGAN_FUSE_GP_ACT=0: under create_graph (the gradient penalty's first backward)
+# every activation backward runs as its own ActBwdFn pass.
+FUSE_GP_ACT = os.environ.get('EEGAN_FUSE_GP_ACT', '1') != '0'
+
+
+def _act_deferred(ctx, fused, cg):
+    """Whether this layer's activation backward runs in its consumers instead.
+    defer_act=True: every consumer is a conv with in_act (gates in the first-
+    order backward and, through GatedConvBwdDataFn, under create_graph);
+    defer_act='first_order': the consumer gates only in the first-order
+    backward (resD's ScaleAddFn h_act)."""
+    return bool(ctx.defer_act) and (fused or (cg and ctx.defer_act is True))
 
 
 class Conv2dFn(torch.autograd.Function):
@@ -420,7 +432,8 @@ class Conv2dFn(torch.autograd.Function):
         g = ctx.g
         gy = _as_bf16_grad(gy)
         fused = FUSE_ACT_BWD and not torch.is_grad_enabled()
-        dz = ActBwdFn.apply(gy, y, ctx.act, ctx.slope) if ctx.act and not (fused and ctx.defer_act) else gy
+        cg = FUSE_ACT_BWD and FUSE_GP_ACT and torch.is_grad_enabled()
+        dz = ActBwdFn.apply(gy, y, ctx.act, ctx.slope) if ctx.act and not _act_deferred(ctx, fused, cg) else gy
         dx = dW = db = None
         if _needed(ctx, 0):
             if g.up2:
@@ -428,6 +441,8 @@ class Conv2dFn(torch.autograd.Function):
             elif fused and ctx.in_act:
                 dx = conv_bwd_data_raw(dz, W, g, ctx.x_shape, ctx.cache, gate=x, gate_act=ctx.in_act,
                                        gate_slope=ctx.in_slope)
+            elif cg and ctx.in_act:
+                dx = GatedConvBwdDataFn.apply(dz, W, x, g, ctx.x_shape, ctx.cache, ctx.in_act, ctx.in_slope)
             else:
                 dx = ConvBwdDataFn.apply(dz, W, g, ctx.x_shape, ctx.cache)
         if _needed(ctx, 1) and not _sink_wgrad(ctx, 1, x, dz, g, W.shape):
@@ -467,11 +482,12 @@ class PoolConvFn(torch.autograd.Function):
         x, W, y = ctx.saved_tensors
         g = ctx.g
         fused = FUSE_ACT_BWD and not torch.is_grad_enabled()
+        cg = FUSE_ACT_BWD and FUSE_GP_ACT and torch.is_grad_enabled()
         dx = dW = db = None
         dz = None
         if gy is not None:
             gy = _as_bf16_grad(gy)
-            dz = ActBwdFn.apply(gy, y, ctx.act, ctx.slope) if ctx.act and not (fused and ctx.defer_act) else gy
+            dz = ActBwdFn.apply(gy, y, ctx.act, ctx.slope) if ctx.act and not _act_deferred(ctx, fused, cg) else gy
         if _needed(ctx, 0):
             if fused and gp is not None and dz is not None:
                 dx = conv_bwd_data_raw(dz, W, g, ctx.x_shape, ctx.cache, res=_as_bf16_grad(gp), res_up2=1,
@@ -529,6 +545,31 @@ class PoolConvBwdDataFn(torch.autograd.Function):
         if ctx.needs_input_grad[2] and _needed(ctx, 2) and not _sink_wgrad(ctx, 2, gdx, dz, ctx.g, W.shape):
             g_W = ConvBwdWeightFn.apply(gdx, dz, ctx.g)
         return g_dz, g_gp, g_W, None, None, None
+
+
+class GatedConvBwdDataFn(torch.autograd.Function):
+    """Conv2dFn's dx under create_graph when its input x = act(z) came from a
+    layer with defer_act=True: conv^T(dz) * act'(x) in one data-gradient launch
+    (the producer's ActBwdFn folded in, as in the first-order path).  act' is
+    piecewise constant, so x gets no gradient; the double backward masks the
+    incoming gradient once and runs ConvBwdDataFn's adjoints on it."""
+
+    @staticmethod
+    def forward(ctx, dz, W, x, g, x_shape, cache, act, slope):
+        ctx.g, ctx.cache, ctx.act, ctx.slope = g, cache, act, slope
+        ctx.save_for_backward(dz, W, x)
+        return conv_bwd_data_raw(dz, W, g, x_shape, cache, gate=x, gate_act=act, gate_slope=slope)
+
+    @staticmethod
+    def backward(ctx, gdx):
+        dz, W, x = ctx.saved_tensors
+        gm = ActBwdFn.apply(_as_bf16_grad(gdx), x, ctx.act, ctx.slope)
+        g_dz = g_W = None
+        if ctx.needs_input_grad[0]:
+            g_dz = Conv2dFn.apply(gm, W, None, ctx.g, 0, 0.0, False, ctx.cache)
+        if ctx.needs_input_grad[1] and _needed(ctx, 1) and not _sink_wgrad(ctx, 1, gm, dz, ctx.g, W.shape):
+            g_W = ConvBwdWeightFn.apply(gm, dz, ctx.g)
+        return g_dz, g_W, None, None, None, None, None, None
 
 
 class ConvBwdDataFn(torch.autograd.Function):

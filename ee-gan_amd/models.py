@@ -284,14 +284,15 @@ class resD(nn.Module):
         self.gamma = nn.Parameter(torch.zeros(1))
 
     def forward(self, x):
-        # residual()'s last LeakyReLU is deferred to ScaleAddFn's backward
+        # residual()'s last LeakyReLU is deferred to ScaleAddFn's backward (first-order
+        # only: under create_graph ScaleAddFn does not gate, so conv_r[2] keeps its ActBwdFn)
         lrelu = Fn.ACT_CODES['lrelu']
         if self.downsample and Fn.FUSE_ACT_BWD:
             # the shortcut's pooling and conv_r[0] read x together (Fn.PoolConvFn: one dx)
             c0 = self.conv_r[0]
             xp, h = Fn.PoolConvFn.apply(x, c0.weight, c0.bias, c0.geom(False), lrelu, 0.2, c0._cache, True)
             sc = self.conv_s(xp) if self.learned_shortcut else xp
-            r = self.conv_r[2](h, act='lrelu', slope=0.2, in_act='lrelu', defer_act=True)
+            r = self.conv_r[2](h, act='lrelu', slope=0.2, in_act='lrelu', defer_act='first_order')
             return Fn.ScaleAddFn.apply(sc, r, self.gamma, lrelu, 0.2)
         return Fn.ScaleAddFn.apply(self.shortcut(x), self.residual(x), self.gamma, lrelu, 0.2)
 
@@ -306,7 +307,7 @@ class resD(nn.Module):
         # each LeakyReLU's backward runs inside its only consumer's backward
         # (the next conv's data gradient, ScaleAddFn): Conv2dFn in_act / defer_act
         h = self.conv_r[0](x, act='lrelu', slope=0.2, defer_act=True)
-        return self.conv_r[2](h, act='lrelu', slope=0.2, in_act='lrelu', defer_act=True)
+        return self.conv_r[2](h, act='lrelu', slope=0.2, in_act='lrelu', defer_act='first_order')
 
 
 class DiscSent(nn.Module):

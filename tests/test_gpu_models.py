@@ -443,12 +443,16 @@ def test_fused_activation_backward_matches_separate(gpu, monkeypatch):
         assert rel_l2(gp1[n], gp0[n]) < 2e-2, n
 
 
-def test_gradient_penalty_fused_adds_match_separate(gpu, monkeypatch):
+@pytest.mark.parametrize('knob', ['FUSE_GP_ADDS', 'FUSE_GP_ACT'])
+def test_gradient_penalty_fused_adds_match_separate(gpu, monkeypatch, knob):
     """The gradient penalty's create_graph backward with resD's two input
     gradients summed in the conv epilogue (PoolConvBwdDataFn) and ScaleAdd's
     double backward in one pass (ScaleAddBwdFn) against the separate passes
-    plus autograd adds (EEGAN_FUSE_GP_ADDS=0): the same sums, rounded to bf16
-    once instead of twice, so gradients agree to bf16 rounding."""
+    plus autograd adds (EEGAN_FUSE_GP_ADDS=0); and with the LeakyReLU
+    backward folded into the consuming conv's data gradient
+    (GatedConvBwdDataFn) against separate ActBwdFn passes
+    (EEGAN_FUSE_GP_ACT=0): the same values, rounded to bf16 once instead of
+    twice, so gradients agree to bf16 rounding."""
     import models
     from eegan_hip import functional as Fn
     from eegan_hip.trainer import Trainer
@@ -463,7 +467,7 @@ def test_gradient_penalty_fused_adds_match_separate(gpu, monkeypatch):
     s = seeded_tensor('gpf:s', (2, 256), 1).to(gpu)
     res = []
     for fuse in (False, True):
-        monkeypatch.setattr(Fn, 'FUSE_GP_ADDS', fuse)
+        monkeypatch.setattr(Fn, knob, fuse)
         D.zero_grad(set_to_none=True)
         gp = Trainer.MA_gradient_penalty(Fn.ImageToNhwcFn.apply(x), s, netD, True)
         gp.backward()
