@@ -56,6 +56,9 @@ GTERM_GRAD_EARLY = int(os.environ.get('EEGAN_GTERM_GRAD_EARLY', '-1'))   # -1: +
 # first packets of the critical lane then do not queue behind the others' (C2: 678 vs 656 img/s,
 # tools/gpu_env_ab.sh); EEGAN_LANE_ORDER=fwd: D64, D128, D256 after the DAMSM lane
 LANE_ORDER = os.environ.get('EEGAN_LANE_ORDER', 'rev')
+# EEGAN_GEN_SIDE=0: the generator's stage 2-3 Cum_Block / image branches stay on the
+# main stream (models.Gen.forward_branched puts them on D64's idle lane)
+GEN_SIDE = os.environ.get('EEGAN_GEN_SIDE', '1') != '0'
 
 # a g_update term already differentiated w.r.t. its fake image on its lane
 # (GTERM_GRAD_EARLY): its value, the image alias and the gradient there
@@ -440,6 +443,11 @@ class Trainer(object):
                                     inputs=self.optimizerG.params)
         else:
             g_loss.backward(inputs=self.optimizerG.params)
+        gen = getattr(self.netG, 'module', self.netG)
+        if getattr(gen, 'side_stream', None) is not None:
+            # the branch's backward nodes ran on the lane: their direct p.grad writes
+            # (functional._grad_sink) are not among autograd's leaf-stream syncs
+            self._join([gen.side_stream])
         Fn.stamp('G backward (D, DAMSM, G)')
         self.optimizerG.step()
         Fn.stamp('G adam')
@@ -505,6 +513,10 @@ class Trainer(object):
             noise = torch.randn(B, 100, device=dev)
         _, attn_attr_emb = self.attr_enhance(sent, attrs)
         attn_attr_emb = self.attr_enhance.module.attr_merge(attn_attr_emb)
+        gen = getattr(self.netG, 'module', self.netG)
+        if hasattr(gen, 'side_stream'):
+            # stage 2-3 Cum_Block / image branches on D64's lane, idle until d_update forks
+            gen.side_stream = self._side_streams(len(self.netsD) + 1, fork=False)[0] if GEN_SIDE else None
         fake_imgs = self.netG(noise, sent, attn_attr_emb)
         Fn.stamp('ATTR + G forward')
         _, _, match_labels = prepare_labels(B, dev)

@@ -165,10 +165,15 @@ class Cum_Block(nn.Module):
         self.fuse_block = conv3x3(cur_channel, cur_channel)
         self.gamma = nn.Parameter(torch.zeros(1))
 
-    def forward(self, prev_feat, cur_feat):
+    def up(self, prev_feat):
         u = self.up_block[0](prev_feat)
-        u = self.up_block[2](u, up2=True)     # nearest-2x folded into the conv's input gather
+        return self.up_block[2](u, up2=True)  # nearest-2x folded into the conv's input gather
+
+    def fuse(self, u, cur_feat):
         return self.fuse_block(Fn.ScaleAddFn.apply(u, cur_feat, self.gamma))
+
+    def forward(self, prev_feat, cur_feat):
+        return self.fuse(self.up(prev_feat), cur_feat)
 
 
 class ATTR_Enhance(nn.Module):
@@ -220,6 +225,9 @@ class Gen(nn.Module):
         self.init_mask = get_mask(ngf * 8)
         self.scales = [4, 8, 16, 32, 64, 128, 256]
         self.stages = 3  # 1: the harness stage-1 slice (img_64 only)
+        # a HIP stream the trainer lends (None: one stream): the Cum_Block / image
+        # branches of stages 2-3 run on it beside SAGB blocks 5-6 (forward_branched)
+        self.side_stream = None
 
     @staticmethod
     def SAGB_progress(feat, conds, stage_mask, scale, SAGB_block, gb=None):
@@ -257,6 +265,8 @@ class Gen(nn.Module):
                                                  gb[ix + 1])
         x_32 = out
         x_64, stage_mask = self.SAGB_progress(x_32, [sent, attrs], stage_mask, 64, self.blocks[4], gb[4])
+        if self.stages == 3 and self.side_stream is not None:
+            return self.forward_branched(x_32, x_64, stage_mask, sent, attrs, gb)
         cum_x_64 = self.cum_64(x_32, x_64)
         img_64 = self.get_image_64(cum_x_64)
         if self.stages == 1:
@@ -266,6 +276,32 @@ class Gen(nn.Module):
         cum_x_128 = self.cum_128(cum_x_64, x_128)
         cum_x_256 = self.cum_256(cum_x_128, x_256)
         img_128 = self.get_image_128(cum_x_128)
+        img_256 = self.get_image_256(cum_x_256)
+        return [img_64, img_128, img_256]
+
+    def forward_branched(self, x_32, x_64, stage_mask, sent, attrs, gb):
+        """Stages 2-3 as two streams: SAGB blocks 5 and 6 (the x_128 / x_256
+        chain, with the masks) on the caller's stream; the Cum_Blocks, the
+        image heads and each next Cum_Block's upsampling branch on
+        `side_stream`, which depends only on x_32 / x_64 / x_128.  The same
+        operations on the same inputs as forward(); their backward nodes run on
+        the stream of their forward (autograd), so the generator's backward
+        splits the same way."""
+        main, side = torch.cuda.current_stream(), self.side_stream
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            cum_x_64 = self.cum_64(x_32, x_64)
+            img_64 = self.get_image_64(cum_x_64)
+            u_128 = self.cum_128.up(cum_x_64)
+        x_128, stage_mask = self.SAGB_progress(x_64, [sent, attrs], stage_mask, 128, self.blocks[5], gb[5])
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            cum_x_128 = self.cum_128.fuse(u_128, x_128)
+            img_128 = self.get_image_128(cum_x_128)
+            u_256 = self.cum_256.up(cum_x_128)
+        x_256, _ = self.SAGB_progress(x_128, [sent, attrs], stage_mask, 256, self.blocks[6], gb[6])
+        main.wait_stream(side)
+        cum_x_256 = self.cum_256.fuse(u_256, x_256)
         img_256 = self.get_image_256(cum_x_256)
         return [img_64, img_128, img_256]
 
