@@ -59,6 +59,11 @@ LANE_ORDER = os.environ.get('EEGAN_LANE_ORDER', 'rev')
 # EEGAN_GEN_SIDE=0: the generator's stage 2-3 Cum_Block / image branches stay on the
 # main stream (models.Gen.forward_branched puts them on D64's idle lane)
 GEN_SIDE = os.environ.get('EEGAN_GEN_SIDE', '1') != '0'
+# EEGAN_WGRAD_LANES=1: the generator's direct weight / bias gradient writes run on
+# D128's / D256's lanes (idle during g_update's backward; functional._WG_SIDE)
+# instead of the streams of their backward nodes: -2.3 % in-process A/B
+# (profiles/r04_wgrad_lanes_ab.txt), off
+WGRAD_LANES = os.environ.get('EEGAN_WGRAD_LANES', '0') != '0'
 
 # a g_update term already differentiated w.r.t. its fake image on its lane
 # (GTERM_GRAD_EARLY): its value, the image alias and the gradient there
@@ -425,6 +430,27 @@ class Trainer(object):
         # zeroes those before every use (train.py:451,457), and the GP's
         # interpolated-image gradient is never read -- skipping them changes no
         # parameter and saves the D weight-gradient passes
+        lanes = self._side_streams(nD + 1, fork=False) if (WGRAD_LANES and self.use_streams and nD >= 3) else None
+        if lanes is not None:
+            gen = getattr(self.netG, 'module', self.netG)
+            Fn._WG_SIDE[torch.cuda.current_stream().cuda_stream] = lanes[1]
+            if getattr(gen, 'side_stream', None) is not None:
+                Fn._WG_SIDE[gen.side_stream.cuda_stream] = lanes[2]
+        try:
+            self._g_backward(terms, dfake, g_adv, g_loss, s_loss, w_loss, a_loss)
+        finally:
+            Fn._WG_SIDE.clear()
+        gen = getattr(self.netG, 'module', self.netG)
+        if getattr(gen, 'side_stream', None) is not None:
+            # the branch's backward nodes ran on the lane: their direct p.grad writes
+            # (functional._grad_sink) are not among autograd's leaf-stream syncs
+            self._join([gen.side_stream])
+        Fn.stamp('G backward (D, DAMSM, G)')
+        self.optimizerG.step()
+        Fn.stamp('G adam')
+        return g_loss.detach()
+
+    def _g_backward(self, terms, dfake, g_adv, g_loss, s_loss, w_loss, a_loss):
         if any(isinstance(t, EarlyTerm) for t in terms):
             # per-D terms differentiated on their lanes enter at their image aliases
             roots, grads = _backward_roots(terms)
@@ -443,15 +469,6 @@ class Trainer(object):
                                     inputs=self.optimizerG.params)
         else:
             g_loss.backward(inputs=self.optimizerG.params)
-        gen = getattr(self.netG, 'module', self.netG)
-        if getattr(gen, 'side_stream', None) is not None:
-            # the branch's backward nodes ran on the lane: their direct p.grad writes
-            # (functional._grad_sink) are not among autograd's leaf-stream syncs
-            self._join([gen.side_stream])
-        Fn.stamp('G backward (D, DAMSM, G)')
-        self.optimizerG.step()
-        Fn.stamp('G adam')
-        return g_loss.detach()
 
     # ---------------------------------------------------- failure checks --
     CHECK_EVERY = 64   # steps between checks of the collectives' error state (each check synchronises)

@@ -200,6 +200,11 @@ class ATTR_Enhance(nn.Module):
         return attn_attrs.sum(dim=1)
 
 
+# Gen.forward_branched: cum_64's upsampling branch beside SAGB block 4 (False: after it;
+# in-process A/B -0.4 %, profiles/r04_gen_side_u64_ab.txt)
+GEN_SIDE_U64 = False
+
+
 class Gen(nn.Module):
     """models.py:183-256."""
 
@@ -264,9 +269,9 @@ class Gen(nn.Module):
             out, stage_mask = self.SAGB_progress(out, [sent, sent], stage_mask, scale, self.blocks[ix + 1],
                                                  gb[ix + 1])
         x_32 = out
-        x_64, stage_mask = self.SAGB_progress(x_32, [sent, attrs], stage_mask, 64, self.blocks[4], gb[4])
         if self.stages == 3 and self.side_stream is not None:
-            return self.forward_branched(x_32, x_64, stage_mask, sent, attrs, gb)
+            return self.forward_branched(x_32, stage_mask, sent, attrs, gb)
+        x_64, stage_mask = self.SAGB_progress(x_32, [sent, attrs], stage_mask, 64, self.blocks[4], gb[4])
         cum_x_64 = self.cum_64(x_32, x_64)
         img_64 = self.get_image_64(cum_x_64)
         if self.stages == 1:
@@ -279,18 +284,24 @@ class Gen(nn.Module):
         img_256 = self.get_image_256(cum_x_256)
         return [img_64, img_128, img_256]
 
-    def forward_branched(self, x_32, x_64, stage_mask, sent, attrs, gb):
-        """Stages 2-3 as two streams: SAGB blocks 5 and 6 (the x_128 / x_256
-        chain, with the masks) on the caller's stream; the Cum_Blocks, the
-        image heads and each next Cum_Block's upsampling branch on
+    def forward_branched(self, x_32, stage_mask, sent, attrs, gb):
+        """Stages 1 (from block 4) to 3 as two streams: SAGB blocks 4-6 (the
+        x_64 / x_128 / x_256 chain, with the masks) on the caller's stream; the
+        Cum_Blocks, the image heads and each Cum_Block's upsampling branch on
         `side_stream`, which depends only on x_32 / x_64 / x_128.  The same
         operations on the same inputs as forward(); their backward nodes run on
         the stream of their forward (autograd), so the generator's backward
         splits the same way."""
         main, side = torch.cuda.current_stream(), self.side_stream
+        u_64 = None
+        if GEN_SIDE_U64:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                u_64 = self.cum_64.up(x_32)
+        x_64, stage_mask = self.SAGB_progress(x_32, [sent, attrs], stage_mask, 64, self.blocks[4], gb[4])
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            cum_x_64 = self.cum_64(x_32, x_64)
+            cum_x_64 = self.cum_64.fuse(u_64 if u_64 is not None else self.cum_64.up(x_32), x_64)
             img_64 = self.get_image_64(cum_x_64)
             u_128 = self.cum_128.up(cum_x_64)
         x_128, stage_mask = self.SAGB_progress(x_64, [sent, attrs], stage_mask, 128, self.blocks[5], gb[5])
