@@ -431,9 +431,10 @@ def _as_bf16_grad(g):
 
 # EEGAN_FUSE_ACT_BWD=0: every activation backward runs as its own pass (A/B switch).
 FUSE_ACT_BWD = os.environ.get('EEGAN_FUSE_ACT_BWD', '1') != '0'
-# EEGAN_FUSE_GP_ACT=0: under create_graph (the gradient penalty's first backward)
-# every activation backward runs as its own ActBwdFn pass.
-FUSE_GP_ACT = os.environ.get('EEGAN_FUSE_GP_ACT', '1') != '0'
+# False: under create_graph (the gradient penalty's first backward) every
+# activation backward runs as its own ActBwdFn pass (module constant for A/B:
+# tools/ab_inproc.py "py:eegan_hip.functional.FUSE_GP_ACT=False").
+FUSE_GP_ACT = True
 
 
 def _act_deferred(ctx, fused, cg):
@@ -560,9 +561,10 @@ class PoolConvFn(torch.autograd.Function):
         return dx, dW, db, None, None, None, None, None
 
 
-# EEGAN_FUSE_GP_ADDS=0: the gradient penalty's create_graph backward sums resD's
-# two input gradients and ScaleAdd's two output gradients with separate passes
-FUSE_GP_ADDS = os.environ.get('EEGAN_FUSE_GP_ADDS', '1') != '0'
+# False: the gradient penalty's create_graph backward sums resD's two input
+# gradients and ScaleAdd's two output gradients with separate passes (module
+# constant for A/B, as FUSE_GP_ACT)
+FUSE_GP_ADDS = True
 
 
 class PoolConvBwdDataFn(torch.autograd.Function):

@@ -56,14 +56,15 @@ GTERM_GRAD_EARLY = int(os.environ.get('EEGAN_GTERM_GRAD_EARLY', '-1'))   # -1: +
 # first packets of the critical lane then do not queue behind the others' (C2: 678 vs 656 img/s,
 # tools/gpu_env_ab.sh); EEGAN_LANE_ORDER=fwd: D64, D128, D256 after the DAMSM lane
 LANE_ORDER = os.environ.get('EEGAN_LANE_ORDER', 'rev')
-# EEGAN_GEN_SIDE=0: the generator's stage 2-3 Cum_Block / image branches stay on the
-# main stream (models.Gen.forward_branched puts them on D64's idle lane)
-GEN_SIDE = os.environ.get('EEGAN_GEN_SIDE', '1') != '0'
-# EEGAN_WGRAD_LANES=1: the generator's direct weight / bias gradient writes run on
-# D128's / D256's lanes (idle during g_update's backward; functional._WG_SIDE)
-# instead of the streams of their backward nodes: -2.3 % in-process A/B
-# (profiles/r04_wgrad_lanes_ab.txt), off
-WGRAD_LANES = os.environ.get('EEGAN_WGRAD_LANES', '0') != '0'
+# False: the generator's stage 2-3 Cum_Block / image branches stay on the main
+# stream (models.Gen.forward_branched puts them on D64's idle lane; module
+# constant for A/B: tools/ab_inproc.py "py:eegan_hip.trainer.GEN_SIDE=False")
+GEN_SIDE = True
+# True: the generator's direct weight / bias gradient writes run on D128's /
+# D256's lanes (idle during g_update's backward; functional._WG_SIDE) instead
+# of the streams of their backward nodes: -2.3 % in-process A/B
+# (profiles/r04_wgrad_lanes_ab.txt), off (module constant)
+WGRAD_LANES = False
 
 # a g_update term already differentiated w.r.t. its fake image on its lane
 # (GTERM_GRAD_EARLY): its value, the image alias and the gradient there

@@ -448,10 +448,10 @@ def test_gradient_penalty_fused_adds_match_separate(gpu, monkeypatch, knob):
     """The gradient penalty's create_graph backward with resD's two input
     gradients summed in the conv epilogue (PoolConvBwdDataFn) and ScaleAdd's
     double backward in one pass (ScaleAddBwdFn) against the separate passes
-    plus autograd adds (EEGAN_FUSE_GP_ADDS=0); and with the LeakyReLU
+    plus autograd adds (Fn.FUSE_GP_ADDS = False); and with the LeakyReLU
     backward folded into the consuming conv's data gradient
     (GatedConvBwdDataFn) against separate ActBwdFn passes
-    (EEGAN_FUSE_GP_ACT=0): the same values, rounded to bf16 once instead of
+    (Fn.FUSE_GP_ACT = False): the same values, rounded to bf16 once instead of
     twice, so gradients agree to bf16 rounding."""
     import models
     from eegan_hip import functional as Fn
