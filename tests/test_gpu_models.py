@@ -377,6 +377,38 @@ def test_generator(gpu):
             _check('gen/' + k, v, g['gen/after/' + k], 2e-2)
 
 
+def test_generator_branched_matches_single_stream(gpu):
+    """Gen.forward_branched (stage 2-3 Cum_Block / image branches on a second
+    stream, the trainer's GEN_SIDE) runs the same operations on the same inputs
+    as the single-stream forward: images bit-identical; the backward sums the
+    gradients of multi-consumer activations in another order (bf16 rounding)."""
+    import models
+    from _util import rel_l2
+    G = _load(models.Gen(8, 100), 'gen', 21, gpu)
+    z = seeded_tensor('g:z', (2, 100), 1).to(gpu)
+    side = torch.cuda.Stream()
+    res = []
+    for st in (None, side):
+        G.side_stream = st
+        G.zero_grad(set_to_none=True)
+        s = seeded_tensor('g:s', (2, 256), 1).to(gpu).requires_grad_()
+        a = seeded_tensor('g:a', (2, 256), 1).to(gpu).requires_grad_()
+        imgs = G(z, s, a)
+        loss = sum((im.float() * seeded_tensor('g:r%d' % k, im.shape, 2).to(gpu)).sum() for k, im in enumerate(imgs))
+        loss.backward()
+        torch.cuda.synchronize()
+        res.append(([im.float().cpu() for im in imgs], s.grad.cpu(), a.grad.cpu(),
+                    {n: p.grad.cpu().clone() for n, p in G.named_parameters() if p.grad is not None}))
+    G.side_stream = None
+    (i0, s0, a0, g0), (i1, s1, a1, g1) = res
+    for x, y in zip(i0, i1):
+        assert torch.equal(x, y)
+    assert set(g0) == set(g1)
+    assert rel_l2(s1, s0) < 2e-2 and rel_l2(a1, a0) < 2e-2
+    for n in g0:
+        assert rel_l2(g1[n], g0[n]) < 2e-2, n
+
+
 def test_generator_grouped_mlps_match_per_layer(gpu, monkeypatch):
     """Fn.AffineMLPsFn (all affine_ssa MLPs in grouped launches) computes the
     same products in the same order as the per-layer LinearFn path: images
