@@ -153,8 +153,10 @@ def cpu_baseline(seconds_budget=30.0):
     reference step, pinned to golden vectors captured from the reference)
     timed on the host: BASELINE.md's CPU plan -- W=32, B=4, the five frozen
     text-encoder calls (train.py:169-184) inside the step, the full 3-stage
-    step (incl. the Inception-v3 restatement) and the C1 stage-1 slice,
-    median of up to 10 steps after 2 warm-ups, threads = all affinity cores."""
+    step (incl. the Inception-v3 restatement) and the C1 stage-1 slice;
+    warm-ups until two consecutive steps agree within 10 %, then the median of
+    at least 10 steps; threads = the affinity set capped by the box's CPU
+    share (stated as `threads_reason`)."""
     from oracle import eegan_oracle as O
     from oracle.seeding import seeded_state, synthetic_batch
     import models
@@ -188,32 +190,48 @@ def cpu_baseline(seconds_budget=30.0):
                                                                       models.Dis256(W, True, ncls)][:nd])]
         nets = O.OracleNets(sd_g, sd_a, sd_ds, W, W, True, ncls)
         og, ods = O.make_adams(nets)
-        for k in range(2):  # warm-ups
+        # warm-ups until two consecutive steps agree within 10 % (the first steps run up to
+        # 2x slower: allocator and thread-pool warm-up), at most 8
+        prev, warm = None, 0
+        while warm < 8:
             t0 = time.time()
             O.train_step(nets, og, ods, batch, encode_text(), enc, stages=stages)
-            print('bench: cpu baseline (%d stage%s) warm-up %d: %.1f s' % (stages, 's' if stages > 1 else '', k,
-                                                                        time.time() - t0), file=sys.stderr, flush=True)
+            dt = time.time() - t0
+            warm += 1
+            print('bench: cpu baseline (%d stage%s) warm-up %d: %.2f s' % (stages, 's' if stages > 1 else '', warm,
+                                                                         dt), file=sys.stderr, flush=True)
+            if prev is not None and abs(dt - prev) <= 0.1 * prev:
+                break
+            prev = dt
         times = []
         t_end = time.time() + budget
-        while len(times) < 10 and (time.time() < t_end or len(times) < 3):
+        while len(times) < 10 or (time.time() < t_end and len(times) < 20):
             t0 = time.time()
             O.train_step(nets, og, ods, batch, encode_text(), enc, stages=stages)
             times.append(time.time() - t0)
-            print('bench: cpu baseline (%d stage%s) step %d: %.1f s' % (stages, 's' if stages > 1 else '',
-                                                                      len(times), times[-1]), file=sys.stderr,
+            print('bench: cpu baseline (%d stage%s) step %d: %.2f s' % (stages, 's' if stages > 1 else '',
+                                                                       len(times), times[-1]), file=sys.stderr,
                   flush=True)
+        spread = (max(times) - min(times)) / min(times)
+        warmups[stages] = (warm, spread)
         times.sort()
         return B / times[len(times) // 2], len(times)
 
+    warmups = {}
     full, n_full = timed(3, seconds_budget)
     c1, n_c1 = timed(1, 0.25 * seconds_budget)
     return {'value': full, 'unit': 'images/sec', 'cores': torch.get_num_threads(), 'kind': 'port',
             'affinity_cores': affinity, 'cpu_model': _cpu_model(),
+            'threads_reason': ('OMP_NUM_THREADS=%d: the CPU share the GPU box grants this process; its affinity mask '
+                               'spans all %d cores of the host, shared with the other GPUs\' jobs' % (share, affinity))
+            if 0 < share < affinity else 'all affinity cores',
             'sample': 'oracle train_step (full 3-stage, W=32, B=4: 5 text-encoder calls, G, 3 x d_update incl. '
                       'the gradient penalty, g_update incl. the Inception-v3 restatement), median of %d steps after '
-                      '2 warm-ups' % n_full,
+                      '%d warm-ups (until two consecutive steps agreed within 10%%); max/min spread of the timed '
+                      'steps %.2f' % (n_full, warmups[3][0], warmups[3][1]),
             'c1_stage1': {'value': c1, 'unit': 'images/sec', 'sample': 'C1 stage-1 slice (img_64, Dis64, DAMSM on '
-                                                                       'img_64), B=4, median of %d steps' % n_c1}}
+                                                                       'img_64), B=4, median of %d steps after %d '
+                                                                       'warm-ups' % (n_c1, warmups[1][0])}}
 
 
 def main():

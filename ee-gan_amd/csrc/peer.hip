@@ -22,9 +22,13 @@
 // parity of epoch e.  The epoch lives on the device, so a captured call keeps
 // counting when the step graph is replayed.
 //
-// Every wait is bounded (~2 s of the 100 MHz wall clock): a rank whose peer
+// Every wait is bounded (30 s of the 100 MHz wall clock): a rank whose peer
 // never arrives records an error and exits, so the grid always drains;
-// eegan_peer_status reports it.
+// eegan_peer_status reports it.  A call that finds the error word set in the
+// own region or in any peer's (a wait of this lane already gave up on some
+// rank) does not push or wait at all: it poisons its result at once, so after
+// a dead peer only the first call of a lane pays the bound, not every later
+// SyncBN call until the host's periodic check raises.
 #include <string.h>
 
 #include "common.h"
@@ -62,24 +66,29 @@ __global__ __launch_bounds__(256) void peer_allreduce_kernel(double* t, int n, i
   __shared__ int s_timeout;
   if (tid == 0) {
     s_ep = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1ull;
-    s_timeout = 0;
+    unsigned err = 0;
+    for (int p = 0; p < world; ++p)
+      err |= __hip_atomic_load(reinterpret_cast<unsigned*>(ps.base[p] + OFF_ERR), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    s_timeout = err != 0u;   // an earlier call of this lane gave up on a rank: poison at once
   }
   __syncthreads();
   const unsigned long long ep = s_ep;
   const int par = (int)(ep & 1ull);
+  const bool live = s_timeout == 0;
 
   // push this rank's message into every rank's slot [par][rank]
-  for (int p = 0; p < world; ++p) {
+  for (int p = 0; p < world && live; ++p) {
     double* dst = slot_at(ps.base[p], par, rank, cap);
     for (int i = tid; i < n; i += 256) dst[i] = t[i];
   }
   __threadfence_system();
   __syncthreads();
-  if (tid < world)
+  if (tid < world && live)
     __hip_atomic_store(flag_at(ps.base[tid], par, rank), ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 
   // wait for every rank's slice in the own region (bounded)
-  if (tid < world) {
+  if (tid < world && live) {
     const unsigned long long t0 = wall_clock64();
     unsigned long long* f = flag_at(own, par, tid);
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != ep) {

@@ -18,10 +18,27 @@ else); any other global in the file raises instead of being imported.
 
 `TextDataset.__getitem__` returns the reference's nested sample
 ([image, cap, cap_len, cls_id, key], attrs, unpair) with `image` a
-`HostImage` (decoded uint8 RGB + bbox); `DeviceDataLoader` batches samples
-(torch DataLoader workers for decoding), runs the device transform and yields
-the reference's batch structure with the three image scales as device tensors,
-so train.py's prepare_data (train.py:58-88) consumes it unchanged.
+`HostImage` (decoded uint8 RGB + bbox).  Two ways to batch them:
+
+  * train.py's own `torch.utils.data.DataLoader` (train.py:274-278, default
+    collate): HostImage registers a collate function, so a batch's `imgs` is a
+    `HostImageBatch` -- one entry per scale whose `.to(device)` (train.py:70)
+    runs the device transform for the whole batch once; the crop / flip draws
+    are taken at collate time from torch's global generator, in the process
+    that collates, in torchvision's per-sample order (where the reference's
+    transform draws them, datasets.py:412-413);
+  * `DeviceDataLoader`: the same, with the draws from its own generator and
+    the images in the drop-in models' NHWC bf16 layout if asked.
+
+Data parallel (one process per GPU, eegan_hip.launch): the reference's
+DataParallel scatters ONE batch over its GPUs (train.py:220-228).  Under
+torchrun every rank runs train.py with the same seed and the same shuffled
+DataLoader, so with a process group of world W up (or `shard=(rank, W)`) the
+dataset is rank r's stride-W shard -- item i is sample i*W + r, len // W items
+on every rank (equal, so every rank runs the same number of steps) -- and the
+constructor puts ranks > 0 on random streams of their own
+(launch.offset_rank_rngs), so captions, crops and noise differ across ranks.
+`--batch_size` is then the per-rank batch.
 """
 import io
 import os
@@ -68,11 +85,13 @@ def load_pickle(path, encoding='ASCII'):
 class HostImage(object):
     """A decoded sample image: uint8 RGB array (H, W, 3) and its bounding box
     (x, y, w, h) or None -- the state of get_imgs (datasets.py:400) before the
-    transform, which the device pipeline applies batch-wise."""
-    __slots__ = ('rgb', 'bbox')
+    transform, which the device pipeline applies batch-wise -- and the
+    dataset's scales (`TextDataset.imsize`; a spawned DataLoader worker's cfg
+    holds the defaults, not the YAML train.py loaded)."""
+    __slots__ = ('rgb', 'bbox', 'imsize')
 
-    def __init__(self, rgb, bbox):
-        self.rgb, self.bbox = rgb, bbox
+    def __init__(self, rgb, bbox, imsize=None):
+        self.rgb, self.bbox, self.imsize = rgb, bbox, imsize
 
 
 def decode_rgb(path):
@@ -92,13 +111,113 @@ def prepare_data(data, device):
     return [real_imgs, caps, cap_lens, cls_ids, keys]
 
 
+class HostImageBatch(object):
+    """A collated batch of HostImages as train.py's prepare_data consumes it
+    (train.py:68-70: `len(imgs)` scales, `imgs[i].to(device)`): entry i is
+    the batch at scale i; the first `.to(device)` of any scale runs the device
+    transform for all of them (eegan_hip.pipeline), the others reuse it.
+    Picklable, so DataLoader workers return it to the rank process."""
+
+    def __init__(self, records, draws, imsize, base_size, branch_num, layout='nchw_f32'):
+        self.records, self.draws = records, draws
+        self.imsize, self.base_size, self.branch_num, self.layout = imsize, base_size, branch_num, layout
+        self._outs = None
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        d['_outs'] = None
+        return d
+
+    def __len__(self):
+        return self.branch_num
+
+    def __getitem__(self, i):
+        if not -self.branch_num <= i < self.branch_num:
+            raise IndexError(i)
+        return _ScaleImages(self, i % self.branch_num)
+
+    def __iter__(self):
+        return (self[i] for i in range(self.branch_num))
+
+    def scale_shape(self, i):
+        s = self.base_size * (2 ** i)
+        return (len(self.records), 3, s, s)
+
+    def tensors(self, device):
+        device = torch.device(device)
+        if self._outs is None or self._outs[0] != device:
+            tf = _transform(device, self.imsize, self.base_size, self.branch_num, self.layout)
+            outs, _ = tf(self.records, None, draws=self.draws)
+            self._outs = (device, outs)
+        return self._outs[1]
+
+
+class _ScaleImages(object):
+    """One scale of a HostImageBatch: `.to(device)` / `.cuda()` give the tensor."""
+
+    def __init__(self, batch, i):
+        self.batch, self.i = batch, i
+
+    @property
+    def shape(self):
+        return torch.Size(self.batch.scale_shape(self.i))
+
+    def size(self, dim=None):
+        return self.shape if dim is None else self.shape[dim]
+
+    def to(self, device, *args, **kwargs):
+        return self.batch.tensors(device)[self.i]
+
+    def cuda(self, device=None):
+        return self.to('cuda' if device is None else device)
+
+
+_TRANSFORMS = {}
+
+
+def _transform(device, imsize, base_size, branch_num, layout):
+    from eegan_hip.pipeline import DeviceImageTransform
+    key = (str(device), imsize, base_size, branch_num, layout)
+    if key not in _TRANSFORMS:
+        _TRANSFORMS[key] = DeviceImageTransform(device, imsize=imsize, base_size=base_size,
+                                                branch_num=branch_num, layout=layout)
+    return _TRANSFORMS[key]
+
+
+def collate_host_images(batch, *, collate_fn_map=None):
+    """default_collate for a list of HostImages (registered below): the crop /
+    flip draws of train.py's transform (train.py:269-272: Resize(304) ->
+    RandomCrop(256) -> RandomHorizontalFlip) taken now, per sample in order,
+    from torch's global generator of the collating process -- the generator
+    the reference's transform draws from in its __getitem__."""
+    from eegan_hip.pipeline import plan_draws
+    sizes = batch[0].imsize or [cfg.TREE.BASE_SIZE * (2 ** i) for i in range(cfg.TREE.BRANCH_NUM)]
+    if any(list(im.imsize or sizes) != list(sizes) for im in batch):
+        raise ValueError('a batch mixes HostImages of different scale sets')
+    base, branch, imsize = sizes[0], len(sizes), sizes[-1]
+    records = [(im.rgb, im.bbox) for im in batch]
+    return HostImageBatch(records, plan_draws(records, imsize, None), imsize, base, branch)
+
+
+def _register_collate():
+    from torch.utils.data._utils.collate import default_collate_fn_map
+    default_collate_fn_map[HostImage] = collate_host_images
+
+
+_register_collate()
+
+
 class TextDataset(data.Dataset):
     """datasets.py:192-445 with the same constructor, loaders, getters and
     sample structure; `transform` is accepted for signature parity and must
     be None or the reference's train transform -- the image transform itself
-    runs in DeviceDataLoader."""
+    runs on the device when a batch's images are moved there.
 
-    def __init__(self, data_dir, dataset_name, attr_name='EE-GAN', split='train', transform=None):
+    `shard=(rank, world)` (default: the process group's, see the module
+    docstring) makes this rank's stride-`world` shard; the unpaired-caption
+    draw still ranges over the whole split, as in the reference."""
+
+    def __init__(self, data_dir, dataset_name, attr_name='EE-GAN', split='train', transform=None, shard=None):
         self.transform = transform
         self.split = split
         self.use_unpair = cfg.TRAIN.USE_UNPAIR
@@ -117,6 +236,21 @@ class TextDataset(data.Dataset):
         if self.use_attr:
             self.attributes = self.load_attributes(data_dir, attr_name, split)
         self.iterator = self.prepare_train_pair
+        if shard is None:
+            from eegan_hip.launch import data_shard
+            shard = data_shard()
+        self.shard_rank, self.shard_world = int(shard[0]), int(shard[1])
+        if not 0 <= self.shard_rank < self.shard_world:
+            raise ValueError('shard %r: need 0 <= rank < world' % (shard,))
+        if self.shard_world > 1:
+            from eegan_hip.launch import offset_rank_rngs
+            offset_rank_rngs(self.shard_rank)
+
+    def base_index(self, index):
+        """The split's sample behind this rank's item `index`."""
+        if not 0 <= index < self.__len__():
+            raise IndexError(index)
+        return index * self.shard_world + self.shard_rank
 
     # --------------------------------------------------------- loaders --
     @staticmethod
@@ -200,7 +334,7 @@ class TextDataset(data.Dataset):
 
     def get_imgs(self, img_path, bbox=None):
         """datasets.py:391-424 up to the transform: decode, keep the bbox."""
-        return HostImage(decode_rgb(img_path), None if bbox is None else [int(v) for v in bbox])
+        return HostImage(decode_rgb(img_path), None if bbox is None else [int(v) for v in bbox], list(self.imsize))
 
     def get_basic_pair(self, index):
         """datasets.py:363-374."""
@@ -212,10 +346,12 @@ class TextDataset(data.Dataset):
         return image, cap, cap_len, cls_id, key, sent_ix
 
     def get_cap_unpair(self, cls_id):
-        """datasets.py:376-382 (numpy randint: high exclusive)."""
-        unpair_idx = random.randint(0, self.__len__())
+        """datasets.py:376-382 (numpy randint: high exclusive), over the whole
+        split (not this rank's shard)."""
+        n = self.number_example
+        unpair_idx = random.randint(0, n)
         while self.class_id[unpair_idx] == cls_id:
-            unpair_idx = (unpair_idx + 1) % self.__len__()
+            unpair_idx = (unpair_idx + 1) % n
         caps, cap_len, _ = self.get_cap_one(unpair_idx)
         return caps, cap_len, self.class_id[unpair_idx], unpair_idx
 
@@ -238,10 +374,10 @@ class TextDataset(data.Dataset):
         return [image, cap, cap_len, cls_id, key], ret_attrs, ret_unpair
 
     def __len__(self):
-        return len(self.filenames)
+        return len(self.filenames) // self.shard_world
 
     def __getitem__(self, index):
-        return self.iterator(index)
+        return self.iterator(self.base_index(index))
 
 
 class TextOnlyDataset(data.Dataset):
@@ -329,7 +465,8 @@ class DeviceDataLoader(object):
         imsize = dataset.imsize[-1]
         self.transform = DeviceImageTransform(device, imsize=imsize, base_size=dataset.imsize[0],
                                               branch_num=len(dataset.imsize), layout=layout)
-        self.generator = torch.Generator().manual_seed(seed)
+        # a rank of a sharded dataset draws its own crops
+        self.generator = torch.Generator().manual_seed(seed + getattr(dataset, 'shard_rank', 0))
         self.last_draws = None
 
     def __len__(self):

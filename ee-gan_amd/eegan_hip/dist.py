@@ -244,6 +244,9 @@ class GradHooks(object):
             torch.autograd.Variable._execution_engine.queue_callback(self._finish)
 
     def _finish(self):
+        self._backwards = getattr(self, '_backwards', 0) + 1
+        if self._backwards % CHECK_EVERY == 0:
+            check_collectives()
         for bi in range(len(self.buckets)):
             if self._fired[bi]:
                 self._launch(bi)
@@ -257,6 +260,46 @@ class GradHooks(object):
                 p.grad.copy_(flat[o:o + n].view_as(p.grad))
                 o += n
         self._reset()
+
+
+def broadcast_state(module, src=0):
+    """Rank `src`'s parameters and buffers into every rank's module, in place
+    (torch DDP does this when it wraps a module).  Under an unchanged train.py
+    the ranks build their models after eegan_hip.launch.offset_rank_rngs gave
+    each rank its own random streams, so their initial weights differ; the
+    reference's replicas all start from GPU0's module (train.py:220-228)."""
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            x = t.data
+            if not x.is_contiguous() and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last):
+                x = x.permute(0, 2, 3, 1)   # channels-last conv weights: a contiguous view of the storage
+            if not x.is_contiguous():
+                raise RuntimeError('eegan_hip: cannot broadcast a non-dense %s of shape %s'
+                                   % (type(module).__name__, tuple(t.shape)))
+            dist.broadcast(x, src)
+
+
+def check_collectives():
+    """Raise if a SyncBN peer-write reduction timed out (EEGAN_SYNCBN_PEER;
+    csrc/peer.hip poisons its output with NaN and every later call of that
+    lane at once).  Synchronises the device when the peer path is on; a no-op
+    otherwise.  Called by the trainer every CHECK_EVERY steps, by GradHooks
+    every CHECK_EVERY backwards (an unchanged train.py) and before any drop-in
+    model's state_dict is taken (a desynchronised rank must not write a
+    checkpoint, train.py:310-318)."""
+    red = Fn.SYNC_BN_ALLREDUCE
+    if red is not None and hasattr(red, 'check'):
+        red.check()
+
+
+CHECK_EVERY = 64   # steps (or backwards) between the periodic checks above
+
+
+def guard_state_dict(module):
+    """state_dict() of `module` (and of any wrapper around it: torch's
+    state_dict recurses through the children's state_dict) checks the
+    collectives first."""
+    module.register_state_dict_pre_hook(lambda m, prefix, keep_vars: check_collectives())
 
 
 def ensure_grad_hooks(module):
@@ -274,5 +317,6 @@ def ensure_grad_hooks(module):
             raise RuntimeError('eegan_hip: %s runs as an nn.DataParallel replica (non-leaf parameters); the '
                                'data-parallel drop-in needs ONE visible GPU per rank (CUDA_VISIBLE_DEVICES / '
                                'HIP_VISIBLE_DEVICES set per rank, see INTEGRATION.md)' % type(module).__name__)
+        broadcast_state(module)
         module._eegan_grad_hooks = GradHooks(module)
     return getattr(module, '_eegan_grad_hooks', None)

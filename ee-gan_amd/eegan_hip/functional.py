@@ -9,7 +9,6 @@ so they are differentiable to any order -- needed by the MA gradient penalty
 Generator-side Functions (BN modulation, upsample-fused convs, linears,
 mask resize) are first-order, as the reference only differentiates G once.
 """
-import contextlib
 import ctypes
 import os
 import math
@@ -111,56 +110,18 @@ def _sink_of(ctx, i):
     return g
 
 
-# Conv weight / bias gradients written straight into p.grad can run on a
-# companion stream of the issuing stream, off the chain of data gradients that
-# the next layer's backward waits for: _WG_SIDE maps a stream handle to an
-# already-existing stream that is idle at the time (the trainer lends its idle
-# discriminator lanes to the generator's backward, trainer.WGRAD_LANES; a new
-# stream forked into the captured step crashes the runtime's end of capture,
-# DESIGN.md §3).  The owning FlatAdam joins the companions before it reads or
-# zeroes the gradients (FlatAdam.join_side_writes) and keeps the tensors they
-# read alive until then.  Not used while FlatAdam's overlapped all-reduce
-# tracks the writes (world > 1).
-_WG_SIDE = {}   # issuing stream handle -> companion stream
-
-
-def _sink_var(ctx, i):
-    node = ctx.next_functions[i][0]
-    return getattr(node, 'variable', None) if node is not None else None
-
-
-def _on_wgrad_side(var, *keep):
-    """Stream context for a direct p.grad write of parameter `var` reading
-    `keep`: the current lane's companion stream, or the lane itself."""
-    if not _WG_SIDE:
-        return contextlib.nullcontext()
-    opt = getattr(var, '_eegan_opt', None) if var is not None else None
-    if (opt is None or not var.is_cuda or getattr(var, '_eegan_track', None) is not None
-            or not hasattr(opt, 'note_side_write')):
-        return contextlib.nullcontext()
-    cur = torch.cuda.current_stream()
-    side = _WG_SIDE.get(cur.cuda_stream)
-    if side is None:
-        return contextlib.nullcontext()
-    side.wait_stream(cur)
-    opt.note_side_write(side, keep)
-    return torch.cuda.stream(side)
-
-
 def _sink_wgrad(ctx, i, x, dz, g, W_shape):
     """dW of input i accumulated into its FlatAdam gradient view; False when
     the gradient has to go through autograd instead."""
     sink = _grad_sink(ctx, i)
     if sink is None or not sink.is_contiguous(memory_format=CL):
         return False
-    with _on_wgrad_side(_sink_var(ctx, i), x, dz):
-        conv_bwd_weight_raw(x, dz, g, W_shape, out=sink)
+    conv_bwd_weight_raw(x, dz, g, W_shape, out=sink)
     return True
 
 
 def _sink_chansum(ctx, i, dz, sink):
-    with _on_wgrad_side(_sink_var(ctx, i), dz):
-        chansum_raw(dz, out=sink)
+    chansum_raw(dz, out=sink)
 
 
 # ============================================================== weights ===
@@ -548,8 +509,7 @@ class PoolConvFn(torch.autograd.Function):
         if dz is not None and _needed(ctx, 1):
             sink = _grad_sink(ctx, 1)
             if sink is not None and sink.is_contiguous(memory_format=CL):
-                with _on_wgrad_side(_sink_var(ctx, 1), x, dz):
-                    conv_bwd_weight_raw(x, dz, g, W.shape, out=sink)
+                conv_bwd_weight_raw(x, dz, g, W.shape, out=sink)
             else:
                 dW = ConvBwdWeightFn.apply(x, dz, g)
         if dz is not None and ctx.needs_input_grad[2] and _needed(ctx, 2):

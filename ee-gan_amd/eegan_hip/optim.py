@@ -99,24 +99,6 @@ class FlatAdam(torch.optim.Optimizer):
         self._key_seen = {}      # window key -> windows opened under it
         self._late = set()       # params whose gradient went through autograd at least once
         self._win = None
-        self._side = {}          # companion streams holding direct gradient writes (functional.WGRAD_SIDE)
-        self._side_keep = []     # tensors those writes read, alive until the join
-
-    def note_side_write(self, stream, keep):
-        """A direct gradient write into gflat is issued on `stream` (a lane's
-        companion, functional._on_wgrad_side), reading `keep`."""
-        self._side[stream.cuda_stream] = stream
-        self._side_keep.extend(keep)
-
-    def join_side_writes(self):
-        """The current stream waits for every companion stream that wrote
-        gradients since the last join; their inputs may be freed after."""
-        if self._side:
-            cur = torch.cuda.current_stream()
-            for s in self._side.values():
-                cur.wait_stream(s)
-            self._side.clear()
-            self._side_keep.clear()
 
     # ------------------------------------------------------ overlapped DP --
     def set_bucket_bytes(self, nbytes):
@@ -216,7 +198,6 @@ class FlatAdam(torch.optim.Optimizer):
         return True
 
     def zero_grad(self, set_to_none=False):
-        self.join_side_writes()
         ops.fill_f32(self.gflat.data_ptr(), self.numel, 0.0, stream())
         for p, o, k, g in self._views:
             if p.grad is None or p.grad.data_ptr() != g.data_ptr():
@@ -277,7 +258,6 @@ class FlatAdam(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
-        self.join_side_writes()
         self._sync_grads()
         self._allreduce()
         g = self.param_groups[0]

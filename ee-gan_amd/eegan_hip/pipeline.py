@@ -103,6 +103,19 @@ def draw_crop_flip(h, w, crop, generator):
     return i, j, flip
 
 
+def plan_draws(records, imsize, generator, resize=None):
+    """The crop / flip draws of a batch, per record in order (host only): the
+    bounding-box crop, Resize(resize) sizes and draw_crop_flip on each."""
+    resize = int(imsize * 76 / 64) if resize is None else resize
+    out = []
+    for arr, bbox in records:
+        H, W = np.asarray(arr).shape[:2]
+        x1, y1, x2, y2 = bbox_crop_box(W, H, bbox)
+        nw, nh = resized_size(x2 - x1, y2 - y1, resize)
+        out.append(draw_crop_flip(nh, nw, imsize, generator))
+    return out
+
+
 class DeviceImageTransform(object):
     """Batch transform on the GPU.  __call__(records, generator) takes a list of
     (uint8 HxWx3 array, bbox or None) and returns the list of images per scale
@@ -127,9 +140,13 @@ class DeviceImageTransform(object):
             ct = torch.from_numpy(c.reshape(-1)).to(self.device)
             self._tables.append((s, k, bt, ct))
 
-    def plan(self, records, generator):
-        """Host side: crop boxes, resize sizes, draws, PIL weights and the
-        packed source sub-rectangles each image's kernels read."""
+    def plan(self, records, generator, draws=None):
+        """Host side: crop boxes, resize sizes, draws (from `generator`, or the
+        given per-record `draws`), PIL weights and the packed source
+        sub-rectangles each image's kernels read."""
+        given = draws
+        if given is not None and len(given) != len(records):
+            raise ValueError('%d draws for %d records' % (len(given), len(records)))
         jobs, coefs, bounds, draws, srcs = [], [], [], [], []
         cof = bof = 0
         src_off = 0
@@ -142,7 +159,12 @@ class DeviceImageTransform(object):
             x1, y1, x2, y2 = bbox_crop_box(W, H, bbox)
             cw, ch = x2 - x1, y2 - y1
             nw, nh = resized_size(cw, ch, self.resize)
-            i, j, flip = draw_crop_flip(nh, nw, crop, generator)
+            if given is None:
+                i, j, flip = draw_crop_flip(nh, nw, crop, generator)
+            else:
+                i, j, flip = (int(given[len(draws)][0]), int(given[len(draws)][1]), bool(given[len(draws)][2]))
+                if not (0 <= i <= nh - crop and 0 <= j <= nw - crop):
+                    raise ValueError('crop draw (%d, %d) outside the %dx%d resized image' % (i, j, nh, nw))
             draws.append((i, j, flip))
             hb, hc, hk = pil_bilinear_coeffs(cw, nw)
             vb, vc, vk = pil_bilinear_coeffs(ch, nh)
@@ -164,9 +186,9 @@ class DeviceImageTransform(object):
             src_off += (sub.nbytes + 15) // 16 * 16
         return jobs, np.concatenate(coefs), np.concatenate(bounds), draws, srcs, src_off
 
-    def __call__(self, records, generator, crop_u8=None):
+    def __call__(self, records, generator, crop_u8=None, draws=None):
         B = len(records)
-        jobs, coef, bounds, draws, srcs, nsrc = self.plan(records, generator)
+        jobs, coef, bounds, draws, srcs, nsrc = self.plan(records, generator, draws)
         dev = self.device
         host = torch.empty(nsrc, dtype=torch.uint8, pin_memory=torch.cuda.is_available())
         hv = host.numpy()

@@ -60,11 +60,6 @@ LANE_ORDER = os.environ.get('EEGAN_LANE_ORDER', 'rev')
 # stream (models.Gen.forward_branched puts them on D64's idle lane; module
 # constant for A/B: tools/ab_inproc.py "py:eegan_hip.trainer.GEN_SIDE=False")
 GEN_SIDE = True
-# True: the generator's direct weight / bias gradient writes run on D128's /
-# D256's lanes (idle during g_update's backward; functional._WG_SIDE) instead
-# of the streams of their backward nodes: -2.3 % in-process A/B
-# (profiles/r04_wgrad_lanes_ab.txt), off (module constant)
-WGRAD_LANES = False
 
 # a g_update term already differentiated w.r.t. its fake image on its lane
 # (GTERM_GRAD_EARLY): its value, the image alias and the gradient there
@@ -431,16 +426,7 @@ class Trainer(object):
         # zeroes those before every use (train.py:451,457), and the GP's
         # interpolated-image gradient is never read -- skipping them changes no
         # parameter and saves the D weight-gradient passes
-        lanes = self._side_streams(nD + 1, fork=False) if (WGRAD_LANES and self.use_streams and nD >= 3) else None
-        if lanes is not None:
-            gen = getattr(self.netG, 'module', self.netG)
-            Fn._WG_SIDE[torch.cuda.current_stream().cuda_stream] = lanes[1]
-            if getattr(gen, 'side_stream', None) is not None:
-                Fn._WG_SIDE[gen.side_stream.cuda_stream] = lanes[2]
-        try:
-            self._g_backward(terms, dfake, g_adv, g_loss, s_loss, w_loss, a_loss)
-        finally:
-            Fn._WG_SIDE.clear()
+        self._g_backward(terms, dfake, g_adv, g_loss, s_loss, w_loss, a_loss)
         gen = getattr(self.netG, 'module', self.netG)
         if getattr(gen, 'side_stream', None) is not None:
             # the branch's backward nodes ran on the lane: their direct p.grad writes
@@ -472,15 +458,13 @@ class Trainer(object):
             g_loss.backward(inputs=self.optimizerG.params)
 
     # ---------------------------------------------------- failure checks --
-    CHECK_EVERY = 64   # steps between checks of the collectives' error state (each check synchronises)
+    CHECK_EVERY = D.CHECK_EVERY   # steps between checks of the collectives' error state (each check synchronises)
 
     @staticmethod
     def check_collectives():
         """Raise if a SyncBN peer-write reduction timed out (EEGAN_SYNCBN_PEER):
         called every CHECK_EVERY steps / replays and before state is saved."""
-        red = Fn.SYNC_BN_ALLREDUCE
-        if red is not None and hasattr(red, 'check'):
-            red.check()
+        D.check_collectives()
 
     def state_dict(self):
         """Optimizer state for checkpoints (collectives checked first: a

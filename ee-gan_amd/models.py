@@ -181,6 +181,7 @@ class ATTR_Enhance(nn.Module):
 
     def __init__(self, ntf=cfg.TEXT.EMBEDDING_DIM):
         super().__init__()
+        D.guard_state_dict(self)   # a rank whose collectives failed must not checkpoint
         self.attr_query = Linear(ntf, ntf)
         self.attr_key = Linear(ntf, ntf)
         self.attr_value = Linear(ntf, ntf)
@@ -210,6 +211,7 @@ class Gen(nn.Module):
 
     def __init__(self, ngf=cfg.GAN.GF_DIM, nz=cfg.GAN.Z_DIM):
         super().__init__()
+        D.guard_state_dict(self)   # a rank whose collectives failed must not checkpoint
         self.ngf = ngf
         self.fc = Linear(nz, ngf * 8 * 4 * 4)
         self.blocks = nn.ModuleList([
@@ -271,16 +273,22 @@ class Gen(nn.Module):
         x_32 = out
         if self.stages == 3 and self.side_stream is not None:
             return self.forward_branched(x_32, stage_mask, sent, attrs, gb)
+        # the same operations as models.py:244-256, created in forward_branched's
+        # order: autograd runs backward nodes by creation order, so the gradients of
+        # multi-consumer activations (x_64, x_128, the masks) are summed in the same
+        # order on one stream and on two -- bit-identical parameter gradients
         x_64, stage_mask = self.SAGB_progress(x_32, [sent, attrs], stage_mask, 64, self.blocks[4], gb[4])
         cum_x_64 = self.cum_64(x_32, x_64)
         img_64 = self.get_image_64(cum_x_64)
         if self.stages == 1:
             return [img_64]
+        u_128 = self.cum_128.up(cum_x_64)
         x_128, stage_mask = self.SAGB_progress(x_64, [sent, attrs], stage_mask, 128, self.blocks[5], gb[5])
-        x_256, _ = self.SAGB_progress(x_128, [sent, attrs], stage_mask, 256, self.blocks[6], gb[6])
-        cum_x_128 = self.cum_128(cum_x_64, x_128)
-        cum_x_256 = self.cum_256(cum_x_128, x_256)
+        cum_x_128 = self.cum_128.fuse(u_128, x_128)
         img_128 = self.get_image_128(cum_x_128)
+        u_256 = self.cum_256.up(cum_x_128)
+        x_256, _ = self.SAGB_progress(x_128, [sent, attrs], stage_mask, 256, self.blocks[6], gb[6])
+        cum_x_256 = self.cum_256.fuse(u_256, x_256)
         img_256 = self.get_image_256(cum_x_256)
         return [img_64, img_128, img_256]
 
@@ -395,6 +403,10 @@ class DiscCond(nn.Module):
 
 
 class _DisBase(nn.Module):
+    def __init__(self):
+        super().__init__()
+        D.guard_state_dict(self)   # a rank whose collectives failed must not checkpoint
+
     def _stem(self, x):
         D.ensure_grad_hooks(self)   # covers COND_DNET, which train.py calls outside forward
         if x.dtype != torch.bfloat16:

@@ -1,18 +1,31 @@
-"""The reference train.py's inner step (train.py:186-206, d_update 437-469,
-g_update 471-502, the loss statics 336-435) written against the DROP-IN
-modules exactly as train.py drives them: Gen wrapped in
-DataParallelWithCallback, ATTR_Enhance and the three discriminators in torch's
-own nn.DataParallel, torch.optim.Adam(betas=(0, 0.9)) (train.py:252-263),
-words_loss / sent_loss from miscc.DAMSM_losses, COND_DNET reached through
-`.module`, and NO call into eegan_hip for synchronisation.
+"""The reference train.py's data + inner step written against the DROP-IN
+modules exactly as train.py drives them, with no mention of ranks:
+
+  * imports first (train.py:22-29), then `CUDA_VISIBLE_DEVICES = --gpu`
+    (train.py:513), then the seeds (train.py:521-525);
+  * `TextDataset` + `torch.utils.data.DataLoader(shuffle=True, drop_last=True)`
+    (train.py:265-280) over a small dataset in the reference's on-disk format,
+    `prepare_data` (train.py:58-88) with `imgs[i].to(device)`;
+  * the networks built from the torch generator in load_networks' order
+    (train.py:208-232): Gen in DataParallelWithCallback, ATTR_Enhance and the
+    three discriminators in torch's own nn.DataParallel; a frozen text encoder
+    (train.py:234-241 loads it from a checkpoint: identical on every rank --
+    here seeded weights); torch.optim.Adam(betas=(0, 0.9)) (train.py:252-263);
+  * the text encodes (train.py:176-188), `torch.randn(batch_size, 100)`
+    (train.py:189), d_update (437-469) and g_update (471-502) with words_loss /
+    sent_loss from miscc.DAMSM_losses and COND_DNET through `.module`.
 
 Run as one process per rank (torchrun; tests/test_gpu_dist.py launches two
-ranks sharing one GPU over gloo) it checks that the drop-in boundary holds at
-N > 1: gradient averaging (GradHooks installed by the models' forward),
-SyncBN statistics over all ranks and global-batch DAMSM.  Imported without a
-process group it is the single-process run of the whole batch.
+ranks sharing one GPU over gloo), the drop-in package alone makes this
+data-parallel: the import pins and joins the ranks (eegan_hip.launch), the
+dataset shards itself and offsets ranks > 0's random streams, the models
+broadcast rank 0's weights at their first forward and average gradients with
+post-accumulate-grad hooks, SyncBN and DAMSM span the ranks.  Each rank saves
+the batch it drew, so the test can step ONE process over the union of the
+ranks' batches (`replay`) and compare.
 """
 import os
+import random
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -21,21 +34,26 @@ for p in (REPO, os.path.join(REPO, 'ee-gan_amd'), HERE):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.nn as nn  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
-B_GLOBAL, W, NCLS = 4, 8, 10
+B_RANK, W, NCLS = 2, 8, 200     # --batch_size (per rank), GF = DF, CLASS_NUM (class_info.pickle holds id 200)
+NETS = ('g', 'a', 'd0', 'd1', 'd2')
 
 
-def build(dev):
+def build(dev, state=None):
+    """load_networks + load_optimizers (train.py:208-263); weights from the
+    torch generator as the reference's constructors draw them, or `state`."""
     import models
     from sync_batchnorm import DataParallelWithCallback
-    from oracle.seeding import seeded_state, state_spec
-    G, A = models.Gen(W, 100), models.ATTR_Enhance()
-    Ds = [models.Dis64(W), models.Dis128(W), models.Dis256(W, True, NCLS)]
-    for i, m in enumerate([G, A] + Ds):
-        m.load_state_dict(seeded_state(state_spec(m.state_dict()), 200 + i))
+    mods = [models.Gen(W, 100), models.ATTR_Enhance(), models.Dis64(W), models.Dis128(W),
+            models.Dis256(W, True, NCLS)]
+    if state is not None:
+        for nm, m in zip(NETS, mods):
+            m.load_state_dict(state[nm])
+    G, A, Ds = mods[0], mods[1], mods[2:]
     netG = DataParallelWithCallback(G.to(dev))
     attr = nn.DataParallel(A.to(dev))
     netsD = [nn.DataParallel(d.to(dev)) for d in Ds]
@@ -44,11 +62,19 @@ def build(dev):
     return netG, attr, netsD, optG, optDs
 
 
-def standin_encoder(dev):
+def encoders(dev, n_words):
+    """The frozen text encoder (seeded: the checkpoint of train.py:236 is the
+    same file on every rank) and a small stand-in image encoder for DAMSM."""
+    import DAMSM
     from eegan_hip import functional as Fn
     from eegan_hip.nn import Conv2d, Linear
-    from oracle.seeding import seeded_state
+    from oracle.seeding import seeded_state, state_spec
     from oracle.eegan_oracle import STANDIN_SPEC
+    text = DAMSM.RNN_ENCODER(n_words, nhidden=256)
+    text.load_state_dict(seeded_state(state_spec(text.state_dict()), 211))
+    text = text.to(dev).eval()
+    for p in text.parameters():
+        p.requires_grad = False
     sd = seeded_state(STANDIN_SPEC, 210)
     rconv = Conv2d(3, 256, 15, 15, 0, bias=False).to(dev)
     rconv.weight.data.copy_(sd['standin.regions.weight'].to(dev))
@@ -58,38 +84,53 @@ def standin_encoder(dev):
     for p in list(rconv.parameters()) + list(clin.parameters()):
         p.requires_grad_(False)
 
-    def enc(x):
+    def image(x):
         r = rconv(x, out_f32=True)
         return r, clin(Fn.GlobalAvgPoolFn.apply(Fn.CastF32Bf16Fn.apply(r)))
-    return enc
+    return text, image
 
 
-def run_step(rank, world, dev):
-    """One iteration on this rank's slice of the global batch; returns the
-    logged losses and every parameter after the step."""
+def prepare_data(data, device):
+    """train.py:58-88."""
+    rev_basic, rev_attrs, rev_unpair = data
+    imgs, caps, cap_lens, cls_ids, keys = rev_basic
+    attrs, attr_nums, attrs_len = rev_attrs
+    unpair_caps, unpair_cap_lens, unpair_cls_ids = rev_unpair
+    real_imgs = [imgs[i].to(device) for i in range(len(imgs))]
+    return {'imgs': real_imgs, 'caps': caps.squeeze().to(device), 'cap_lens': cap_lens.to(device),
+            'cls_ids': cls_ids.numpy(), 'attrs': attrs.squeeze().to(device), 'attrs_len': attrs_len.squeeze(),
+            'unpair_caps': unpair_caps.squeeze().to(device), 'unpair_cap_lens': unpair_cap_lens.to(device),
+            'keys': list(keys)}
+
+
+def encode(text, b, B):
+    """train.py:176-188."""
+    with torch.no_grad():
+        hidden = text.init_hidden(B)
+        words, sent = text(b['caps'], b['cap_lens'], hidden)
+        ae = []
+        for i in range(b['attrs'].shape[1]):
+            _, e = text(b['attrs'][:, i, :].squeeze(-1), b['attrs_len'][:, i].squeeze(-1), hidden)
+            ae.append(e)
+        attrs_emb = torch.stack(ae, dim=1)
+        _, unpair = text(b['unpair_caps'], b['unpair_cap_lens'], hidden)
+    return words.detach(), sent.detach(), attrs_emb.detach(), unpair.detach()
+
+
+def step(nets, image_enc, b, words, sent, attrs_emb, unpair, noise, B, dev):
+    """train.py:186-206 with d_update (437-469) and g_update (471-502);
+    returns the logged losses."""
     from miscc.DAMSM_losses import words_loss, sent_loss
-    from oracle.seeding import synthetic_batch, seeded_tensor
-    netG, attr, netsD, optG, optDs = build(dev)
-    enc = standin_encoder(dev)
-    Bl = B_GLOBAL // world
-    sl = slice(rank * Bl, (rank + 1) * Bl)
-    batch = synthetic_batch(B_GLOBAL, seed=7, class_num=NCLS, sizes=(64, 128, 256))
-    imgs = [t[sl].to(dev) for t in batch['imgs']]
-    noise = batch['noise'][sl].to(dev)
-    words = seeded_tensor('dp:words', (B_GLOBAL, 256, 18), 1)[sl].to(dev)
-    sent = seeded_tensor('dp:sent', (B_GLOBAL, 256), 1)[sl].to(dev)
-    attrs = seeded_tensor('dp:attrs', (B_GLOBAL, 3, 256), 1)[sl].to(dev)
-    unpair = seeded_tensor('dp:unpair', (B_GLOBAL, 256), 1)[sl].to(dev)
-    cap_lens = batch['cap_lens'][sl].to(dev)
-    cls_ids = batch['cls_ids'][sl].numpy()
+    netG, attr, netsD, optG, optDs = nets
+    imgs, cap_lens, cls_ids = b['imgs'], b['cap_lens'], b['cls_ids']
     rec = {}
     # prepare_labels / prepare_class_labels (train.py:90-103)
-    match = torch.arange(Bl, device=dev)
-    cl = torch.zeros(Bl, NCLS, device=dev)
+    match = torch.arange(B, device=dev)
+    cl = torch.zeros(B, NCLS, device=dev)
     for i, idx in enumerate(cls_ids):
         cl[i][int(idx) - 1] = 1
     # train.py:193-195
-    _, att = attr(sent, attrs)
+    _, att = attr(sent, attrs_emb)
     attn_attr = attr.module.attr_merge(att)
     fakes = netG(noise, sent, attn_attr)
     # d_update (train.py:437-469)
@@ -134,43 +175,81 @@ def run_step(rank, world, dev):
             g_loss = g_loss - o[0].mean() + F.binary_cross_entropy_with_logits(o[1], cl) * 10.0
         else:
             g_loss = g_loss - o.mean()
-    regions, code = enc(fakes[-1])
-    s0, s1 = sent_loss(code, sent, match, torch.LongTensor(cls_ids), Bl)
-    w0, w1, _ = words_loss(regions, words, match, cap_lens, torch.LongTensor(cls_ids), Bl)
-    a0, a1 = sent_loss(code, attn_attr, match, torch.LongTensor(cls_ids), Bl)
+    regions, code = image_enc(fakes[-1])
+    cids = torch.LongTensor(np.asarray(cls_ids, dtype=np.int64))
+    s0, s1 = sent_loss(code, sent, match, cids, B)
+    w0, w1, _ = words_loss(regions, words, match, cap_lens, cids, B)
+    a0, a1 = sent_loss(code, attn_attr, match, cids, B)
     g_loss = g_loss + 0.05 * ((s0 + s1) + (w0 + w1) + (a0 + a1))
     optG.zero_grad()
     g_loss.backward()
     optG.step()
     rec.update(s=float(s0 + s1), w=float(w0 + w1), a=float(a0 + a1), g=float(g_loss))
-    params = {}
-    for nm, m in [('g', netG), ('a', attr)] + [('d%d' % i, d) for i, d in enumerate(netsD)]:
-        for k, v in m.module.state_dict().items():
-            params['%s/%s' % (nm, k)] = v.detach().float().cpu().clone()
-    return rec, params
+    return rec
 
 
-def main():
-    """train.py's process shape under torchrun: the drop-in modules are
-    imported first (train.py:22-29), then CUDA_VISIBLE_DEVICES is overwritten
-    with the --gpu argument for every rank alike (train.py:513; here '1', i.e.
-    `--gpu 1`, a device this one-GPU box does not have), then the device is
-    torch.device('cuda') (train.py:114).  No call into torch.distributed or
-    eegan_hip.dist: the import pins this rank's GPU and joins the ranks
-    (eegan_hip.launch)."""
-    import miscc.config  # noqa: F401  (train.py:23-29 import order)
+def states(nets):
+    netG, attr, netsD = nets[:3]
+    out = {}
+    for nm, m in zip(NETS, [netG, attr] + list(netsD)):
+        out[nm] = {k: v.detach().cpu().clone() for k, v in m.module.state_dict().items()}
+    return out
+
+
+def flat_params(st):
+    return {'%s/%s' % (nm, k): v.float() for nm in NETS for k, v in st[nm].items()}
+
+
+def replay(records, dev, n_words):
+    """ONE process stepping the union of the ranks' batches (rank order), from
+    rank 0's initial weights: the reference's single-process DataParallel
+    step over the whole batch."""
+    nets = build(dev, records[0]['init'])
+    text, image = encoders(dev, n_words)
+    cat = lambda k: torch.cat([r['batch'][k] for r in records], 0)  # noqa: E731
+    b = {'imgs': [torch.cat([r['batch']['imgs'][s] for r in records], 0).to(dev) for s in range(3)],
+         'caps': cat('caps').to(dev), 'cap_lens': cat('cap_lens').to(dev),
+         'cls_ids': cat('cls_ids').numpy(),
+         'attrs': cat('attrs').to(dev), 'attrs_len': cat('attrs_len'),
+         'unpair_caps': cat('unpair_caps').to(dev), 'unpair_cap_lens': cat('unpair_cap_lens').to(dev)}
+    B = len(b['cls_ids'])
+    words, sent, attrs_emb, unpair = encode(text, b, B)
+    rec = step(nets, image, b, words, sent, attrs_emb, unpair, cat('noise').to(dev), B, dev)
+    return rec, flat_params(states(nets))
+
+
+def main(data_dir, out):
+    """train.py's process shape under torchrun, in train.py's order."""
+    import miscc.config  # noqa: F401  (train.py:22-29 import order)
     import miscc.DAMSM_losses  # noqa: F401
     import sync_batchnorm  # noqa: F401
+    from datasets import TextDataset
     import models  # noqa: F401
     import DAMSM  # noqa: F401
-    os.environ['CUDA_VISIBLE_DEVICES'] = os.environ.get('DP_GPU_IDS', '1')   # train.py:513
-    rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
-    dev = torch.device('cuda')
-    rec, params = run_step(rank, world, dev)
+    os.environ['CUDA_VISIBLE_DEVICES'] = os.environ.get('DP_GPU_IDS', '1')   # train.py:513 (`--gpu 1`)
+    random.seed(3407)                                                       # train.py:521-525
+    np.random.seed(3407)
+    torch.manual_seed(3407)
+    dev = torch.device('cuda')                                              # train.py:114
+    ds = TextDataset(data_dir=data_dir, dataset_name='bird', transform=None)
+    loader = torch.utils.data.DataLoader(ds, batch_size=B_RANK, drop_last=True, shuffle=True, num_workers=0)
+    nets = build(dev)
+    init = states(nets)
+    text, image = encoders(dev, ds.n_words)
+    b = prepare_data(next(iter(loader)), dev)
+    words, sent, attrs_emb, unpair = encode(text, b, B_RANK)
+    noise = torch.randn(B_RANK, 100)                                        # train.py:189
+    batch = {'imgs': [t.cpu() for t in b['imgs']], 'noise': noise.clone(), 'keys': b['keys'],
+             'cls_ids': torch.as_tensor(np.asarray(b['cls_ids'], dtype=np.int64)), 'attrs_len': b['attrs_len'].clone()}
+    for k in ('caps', 'cap_lens', 'attrs', 'unpair_caps', 'unpair_cap_lens'):
+        batch[k] = b[k].cpu()
+    rec = step(nets, image, b, words, sent, attrs_emb, unpair, noise.to(dev), B_RANK, dev)
     info = {'device_count': torch.cuda.device_count(), 'rocr': os.environ.get('ROCR_VISIBLE_DEVICES'),
-            'hip': os.environ.get('HIP_VISIBLE_DEVICES')}
-    torch.save({'rec': rec, 'params': params, 'info': info}, os.path.join(sys.argv[1], 'rank%d.pt' % rank))
+            'hip': os.environ.get('HIP_VISIBLE_DEVICES'), 'len': len(ds), 'n_words': ds.n_words,
+            'base': [ds.base_index(i) for i in range(len(ds))]}
+    torch.save({'rec': rec, 'params': flat_params(states(nets)), 'init': init, 'batch': batch, 'info': info},
+               os.path.join(out, 'rank%s.pt' % os.environ['RANK']))
 
 
 if __name__ == '__main__':
-    main()
+    main(sys.argv[1], sys.argv[2])

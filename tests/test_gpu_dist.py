@@ -1,8 +1,10 @@
 """The drop-in boundary at N > 1 on one GPU box: two ranks (torchrun, gloo --
-RCCL refuses two ranks on one device) run the reference train.py's inner step
-(tests/dp_dropin_worker.py: torch.optim.Adam, nn.DataParallel-wrapped D and
-ATTR_Enhance, words_loss / sent_loss from miscc.DAMSM_losses, no explicit
-synchronisation call) on halves of one batch.  Checked: the ranks end the
+RCCL refuses two ranks on one device) run the reference train.py's data side and inner
+step (tests/dp_dropin_worker.py: TextDataset + DataLoader(shuffle=True) after
+train.py's seeding, torch.optim.Adam, nn.DataParallel-wrapped D and
+ATTR_Enhance, words_loss / sent_loss from miscc.DAMSM_losses, no rank and no
+synchronisation call anywhere).  Checked: each rank draws its own images and
+noise; the ranks end the
 step with bit-identical parameters (gradient averaging by the models' own
 post-accumulate-grad hooks), and they match ONE process stepping the whole
 batch (the reference's DataParallel semantics: global-batch SyncBN
@@ -28,9 +30,19 @@ def _free_port():
 
 
 def test_dropin_train_step_two_ranks(gpu, tmp_path, monkeypatch):
+    """Two ranks of train.py's data + inner step (tests/dp_dropin_worker.py:
+    no rank, no slicing, no synchronisation call anywhere in it).  Each rank
+    must draw its OWN images (disjoint stride-2 shards of the split), noise
+    and initial weights from its own random streams, start from rank 0's
+    weights (broadcast at the first forward), end bit-identical to the other
+    rank, and match ONE process stepping the union of the two batches."""
+    sys.path.insert(0, HERE)
+    import _pipeline_data as PD
+    data = tmp_path / 'data'
+    PD.build(str(data))
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
            '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
-           os.path.join(HERE, 'dp_dropin_worker.py'), str(tmp_path)]
+           os.path.join(HERE, 'dp_dropin_worker.py'), str(data), str(tmp_path)]
     # the worker never calls torch.distributed / eegan_hip.dist: importing the drop-in
     # modules under torchrun pins each rank's GPU and starts the group (eegan_hip.launch);
     # gloo because both ranks share this box's one GPU (RCCL refuses that)
@@ -39,12 +51,20 @@ def test_dropin_train_step_two_ranks(gpu, tmp_path, monkeypatch):
     r = subprocess.run(cmd, env=env, timeout=240, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     ranks = [torch.load(os.path.join(tmp_path, 'rank%d.pt' % i)) for i in range(2)]
-    for rk in ranks:   # train.py:513's CUDA_VISIBLE_DEVICES=1 did not unpin the rank's device
-        print('DP2 rank device pin', rk['info'])
+    for i, rk in enumerate(ranks):   # train.py:513's CUDA_VISIBLE_DEVICES=1 did not unpin the rank's device
+        print('DP2 rank', i, 'device pin', rk['info'], 'keys', rk['batch']['keys'])
         assert rk['info']['device_count'] == 1 and rk['info']['hip'] == '0', rk['info']
+        assert rk['info']['len'] == len(PD.SIZES) // 2
+        assert rk['info']['base'] == list(range(i, len(PD.SIZES), 2))   # the rank's stride-2 shard
+        assert all(int(k[3:]) % 2 == i for k in rk['batch']['keys'])
+    b0, b1 = ranks[0]['batch'], ranks[1]['batch']
+    assert not set(b0['keys']) & set(b1['keys'])                       # disjoint images
+    assert not torch.equal(b0['noise'], b1['noise'])                   # train.py:189 differs per rank
+    g0, g1 = ranks[0]['init']['g'], ranks[1]['init']['g']
+    assert any(not torch.equal(g0[k], g1[k]) for k in g0)              # built from the offset streams
     p0, p1 = ranks[0]['params'], ranks[1]['params']
     assert set(p0) == set(p1)
-    for k in p0:   # averaged gradients -> identical Adam steps on every rank
+    for k in p0:   # rank 0's weights broadcast, averaged gradients -> identical Adam steps
         assert torch.equal(p0[k], p1[k]), k
     # DAMSM losses are global: the same value on both ranks
     for k in ('s', 'w', 'a'):
@@ -53,7 +73,7 @@ def test_dropin_train_step_two_ranks(gpu, tmp_path, monkeypatch):
     import dp_dropin_worker as W
     from eegan_hip import functional as Fn
     monkeypatch.setattr(Fn, 'SYNC_BN_FORCE_MULTI', True)   # the reference's multi-device BN numerics
-    rec, params = W.run_step(0, 1, gpu)
+    rec, params = W.replay(ranks, gpu, ranks[0]['info']['n_words'])
     for k, v in rec.items():
         got = 0.5 * (ranks[0]['rec'][k] + ranks[1]['rec'][k])   # per-rank means over equal halves
         e = abs(got - v) / max(abs(v), 1e-3)

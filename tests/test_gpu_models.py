@@ -306,9 +306,12 @@ def test_syncbn_multi_device_formula(gpu, monkeypatch, affine):
 # stay within max |d| <= 2e-2, mean <= 5e-3 of the fp32 reference on images).  The
 # HIP path holds activations AND conv weights in bf16; the survey measured
 # all-bf16 (weights + activations) at max 4.2e-2 from fp64.  So the gate is the
-# survey's 2e-2 or, where bf16 storage alone moves the images further, 1.5 x
+# survey's 2e-2 or, where bf16 storage alone moves the images further, 1.2 x
 # the fp32 oracle's own max |d| with every conv input / output and weight
 # rounded to bf16 (oracle.SIM_BF16 + rounded weights) -- the bound is logged.
+# Measured (profiles/r04_parity_log.txt): GPU / simulation = 2.59e-2 / 2.42e-2,
+# 4.06e-2 / 3.89e-2, 3.51e-2 / 3.87e-2 (ratios 1.07, 1.04, 0.91).
+TOL_IMG_SIM = 1.2
 TOL_IMG_MAX, TOL_IMG_MEAN = 2e-2, 5e-3
 
 
@@ -332,7 +335,7 @@ def _image_maxabs_gate(imgs, z, s, a, W=8):
     for k, (im, r, sm) in enumerate(zip(imgs, ref, sim)):
         d = (im.float().cpu() - r).abs()
         ds = (sm - r).abs()
-        bound = max(TOL_IMG_MAX, 1.5 * float(ds.max()))
+        bound = max(TOL_IMG_MAX, TOL_IMG_SIM * float(ds.max()))
         _LOG.append(('gen/img%d max|d|' % k, float(d.max())))
         _LOG.append(('gen/img%d mean|d|' % k, float(d.mean())))
         _LOG.append(('gen/img%d max|d| of the bf16 simulation' % k, float(ds.max())))
@@ -380,10 +383,11 @@ def test_generator(gpu):
 def test_generator_branched_matches_single_stream(gpu):
     """Gen.forward_branched (stage 2-3 Cum_Block / image branches on a second
     stream, the trainer's GEN_SIDE) runs the same operations on the same inputs
-    as the single-stream forward: images bit-identical; the backward sums the
-    gradients of multi-consumer activations in another order (bf16 rounding)."""
+    as the single-stream forward, created in the same order: images AND every
+    gradient bit-identical (autograd orders the backward by node creation, so
+    the multi-consumer sums -- x_64, x_128, the masks -- add in the same order
+    whichever stream a node ran on)."""
     import models
-    from _util import rel_l2
     G = _load(models.Gen(8, 100), 'gen', 21, gpu)
     z = seeded_tensor('g:z', (2, 100), 1).to(gpu)
     side = torch.cuda.Stream()
@@ -404,13 +408,9 @@ def test_generator_branched_matches_single_stream(gpu):
     for x, y in zip(i0, i1):
         assert torch.equal(x, y)
     assert set(g0) == set(g1)
-    assert rel_l2(s1, s0) < 2e-2 and rel_l2(a1, a0) < 2e-2
-    # per parameter within TOL_BWD (a bias gradient is a sum with heavy
-    # cancellation: 2.0e-2 measured on blocks.0.conv_mask), typically ~1e-3
-    errs = {n: rel_l2(g1[n], g0[n]) for n in g0}
-    for n, e in errs.items():
-        assert e < TOL_BWD, (n, e)
-    assert float(np.median(list(errs.values()))) < 1e-2
+    assert torch.equal(s1, s0) and torch.equal(a1, a0)
+    diff = [n for n in g0 if not torch.equal(g1[n], g0[n])]
+    assert not diff, diff
 
 
 def test_generator_grouped_mlps_match_per_layer(gpu, monkeypatch):
@@ -746,8 +746,12 @@ def test_cnn_encoder_stages(gpu):
 # other way, and that step is a large part of those quantities (the update
 # moves the penalty by 4-73% on these fixtures).  They are gated in units of
 # the update's own effect U = ref - (the quantity at D's initial weights,
-# fp32 oracle): |got - ref| <= TOL_STEP_LOSS |ref| + TOL_STEP_UPDATE |U|
-# (measured up to 0.34 |U| on the GPU, 0.13 |U| in the bf16 simulation).
+# fp32 oracle): |got - ref| <= TOL_STEP_LOSS |ref| + TOL_STEP_UPDATE |U|.
+# Measured on the GPU up to 0.438 |U| (step/errD_2/d_loss_gp,
+# profiles/r04_parity_log.txt; the other post-update terms <= 0.03 |U|); the
+# fp32 oracle with bf16 activations AND bf16 conv weights lands at 0.30-0.39 |U|
+# on the same term (tools/gp_sim_parity.py), so the gate
+# keeps a 0.06 |U| margin over the measurement.
 TOL_STEP_LOSS = 3e-2
 TOL_STEP_UPDATE = 0.5
 # Adam's first steps move each weight by ~lr * sign(grad), so post-step

@@ -94,3 +94,27 @@ def test_peer_timeout_raises_on_trainer_path(monkeypatch):
     T = Trainer.__new__(Trainer)
     with pytest.raises(RuntimeError, match='timed out'):
         T.state_dict()
+
+
+def test_peer_timeout_blocks_dropin_checkpoint(monkeypatch):
+    """Under an unchanged train.py (its own loop, train.py:310-318 saving
+    netG / attr_enhance / netsD state_dicts directly), a timed-out SyncBN peer
+    reduction must stop the checkpoint: every drop-in model's state_dict --
+    also through DataParallelWithCallback / nn.DataParallel -- checks first."""
+    import torch.nn as nn
+    import models
+    from sync_batchnorm import DataParallelWithCallback
+    from eegan_hip import functional as Fn
+    from eegan_hip.peer import PeerAllReduce
+    red = PeerAllReduce.__new__(PeerAllReduce)
+    red.regions = {}
+    monkeypatch.setattr(Fn, 'SYNC_BN_ALLREDUCE', red)
+    monkeypatch.setattr(PeerAllReduce, 'timed_out', lambda self: 0)
+    nets = [DataParallelWithCallback(models.Gen(8, 100)), nn.DataParallel(models.ATTR_Enhance()),
+            nn.DataParallel(models.Dis64(8)), models.Dis256(8, True, 200)]
+    for n in nets:
+        n.state_dict()    # healthy: no error
+    monkeypatch.setattr(PeerAllReduce, 'timed_out', lambda self: 1 + 1)
+    for n in nets:
+        with pytest.raises(RuntimeError, match='timed out waiting for rank 1'):
+            n.state_dict()
