@@ -158,75 +158,109 @@ struct ModArgs {
   const float* mask;    // [N][Ho*Wo]
   int act;
   float slope;
+  int wsh;              // log2 of the output width when it is a power of two, else -1
+  float nslope;         // the activation's slope below 0: 1 (none), 0 (relu), slope (lrelu)
 };
 
 // Blocks cover (pixel chunk, sample); a thread owns 8 consecutive channels
 // (one 16-byte NHWC load) for every pixel it visits, so the per-channel
-// statistics / modulation parameters of its sample stay in registers.
+// statistics / modulation parameters of its sample stay in registers.  The
+// arithmetic runs on channel pairs (float2: packed v_pk_* fp32 instructions,
+// half the VALU issue of scalar code), pixel coordinates by shifts when the
+// output width is a power of two (no integer division per pixel), offsets in
+// 32 bits (host-checked).
+typedef float f2_t __attribute__((ext_vector_type(2)));
+
 struct ChanParams {
-  float mean[8], istd[8], pm[8], pa[8];  // mode 0: w, b ; mode 1: gam[n], bet[n]
+  f2_t mean[4], istd[4], pm[4], pa[4];  // mode 0: w, b ; mode 1: gam[n], bet[n]
 };
+
+EE_DEV f2_t splat2(float v) { return f2_t{v, v}; }
 
 EE_DEV void load_params(const ModArgs& a, int n, int c0, ChanParams& q, const FinArgs* fin = nullptr) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = min(c0 + j, a.C - 1);
+    float mean, istd, pm, pa;
     if (fin) {   // statistics straight from the sums (the forward's fused finalize)
-      bn_finalize_channel(*fin, a.C, c, q.mean[j], q.istd[j], false);
+      bn_finalize_channel(*fin, a.C, c, mean, istd, false);
     } else {
-      q.mean[j] = a.stats[c];
-      q.istd[j] = a.stats[a.C + c];
+      mean = a.stats[c];
+      istd = a.stats[a.C + c];
     }
     if (a.mode == 0) {
-      q.pm[j] = a.w ? a.w[c] : 1.f;
-      q.pa[j] = a.b ? a.b[c] : 0.f;
+      pm = a.w ? a.w[c] : 1.f;
+      pa = a.b ? a.b[c] : 0.f;
     } else {
-      q.pm[j] = a.gam[(long)n * a.C + c];
-      q.pa[j] = a.bet[(long)n * a.C + c];
+      pm = a.gam[(long)n * a.C + c];
+      pa = a.bet[(long)n * a.C + c];
     }
+    q.mean[j >> 1][j & 1] = mean;
+    q.istd[j >> 1][j & 1] = istd;
+    q.pm[j >> 1][j & 1] = pm;
+    q.pa[j >> 1][j & 1] = pa;
   }
 }
 
-// t = act(xhat * mul + add)
-EE_DEV void coeffs(const ModArgs& a, const ChanParams& q, int j, float m, float& mul, float& add) {
-  if (a.mode == 0) {
-    mul = q.pm[j];
-    add = q.pa[j];
-  } else {
-    mul = q.pm[j] * m + 1.f;
-    add = q.pa[j] * m;
-  }
-}
-
-EE_DEV void unpack8(uint4 v, float (&f)[8]) {
+EE_DEV void unpack8(uint4 v, f2_t (&f)[4]) {
   const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    f[2 * j] = lo_f(w4[j]);
-    f[2 * j + 1] = hi_f(w4[j]);
-  }
+  for (int j = 0; j < 4; ++j) f[j] = f2_t{lo_f(w4[j]), hi_f(w4[j])};
 }
 
-EE_DEV void store8(bf16_t* dst, const float (&o)[8], int nvalid) {
+// zero the channels >= nv of a padded row's last chunk (padding may hold anything)
+EE_DEV void clip8(f2_t (&f)[4], int nv) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (j >= nv) f[j >> 1][j & 1] = 0.f;
+}
+
+// act(v) for none / relu / lrelu: v > 0 ? v : v * nslope
+EE_DEV f2_t act2(f2_t v, float ns) {
+  const f2_t vs = v * splat2(ns);
+  return f2_t{v.x > 0.f ? v.x : vs.x, v.y > 0.f ? v.y : vs.y};
+}
+// g * act'(t)
+EE_DEV f2_t gact2(f2_t g, f2_t t, float ns) {
+  const f2_t gs = g * splat2(ns);
+  return f2_t{t.x > 0.f ? g.x : gs.x, t.y > 0.f ? g.y : gs.y};
+}
+
+EE_DEV void store8(bf16_t* dst, const f2_t (&o)[4], int nvalid) {
   if (nvalid >= 8) {
-    *reinterpret_cast<uint4*>(dst) = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+    *reinterpret_cast<uint4*>(dst) =
+        make_uint4(pack2(o[0].x, o[0].y), pack2(o[1].x, o[1].y), pack2(o[2].x, o[2].y), pack2(o[3].x, o[3].y));
   } else {
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      if (j < nvalid) dst[j] = f2bf(o[j]);
+      if (j < nvalid) dst[j] = f2bf(o[j >> 1][j & 1]);
   }
+}
+
+// input-grid pixel (relative to the sample) of output pixel q
+EE_DEV int in_pix(const ModArgs& a, int q, int Wo) {
+  if (!a.up2) return q;
+  int oy, ox;
+  if (a.wsh >= 0) {
+    oy = q >> a.wsh;
+    ox = q & (Wo - 1);
+  } else {
+    oy = (unsigned)q / (unsigned)Wo;
+    ox = q - oy * Wo;
+  }
+  return (oy >> 1) * a.W + (ox >> 1);
 }
 
 // grid (chunks, N): output pixels [chunk*ppc, ...) of sample n.  FUNR pixels
 // per thread per iteration: their loads are all issued before any arithmetic
 // (a single 16-byte load per iteration left these kernels latency-bound).
-constexpr int FUNR = 4;
+constexpr int FUNR = 2;
 
 // FIN: the statistics come from the sums (the finalize kernel folded in: every block
 // recomputes its channels' mean / inv_std, block (0, 0) also writes stats[] and the
 // running statistics -- one launch less per BN call on the generator's serial chain)
 template <bool FIN>
-__global__ __launch_bounds__(NT) void bnmod_fwd_kernel(ModArgs a, bf16_t* __restrict__ y, int ldy, int ppc,
+__global__ __launch_bounds__(NT, 6) void bnmod_fwd_kernel(ModArgs a, bf16_t* __restrict__ y, int ldy, int ppc,
                                                        FinArgs fin) {
   if (FIN && blockIdx.x == 0 && blockIdx.y == 0) {
     for (int c = threadIdx.x; c < a.C; c += NT) {
@@ -243,6 +277,10 @@ __global__ __launch_bounds__(NT) void bnmod_fwd_kernel(ModArgs a, bf16_t* __rest
   const int q1 = min(HWo, ((int)blockIdx.x + 1) * ppc);
   ChanParams P;
   load_params(a, n, c0, P, FIN ? &fin : nullptr);
+  const bf16_t* xs = a.x + (unsigned)(n * a.H * a.W) * (unsigned)a.ldx + c0;
+  bf16_t* ys = y + (unsigned)(n * HWo) * (unsigned)ldy + c0;
+  const float* ms = a.mask + (long)n * HWo;
+  const float ns = a.nslope;
   for (int qb = (int)blockIdx.x * ppc + row; qb < q1; qb += FUNR * rows) {
     uint4 xr[FUNR];
     float mr[FUNR];
@@ -250,39 +288,61 @@ __global__ __launch_bounds__(NT) void bnmod_fwd_kernel(ModArgs a, bf16_t* __rest
     for (int u = 0; u < FUNR; ++u) {
       const int q = qb + u * rows;
       if (q < q1) {
-        const int oy = (unsigned)q / (unsigned)Wo, ox = q - oy * Wo;
-        const long ip = ((long)n * a.H + (oy >> a.up2)) * a.W + (ox >> a.up2);
-        xr[u] = *reinterpret_cast<const uint4*>(a.x + ip * a.ldx + c0);
-        mr[u] = a.mode == 1 ? a.mask[(long)n * HWo + q] : 0.f;
+        xr[u] = *reinterpret_cast<const uint4*>(xs + (unsigned)in_pix(a, q, Wo) * (unsigned)a.ldx);
+        mr[u] = a.mode == 1 ? ms[q] : 0.f;
       }
     }
 #pragma unroll
     for (int u = 0; u < FUNR; ++u) {
       const int q = qb + u * rows;
       if (q >= q1) break;
-      float xv[8], o[8];
+      f2_t xv[4], o[4];
       unpack8(xr[u], xv);
+      const f2_t m2 = splat2(mr[u]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float mul, add;
-        coeffs(a, P, j, mr[u], mul, add);
-        o[j] = act_fwd((xv[j] - P.mean[j]) * P.istd[j] * mul + add, a.act, a.slope);
+      for (int k = 0; k < 4; ++k) {
+        const f2_t xh = (xv[k] - P.mean[k]) * P.istd[k];
+        const f2_t mul = a.mode == 1 ? P.pm[k] * m2 + splat2(1.f) : P.pm[k];
+        const f2_t add = a.mode == 1 ? P.pa[k] * m2 : P.pa[k];
+        o[k] = act2(xh * mul + add, ns);
       }
-      store8(y + ((long)n * HWo + q) * ldy + c0, o, nv);
+      store8(ys + (unsigned)q * (unsigned)ldy, o, nv);
     }
   }
 }
 
 // ------------------------------------------------------ backward, pass 1 --
-// RU pixels' loads per thread are issued before their arithmetic (2 left the
-// reduce at ~3 TB/s on the generator's 128^2 / 256^2 layers)
-constexpr int RU = 4;
+constexpr int RU = 2;
+
+// sum of v over the C8 consecutive lanes that hold one pixel's channel groups
+// (C8 a power of two <= 64; every lane of the group gets the same bits, summed
+// in the butterfly order xor 1, 2, 4, ...): DPP within 16-lane rows, no LDS trips
+template <int CTRL>
+EE_DEV float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+EE_DEV float group_sum(float v, int c8) {
+  if (c8 >= 2) v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]: lane ^ 1
+  if (c8 >= 4) v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]: lane ^ 2
+  if (c8 >= 8) v += dpp_f<0x141>(v);   // row_half_mirror: the other quad of 8
+  if (c8 >= 16) v += dpp_f<0x140>(v);  // row_mirror: the other half-row
+  if (c8 >= 32) v += __shfl_xor(v, 16);
+  if (c8 >= 64) v += __shfl_xor(v, 32);
+  return v;
+}
 
 // grid: (chunks, N). Each block reduces a pixel range of ONE sample into
 // ws[n][chunk][4][C]:  S0 = sum g*m*xhat, S1 = sum g*m (ssa: dgamma/dbeta
-// partials; affine: sum g*xhat / sum g), S2 = sum dxhat, S3 = sum dxhat*xhat.
+// partials; affine: sum g*xhat / sum g), S2 = sum dxhat, S3 = sum dxhat*xhat,
+// with g the gradient behind the activation and dxhat = g * mul.
 // dmask[n][pix] = sum_c g*(gam*xhat + bet)  (ssa only).
-__global__ __launch_bounds__(NT) void bnmod_bwd_reduce_kernel(ModArgs a, const bf16_t* __restrict__ dt, int lddt,
+// The loop accumulates A = sum g*m*xhat, B = sum g*m, G = sum g, D = sum g*xhat
+// (ssa; affine: D and G only) and the block's tail forms, with its sample's
+// per-channel pm (ssa: gam[n], affine: w): S2 = pm*B + G, S3 = pm*A + D
+// (affine: S0 = D, S1 = G, S2 = pm*G, S3 = pm*D) -- dxhat = g*(pm*m + 1).
+// RU pixels' loads per thread are issued before their arithmetic; at <= 128
+// VGPRs four blocks fit a CU, so the ~1024-block grid runs in one round.
+__global__ __launch_bounds__(NT, 4) void bnmod_bwd_reduce_kernel(ModArgs a, const bf16_t* __restrict__ dt, int lddt,
                                                               int pix_per_chunk, float* __restrict__ ws,
                                                               float* __restrict__ dmask) {
   extern __shared__ float sh[];
@@ -296,72 +356,75 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_reduce_kernel(ModArgs a, const b
   const int HWo = Ho * Wo;  // per-sample pixel counts fit 32 bits
   const int q0 = (int)blockIdx.x * pix_per_chunk;
   const int q1 = min(HWo, q0 + pix_per_chunk);
-  float acc[4][8];
+  const bool ssa = a.mode == 1;
+  f2_t acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
-  const int c0 = cg * 8;
+    for (int k = 0; k < 4; ++k) acc[i][k] = splat2(0.f);
+  const int c0 = cg * 8, nv = C - c0;
   float* red = sh;                 // [rows][C8] for dmask
   ChanParams P;
-  if (row < rows) load_params(a, n, c0, P);
+  const bool live = row < rows;
+  if (live) load_params(a, n, c0, P);
   // a pixel's C8 channel groups are C8 consecutive lanes of one wave when C8 is a
-  // power of two <= 64: its dmask is then a shuffle reduction (no LDS, no barriers)
+  // power of two <= 64: its dmask is then a DPP / shuffle reduction (no barriers)
   const bool wave_red = (C8 & (C8 - 1)) == 0 && C8 <= 64;
+  const bf16_t* xs = a.x + (unsigned)(n * a.H * a.W) * (unsigned)a.ldx + c0;
+  const bf16_t* gs = dt + (unsigned)(n * HWo) * (unsigned)lddt + c0;
+  const float* ms = a.mask + (long)n * HWo;
+  const float ns = a.nslope;
   // base of the pixel loop must be block-uniform for the dmask reduction
   for (int qb = q0; qb < q1; qb += RU * rows) {
-    uint4 xr[RU], gr[RU];
-    float mr[RU];
+    uint4 xc[RU], gc[RU];
+    float mc[RU];
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int q = qb + u * rows + row;
-      if (row < rows && q < q1) {
-        const int oy = (unsigned)q / (unsigned)Wo, ox = q - oy * Wo;
-        const long ip = ((long)n * a.H + (oy >> a.up2)) * a.W + (ox >> a.up2);
-        const long op = (long)n * HWo + q;
-        xr[u] = *reinterpret_cast<const uint4*>(a.x + ip * a.ldx + c0);
-        gr[u] = *reinterpret_cast<const uint4*>(dt + op * lddt + c0);
-        mr[u] = a.mode == 1 ? a.mask[op] : 0.f;
+      if (live && q < q1) {
+        xc[u] = *reinterpret_cast<const uint4*>(xs + (unsigned)in_pix(a, q, Wo) * (unsigned)a.ldx);
+        gc[u] = *reinterpret_cast<const uint4*>(gs + (unsigned)q * (unsigned)lddt);
+        mc[u] = ssa ? ms[q] : 0.f;
       }
     }
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int q = qb + u * rows + row;
-      float dm = 0.f;
-      if (row < rows && q < q1) {
-        const float m = mr[u];
-        float xv[8], gv[8];
-        unpack8(xr[u], xv);
-        unpack8(gr[u], gv);
+      f2_t dm2 = splat2(0.f);
+      if (live && q < q1) {
+        f2_t xv[4], gv[4];
+        unpack8(xc[u], xv);
+        unpack8(gc[u], gv);
+        if (nv < 8) {
+          clip8(xv, nv);
+          clip8(gv, nv);
+        }
+        const f2_t m2 = splat2(mc[u]);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const bool ok = c0 + j < C;  // channel padding may hold anything
-          const float xh = ok ? (xv[j] - P.mean[j]) * P.istd[j] : 0.f;
-          float mul, add;
-          coeffs(a, P, j, m, mul, add);
-          const float tv = xh * mul + add;
-          float g = ok ? gv[j] : 0.f;
-          if (a.act == ACT_RELU) g = tv > 0.f ? g : 0.f;
-          else if (a.act == ACT_LRELU) g = tv > 0.f ? g : g * a.slope;
-          const float dxh = g * mul;
-          if (a.mode == 1) {
-            acc[0][j] += g * m * xh;
-            acc[1][j] += g * m;
-            dm += g * (P.pm[j] * xh + P.pa[j]);
-          } else {
-            acc[0][j] += g * xh;
-            acc[1][j] += g;
+        for (int k = 0; k < 4; ++k) {
+          const f2_t xh = (xv[k] - P.mean[k]) * P.istd[k];
+          const f2_t mul = ssa ? P.pm[k] * m2 + splat2(1.f) : P.pm[k];
+          const f2_t add = ssa ? P.pa[k] * m2 : P.pa[k];
+          const f2_t g = gact2(gv[k], xh * mul + add, ns);
+          const f2_t gx = g * xh;
+          if (ssa) {
+            const f2_t gm = g * m2;
+            acc[0][k] += gm * xh;
+            acc[1][k] += gm;
+            dm2 += P.pm[k] * gx;
+            dm2 += P.pa[k] * g;
           }
-          acc[2][j] += dxh;
-          acc[3][j] += dxh * xh;
+          acc[2][k] += g;
+          acc[3][k] += gx;
         }
       }
-      if (a.mode == 1 && dmask) {
+      if (ssa && dmask) {
+        float dm = dm2.x + dm2.y;
         if (wave_red) {
-          for (int off = 1; off < C8; off <<= 1) dm += __shfl_xor(dm, off);
-          if (cg == 0 && row < rows && q < q1) dmask[(long)n * HWo + q] = dm;
+          dm = group_sum(dm, C8);
+          if (cg == 0 && live && q < q1) dmask[(long)n * HWo + q] = dm;
         } else {
-          if (row < rows) red[row * C8 + cg] = dm;
+          if (live) red[row * C8 + cg] = dm;
           __syncthreads();
           const int qt = qb + u * rows + t;
           if (t < rows && qt < q1) {
@@ -376,23 +439,34 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_reduce_kernel(ModArgs a, const b
   }
   // reduce acc over rows -> ws: every row's partials through LDS (a row stride of
   // 4 * W8 + 1 floats spreads a wave's rows over the banks), then one thread per
-  // output sums the rows in order.  (Reducing a wave's rows by shuffles first took
-  // 4 x 32 lane exchanges per thread at C = 32.)
+  // output sums the rows in order and forms S0..S3.
   float* sacc = sh + rows * C8;  // [rows][4 * W8 + 1]
   const int W8 = C8 * 8, RS = 4 * W8 + 1;
-  if (row < rows) {
+  if (live) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sacc[row * RS + i * W8 + c0 + j] = acc[i][j];
+      for (int j = 0; j < 8; ++j) sacc[row * RS + i * W8 + c0 + j] = acc[i][j >> 1][j & 1];
   }
   __syncthreads();
   float* out = ws + ((long)n * gridDim.x + blockIdx.x) * 4 * C;
-  for (int e = t; e < 4 * C; e += NT) {
-    const int i = e / C, c = e - i * C;
-    float s = 0.f;
-    for (int r = 0; r < rows; ++r) s += sacc[r * RS + i * W8 + c];
-    out[e] = s;
+  for (int c = t; c < C; c += NT) {
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < rows; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s[i] += sacc[r * RS + i * W8 + c];
+    const float pm = ssa ? a.gam[(long)n * C + c] : (a.w ? a.w[c] : 1.f);
+    if (ssa) {
+      out[c] = s[0];
+      out[C + c] = s[1];
+      out[2 * C + c] = fmaf(pm, s[1], s[2]);
+      out[3 * C + c] = fmaf(pm, s[0], s[3]);
+    } else {
+      out[c] = s[3];
+      out[C + c] = s[2];
+      out[2 * C + c] = pm * s[2];
+      out[3 * C + c] = pm * s[3];
+    }
   }
 }
 
@@ -427,10 +501,17 @@ __global__ void bnmod_bwd_sums_kernel(const double* __restrict__ tmp, int N, int
 // DXU input pixels x NCH (1, or the 4 upsampled) output children per iteration, loads first
 template <int DXU, int NCH>
 EE_DEV void bwd_dx_body(const ModArgs& a, const bf16_t* __restrict__ dt, int lddt, bf16_t* __restrict__ dx, int lddx,
-                        int ppc, const ChanParams& P, const float (&vg)[8], const float (&m1)[8], const float (&m2)[8],
+                        int ppc, const ChanParams& P, const f2_t (&vg)[4], const f2_t (&m1)[4], const f2_t (&m2)[4],
                         int n, int c0, int nv, int row, int rows, int q1) {
-  const int Ho = a.H << a.up2, Wo = a.W << a.up2;
+  const int Wo = a.W << a.up2;
   const int HW = a.H * a.W;
+  const int wish = a.wsh >= 0 ? a.wsh - a.up2 : -1;   // log2 of the input width
+  const bf16_t* xs = a.x + (unsigned)(n * HW) * (unsigned)a.ldx + c0;
+  const bf16_t* gs = dt + (unsigned)(n * (HW << (2 * a.up2))) * (unsigned)lddt + c0;
+  const float* ms = a.mask + (long)n * (HW << (2 * a.up2));
+  bf16_t* ds = dx + (unsigned)(n * HW) * (unsigned)lddx + c0;
+  const float ns = a.nslope;
+  const bool ssa = a.mode == 1;
   for (int qb = (int)blockIdx.x * ppc + row; qb < q1; qb += DXU * rows) {
     uint4 xr[DXU], gr[DXU][NCH];
     float mr[DXU][NCH];
@@ -438,16 +519,22 @@ EE_DEV void bwd_dx_body(const ModArgs& a, const bf16_t* __restrict__ dt, int ldd
     for (int u = 0; u < DXU; ++u) {
       const int q = qb + u * rows;
       if (q < q1) {
-        const int iy = (unsigned)q / (unsigned)a.W, ix = q - iy * a.W;
-        xr[u] = *reinterpret_cast<const uint4*>(a.x + ((long)n * HW + q) * a.ldx + c0);
+        xr[u] = *reinterpret_cast<const uint4*>(xs + (unsigned)q * (unsigned)a.ldx);
+        int iy = 0, ix = q;
+        if (NCH > 1) {
+          if (wish >= 0) {
+            iy = q >> wish;
+            ix = q & (a.W - 1);
+          } else {
+            iy = (unsigned)q / (unsigned)a.W;
+            ix = q - iy * a.W;
+          }
+        }
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
-          {
-            const int oy = (iy << a.up2) + (ch >> 1), ox = (ix << a.up2) + (ch & 1);
-            const long op = ((long)n * Ho + oy) * Wo + ox;
-            gr[u][ch] = *reinterpret_cast<const uint4*>(dt + op * lddt + c0);
-            mr[u][ch] = a.mode == 1 ? a.mask[op] : 0.f;
-          }
+          const int op = NCH > 1 ? ((iy << a.up2) + (ch >> 1)) * Wo + (ix << a.up2) + (ch & 1) : q;
+          gr[u][ch] = *reinterpret_cast<const uint4*>(gs + (unsigned)op * (unsigned)lddt);
+          mr[u][ch] = ssa ? ms[op] : 0.f;
         }
       }
     }
@@ -455,34 +542,32 @@ EE_DEV void bwd_dx_body(const ModArgs& a, const bf16_t* __restrict__ dt, int ldd
     for (int u = 0; u < DXU; ++u) {
       const int q = qb + u * rows;
       if (q >= q1) break;
-      float xh[8], o[8];
+      f2_t xh[4], o[4];
       unpack8(xr[u], xh);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        xh[j] = (xh[j] - P.mean[j]) * P.istd[j];
-        o[j] = 0.f;
+      for (int k = 0; k < 4; ++k) {
+        xh[k] = (xh[k] - P.mean[k]) * P.istd[k];
+        o[k] = splat2(0.f);
       }
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
-        float gv[8];
+        f2_t gv[4];
         unpack8(gr[u][ch], gv);
+        const f2_t mm = splat2(mr[u][ch]);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float mul, add;
-          coeffs(a, P, j, mr[u][ch], mul, add);
-          const float tv = xh[j] * mul + add;
-          float g = gv[j];
-          if (a.act == ACT_RELU) g = tv > 0.f ? g : 0.f;
-          else if (a.act == ACT_LRELU) g = tv > 0.f ? g : g * a.slope;
-          o[j] += P.istd[j] * (g * mul - m1[j] - vg[j] * xh[j] * m2[j]);
+        for (int k = 0; k < 4; ++k) {
+          const f2_t mul = ssa ? P.pm[k] * mm + splat2(1.f) : P.pm[k];
+          const f2_t add = ssa ? P.pa[k] * mm : P.pa[k];
+          const f2_t g = gact2(gv[k], xh[k] * mul + add, ns);
+          o[k] += P.istd[k] * (g * mul - m1[k] - vg[k] * xh[k] * m2[k]);
         }
       }
-      store8(dx + ((long)n * HW + q) * lddx + c0, o, nv);
+      store8(ds + (unsigned)q * (unsigned)lddx, o, nv);
     }
   }
 }
 
-__global__ __launch_bounds__(NT) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_t* __restrict__ dt, int lddt,
+__global__ __launch_bounds__(NT, 4) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_t* __restrict__ dt, int lddt,
                                                           const double* __restrict__ chan, double count,
                                                           bf16_t* __restrict__ dx, int lddx, int ppc) {
   const int C8 = (a.C + 7) / 8, rows = NT / C8;
@@ -492,16 +577,16 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_
   const int q1 = min(a.H * a.W, ((int)blockIdx.x + 1) * ppc);
   ChanParams P;
   load_params(a, n, c0, P);
-  float vg[8], m1[8], m2[8];
+  f2_t vg[4], m1[4], m2[4];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = min(c0 + j, a.C - 1);
-    vg[j] = a.stats[2 * a.C + c];
-    m1[j] = (float)(chan[c] / count);
-    m2[j] = (float)(chan[a.C + c] / count);
+    vg[j >> 1][j & 1] = a.stats[2 * a.C + c];
+    m1[j >> 1][j & 1] = (float)(chan[c] / count);
+    m2[j >> 1][j & 1] = (float)(chan[a.C + c] / count);
   }
-  if (a.up2) bwd_dx_body<2, 4>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
-  else bwd_dx_body<4, 1>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
+  if (a.up2) bwd_dx_body<1, 4>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
+  else bwd_dx_body<2, 1>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
 }
 
 ModArgs make_args(const eegan_bnmod_desc* d) {
@@ -522,13 +607,18 @@ ModArgs make_args(const eegan_bnmod_desc* d) {
   a.mask = d->mask;
   a.act = d->act;
   a.slope = d->slope;
+  const int Wo = d->W << d->up2;
+  a.wsh = (Wo & (Wo - 1)) == 0 ? __builtin_ctz((unsigned)Wo) : -1;
+  a.nslope = d->act == ACT_RELU ? 0.f : d->act == ACT_LRELU ? d->slope : 1.f;
   return a;
 }
 
-// chunks of a per-sample pixel range: ~2048 blocks overall, >= 8 pixel rows per block
-int pix_chunks(int N, long HW, int C, int& ppc) {
+// chunks of a per-sample pixel range: ~`target` blocks overall (whole rounds of
+// resident blocks: the forward holds 6 blocks per CU -> 1536, the dx pass 4 ->
+// 2048 = two rounds), >= 8 pixel rows per block
+int pix_chunks(int N, long HW, int C, int& ppc, int target = 2048) {
   const int rows = NT / ((C + 7) / 8);
-  ppc = (int)std::max<long>((long)rows * 8, (HW * N + 2047) / 2048);
+  ppc = (int)std::max<long>((long)rows * 8, (HW * N + target - 1) / target);
   return std::max(1, ee_cdiv(HW, ppc));
 }
 
@@ -536,6 +626,17 @@ bool vec_ok(const eegan_bnmod_desc* d, int ld, const void* p, const char* what) 
   if ((d->ldx % 8) || (ld % 8) || ((uintptr_t)d->x & 15) || ((uintptr_t)p & 15) || (d->C + 7) / 8 > NT) {
     ee_set_error("%s: bf16 rows must be 16-byte aligned with channel strides multiple of 8 (ldx %d, ld %d, C %d)",
                  what, d->ldx, ld, d->C);
+    return false;
+  }
+  if (d->act != ACT_NONE && d->act != ACT_RELU && d->act != ACT_LRELU) {
+    ee_set_error("%s: activation %d (none / relu / leaky relu only)", what, d->act);
+    return false;
+  }
+  // element offsets of one sample's rows are 32-bit in the kernels
+  const long HWo = (long)(d->H << d->up2) * (d->W << d->up2);
+  if ((long)d->N * HWo * std::max(ld, d->ldx) >= (1L << 31)) {
+    ee_set_error("%s: tensor of %ld elements exceeds the kernels' 32-bit offsets", what,
+                 (long)d->N * HWo * std::max(ld, d->ldx));
     return false;
   }
   return true;
@@ -590,7 +691,7 @@ int eegan_bnmod_fwd(const eegan_bnmod_desc* d, uint16_t* y, int ldy, hipStream_t
   ModArgs a = make_args(d);
   if (!vec_ok(d, ldy, y, "bnmod_fwd")) return -22;
   int ppc;
-  const int chunks = pix_chunks(d->N, (long)(d->H << d->up2) * (d->W << d->up2), d->C, ppc);
+  const int chunks = pix_chunks(d->N, (long)(d->H << d->up2) * (d->W << d->up2), d->C, ppc, 1536);
   bnmod_fwd_kernel<false><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, FinArgs{});
   return ee_check_launch("bnmod_fwd");
 }
@@ -605,7 +706,7 @@ int eegan_bnmod_fwd_fin(const eegan_bnmod_desc* d, const double* sums, double co
     return -22;
   }
   int ppc;
-  const int chunks = pix_chunks(d->N, (long)(d->H << d->up2) * (d->W << d->up2), d->C, ppc);
+  const int chunks = pix_chunks(d->N, (long)(d->H << d->up2) * (d->W << d->up2), d->C, ppc, 1536);
   const FinArgs f{sums, count, sum_scale, eps, momentum, clamp_mode, running_mean, running_var,
                   const_cast<float*>(d->stats)};
   bnmod_fwd_kernel<true><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, f);

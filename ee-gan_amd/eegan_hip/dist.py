@@ -26,9 +26,12 @@ from . import functional as Fn
 FORCE = os.environ.get('EEGAN_FORCE_DIST') == '1'
 COMMS = []    # eegan_hip.rccl.Communicator per stream lane when the ranks own GPUs (graph-capturable)
 # SyncBN statistics by the one-shot peer-write kernel (eegan_hip.peer) instead
-# of RCCL (EEGAN_SYNCBN_PEER=1; off by default -- unmeasured at N > 1)
-PEER = os.environ.get('EEGAN_SYNCBN_PEER', '0') == '1'
-N_LANES = 6   # lane 0: the caller's (main) stream; 1..: streams bound with bind_stream
+# of RCCL: EEGAN_SYNCBN_PEER=1 / 0 forces it on / off; unset, it is on when the
+# ranks own GPUs over RCCL (backend "nccl", world > 1).  The regions are
+# validated collectively when they are built; if any rank cannot map or
+# exchange through them, every rank keeps RCCL (eegan_hip.peer)
+PEER = os.environ.get('EEGAN_SYNCBN_PEER')
+N_LANES = 7   # lane 0: the caller's (main) stream; 1..: streams bound with bind_stream
 _LANE_OF = {}
 
 
@@ -88,9 +91,16 @@ def init_from_env(backend=None):
     return rank(), world_size()
 
 
+def peer_syncbn(group=None):
+    """Whether SyncBN statistics go through the peer-write all-reduce."""
+    if PEER is not None:
+        return PEER == '1'
+    return is_on() and dist.get_backend(group) == 'nccl' and dist.get_world_size(group) > 1
+
+
 def install_syncbn_hook(group=None):
     if is_on() and (dist.get_world_size(group) > 1 or FORCE):
-        if PEER:
+        if peer_syncbn(group):
             from .peer import PeerAllReduce
             Fn.SYNC_BN_ALLREDUCE = PeerAllReduce(group)
         elif COMMS and group is None:
@@ -129,6 +139,29 @@ def all_reduce(t):
         c.all_reduce(t)
     else:
         dist.all_reduce(t)
+
+
+def broadcast(t, src=0):
+    """In place: rank `src`'s t on every rank (own RCCL communicator for device tensors)."""
+    c = comm() if t.is_cuda and t.is_contiguous() else None
+    if c is not None:
+        c.broadcast(t, src)
+    else:
+        dist.broadcast(t, src)
+
+
+def all_gather_bytes(b, device=None):
+    """[every rank's b] (equal lengths): over the current lane's own RCCL
+    communicator when the ranks own GPUs (no ProcessGroupNCCL work that its
+    watchdog would still track when a graph capture starts), else through the
+    process group.  Synchronises the host."""
+    if COMMS:
+        x = torch.tensor(list(b), dtype=torch.uint8, device=device if device is not None else 'cuda')
+        out = _gather(x).cpu().reshape(world_size(), len(b))
+        return [bytes(row.tolist()) for row in out]
+    out = [None] * world_size()
+    dist.all_gather_object(out, bytes(b))
+    return out
 
 
 def _gather(x):
@@ -276,7 +309,7 @@ def broadcast_state(module, src=0):
             if not x.is_contiguous():
                 raise RuntimeError('eegan_hip: cannot broadcast a non-dense %s of shape %s'
                                    % (type(module).__name__, tuple(t.shape)))
-            dist.broadcast(x, src)
+            broadcast(x, src)
 
 
 def check_collectives():

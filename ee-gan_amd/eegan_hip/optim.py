@@ -35,6 +35,14 @@ completes it (the all-reduce is issued there); buckets written from several
 streams, or holding a parameter whose gradient arrives any other way
 (autograd's own accumulation), are reduced at step(), as are all buckets of
 an unlearned window.  EEGAN_GRAD_OVERLAP=0 reduces everything at step().
+
+Communication lane (`comm_stream`, set by the trainer for the optimizers on
+the step's critical path): a bucket's all-reduce is issued on that stream
+instead -- ordered behind every write issued so far on the writing stream by
+an event -- so the rest of the backward on the writing stream does not queue
+behind the reduction; step() waits for the lane before averaging and the
+Adam launch.  The lane has its own RCCL communicator (eegan_hip.dist.
+bind_stream); its reductions keep the plan's bucket order on every rank.
 """
 import os
 
@@ -99,6 +107,8 @@ class FlatAdam(torch.optim.Optimizer):
         self._key_seen = {}      # window key -> windows opened under it
         self._late = set()       # params whose gradient went through autograd at least once
         self._win = None
+        self.comm_stream = None  # bucket all-reduces on this stream (the trainer's communication lane)
+        self._comm_used = False
 
     # ------------------------------------------------------ overlapped DP --
     def set_bucket_bytes(self, nbytes):
@@ -137,10 +147,20 @@ class FlatAdam(torch.optim.Optimizer):
         import torch.distributed as dist
         from . import dist as D
         s, e = self._flat_range(b)
-        if self.process_group is dist.group.WORLD:
-            D.all_reduce(self.gflat[s:e])
+
+        def issue():
+            if self.process_group is dist.group.WORLD:
+                D.all_reduce(self.gflat[s:e])
+            else:
+                dist.all_reduce(self.gflat[s:e], group=self.process_group)
+        cs = self.comm_stream
+        if cs is not None and self.gflat.is_cuda:
+            cs.wait_stream(torch.cuda.current_stream())   # behind every gradient write issued so far
+            with torch.cuda.stream(cs):
+                issue()
+            self._comm_used = True
         else:
-            dist.all_reduce(self.gflat[s:e], group=self.process_group)
+            issue()
         self._win['done'][b] = True
 
     def _new_window(self):
@@ -253,6 +273,9 @@ class FlatAdam(torch.optim.Optimizer):
         self._win = None
         for p in self.params:
             p._eegan_track = None
+        if self._comm_used:
+            torch.cuda.current_stream().wait_stream(self.comm_stream)
+            self._comm_used = False
         self.gflat.mul_(1.0 / world)
 
     @torch.no_grad()

@@ -47,22 +47,37 @@ class PeerRegion(object):
         nbytes = LIB.eegan_peer_region_bytes(cap)
         own = C.c_void_p()
         handle = (C.c_ubyte * 64)()
-        with torch.cuda.device(device if device is not None else torch.cuda.current_device()):
-            ops.peer_alloc(nbytes, C.byref(own), handle)
-        self.own = own.value
-        handles = [None] * self.world
-        dist.all_gather_object(handles, bytes(handle), group=self.group)
-        bases = []
+        self.own, err = None, None
+        try:
+            with torch.cuda.device(device if device is not None else torch.cuda.current_device()):
+                ops.peer_alloc(nbytes, C.byref(own), handle)
+            self.own = own.value
+        except Exception as e:
+            err = str(e)
         self._opened = []
-        for r, h in enumerate(handles):
-            if r == self.rank:
-                bases.append(self.own)
-                continue
-            hb = (C.c_ubyte * 64).from_buffer_copy(h)
-            p = C.c_void_p()
-            ops.peer_open(hb, C.byref(p))
-            bases.append(p.value)
-            self._opened.append(p.value)
+        # every rank joins the exchange, a failed allocation included (flag byte 0)
+        handles = _exchange(bytes([0 if err else 1]) + bytes(handle), self.group)
+        handles = [h[1:] if h[0] else None for h in handles]
+        if any(h is None for h in handles):
+            if self.own:
+                ops.peer_free(self.own)
+                self.own = None
+            raise RuntimeError('peer region allocation failed on rank(s) %s%s' % (
+                [r for r, h in enumerate(handles) if h is None], (': ' + err) if err else ''))
+        bases = []
+        try:
+            for r, h in enumerate(handles):
+                if r == self.rank:
+                    bases.append(self.own)
+                    continue
+                hb = (C.c_ubyte * 64).from_buffer_copy(h)
+                p = C.c_void_p()
+                ops.peer_open(hb, C.byref(p))
+                bases.append(p.value)
+                self._opened.append(p.value)
+        except Exception:
+            self.close()
+            raise
         self._bases = (C.c_void_p * self.world)(*bases)
 
     def all_reduce(self, t):
@@ -88,21 +103,62 @@ class PeerRegion(object):
 
 
 class PeerAllReduce(object):
-    """callable(t) -> in-place sum over the ranks; one region per issuing stream."""
+    """callable(t) -> in-place sum over the ranks; one region per issuing stream.
+
+    A region is built collectively the first time a stream reduces (eager) and
+    validated at once: every rank must map every peer's region and one test
+    exchange (rank + 1 from each rank) must return the exact sum on every rank
+    within the kernel's wait bound.  The verdict is agreed over the process
+    group, so if ANY rank fails, ALL ranks switch this reducer to RCCL
+    (`fallback`) for the rest of the run -- never a mixed state."""
 
     def __init__(self, group=None, cap=CAP):
         self.group = group
         self.cap = cap
         self.regions = {}
+        self.fallback = None   # the reason, once the ranks agreed to use RCCL instead
+
+    def _agree(self, ok):
+        return all(f == b'\x01' for f in _exchange(b'\x01' if ok else b'\x00', self.group))
+
+    def _build(self):
+        r, why = None, None
+        try:
+            r = PeerRegion(self.group, self.cap)
+        except Exception as e:   # this rank cannot allocate / map: agreed below
+            why = 'region setup: %s' % e
+        if self._agree(r is not None):
+            world = dist.get_world_size(self.group)
+            t = torch.full((8,), float(dist.get_rank(self.group) + 1), dtype=torch.float64,
+                           device=torch.cuda.current_device())
+            r.all_reduce(t)
+            torch.cuda.synchronize()
+            good = r.timed_out() == 0 and bool((t == world * (world + 1) / 2.0).all())
+            if not good:
+                why = 'test exchange returned %s' % t[:2].tolist()
+            if self._agree(good):
+                return r
+        elif why is None:
+            why = 'another rank could not set up its region'
+        if r is not None:
+            dist.barrier(group=self.group)
+            r.close()
+        self.fallback = why or 'a peer rank failed the test exchange'
+        import warnings
+        warnings.warn('eegan_hip.peer: SyncBN statistics over RCCL instead of the peer-write all-reduce (%s)'
+                      % self.fallback)
+        return None
 
     def region(self):
         s = torch.cuda.current_stream()
         r = self.regions.get(s.cuda_stream)
-        if r is None:
+        if r is None and self.fallback is None:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError('eegan_hip.peer: first SyncBN reduction of a stream inside graph capture; run '
                                    'one eager step first (regions are created collectively, outside capture)')
-            r = self.regions[s.cuda_stream] = PeerRegion(self.group, self.cap)
+            r = self._build()
+            if r is not None:
+                self.regions[s.cuda_stream] = r
         return r
 
     def __call__(self, t):
@@ -111,7 +167,14 @@ class PeerAllReduce(object):
         elif t.dtype != torch.float64 or not t.is_contiguous() or t.numel() > self.cap:
             dist.all_reduce(t, group=self.group)
         else:
-            self.region().all_reduce(t)
+            r = self.region()
+            if r is not None:
+                r.all_reduce(t)
+            elif self.group is None:
+                from . import dist as D
+                D.all_reduce(t)      # RCCL on the stream's own communicator (capturable)
+            else:
+                dist.all_reduce(t, group=self.group)
 
     def timed_out(self):
         return max([r.timed_out() for r in self.regions.values()] or [0])
@@ -129,6 +192,18 @@ class PeerAllReduce(object):
         for r in self.regions.values():
             r.close()
         self.regions = {}
+
+
+def _exchange(b, group):
+    """Every rank's bytes b (equal lengths), in rank order: over the lane's own
+    RCCL communicator for the default group (eegan_hip.dist.all_gather_bytes),
+    else through the group."""
+    if group is None:
+        from . import dist as D
+        return D.all_gather_bytes(b, torch.cuda.current_device())
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, b, group=group)
+    return out
 
 
 def fixed_order_sum(t, group=None):

@@ -6,7 +6,11 @@ data-parallel step -- collectives included -- can be captured into the step's
 HIP graph.  torch's ProcessGroupNCCL is used only to exchange the unique ids
 and for host-side barriers outside the timed region: collectives it issues
 inside a graph capture leave events its watchdog thread later queries, which
-the HIP runtime rejects (hipErrorCapturedEvent) and aborts the process.
+the HIP runtime rejects (hipErrorCapturedEvent) and aborts the process -- and
+so does one issued just before a capture, while the watchdog still tracks it.
+Set-up exchanges that run at a step's first (eager) pass -- the weight
+broadcast of eegan_hip.dist.broadcast_state, the peer-region handles of
+eegan_hip.peer -- therefore go over these communicators too.
 
 Ordering: RCCL needs the operations of one communicator issued in the same
 order on every rank and never concurrently from two streams.  The step runs
@@ -40,6 +44,7 @@ def _load():
     lib.ncclCommInitRank.argtypes = [C.POINTER(C.c_void_p), C.c_int, _UniqueId, C.c_int]
     lib.ncclAllReduce.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
     lib.ncclAllGather.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_void_p]
+    lib.ncclBroadcast.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
     lib.ncclCommDestroy.argtypes = [C.c_void_p]
     lib.ncclGetErrorString.restype = C.c_char_p
     lib.ncclGetErrorString.argtypes = [C.c_int]
@@ -84,6 +89,12 @@ class Communicator(object):
         self._run(lambda s: self._check(self.lib.ncclAllGather(x.data_ptr(), out.data_ptr(), x.numel(), _DT[x.dtype],
                                                                self.comm, s), 'ncclAllGather'))
         return out
+
+    def broadcast(self, t, root=0):
+        """Rank `root`'s t into every rank's t (contiguous device tensor, in place)."""
+        assert t.is_contiguous() and t.is_cuda
+        self._run(lambda s: self._check(self.lib.ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
+                                                               root, self.comm, s), 'ncclBroadcast'))
 
     def close(self):
         if self.comm:

@@ -60,6 +60,12 @@ LANE_ORDER = os.environ.get('EEGAN_LANE_ORDER', 'rev')
 # stream (models.Gen.forward_branched puts them on D64's idle lane; module
 # constant for A/B: tools/ab_inproc.py "py:eegan_hip.trainer.GEN_SIDE=False")
 GEN_SIDE = True
+# True (N > 1 with stream lanes): the largest discriminator's and the generator's
+# gradient buckets are all-reduced on communication lanes of their own (streams
+# forked from the step's origin stream, own RCCL communicators), so their
+# backward kernels do not queue behind the reductions; each optimizer's step
+# waits for its lane (FlatAdam.comm_stream).  Module constant for A/B.
+COMM_LANES = True
 
 # a g_update term already differentiated w.r.t. its fake image on its lane
 # (GTERM_GRAD_EARLY): its value, the image alias and the gradient there
@@ -127,6 +133,19 @@ class Trainer(object):
             for s in self._streams[:n]:
                 s.wait_stream(main)
         return self._streams[:n]
+
+    def _comm_lanes(self):
+        """The communication lanes (N > 1): created once, bound to communicators
+        5 and 6 (eegan_hip.dist lanes 4 / 5) and handed to the optimizers."""
+        if not (COMM_LANES and self.use_streams and D.collective()):
+            return []
+        if getattr(self, '_comm', None) is None:
+            self._comm = [new_stream(self.device, 0) for _ in range(2)]
+            for i, st in enumerate(self._comm):
+                D.bind_stream(st, 4 + i)
+            self.optimizerDs[-1].comm_stream = self._comm[0]
+            self.optimizerG.comm_stream = self._comm[1]
+        return self._comm
 
     @staticmethod
     def _on(stream):
@@ -506,6 +525,10 @@ class Trainer(object):
         B = self.batch_size
         dev = self.device
         Fn.stamp('start')
+        comm = self._comm_lanes()
+        main = torch.cuda.current_stream()
+        for cs in comm:   # forked from the origin stream at the start (graph capture: never from a lane)
+            cs.wait_stream(main)
         words, sent, attrs, unpair = emb if emb is not None else self.encode_text(batch)
         Fn.stamp('text encode')
         class_labels = None
@@ -537,6 +560,7 @@ class Trainer(object):
         damsm = damsm or None
         g = self.g_update(fake_imgs, sent, words, attn_attr_emb, cls_ids, B, match_labels, batch['cap_lens'],
                           class_labels, iter_rec, damsm=damsm, terms=terms)
+        self._join(comm)   # (each optimizer step already waited for its lane)
         Fn.stamp('end')
         self._steps = getattr(self, '_steps', 0) + 1
         if self._steps % self.CHECK_EVERY == 0 and not torch.cuda.is_current_stream_capturing():

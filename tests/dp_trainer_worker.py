@@ -3,8 +3,10 @@ optimizer) on one rank of a torchrun group; writes every parameter after the
 steps and how many gradient buckets each optimizer reduced DURING a backward
 (FlatAdam's overlapped all-reduce) to OUT/rankR_<tag>.pt.  The first step's
 windows learn the write plans, the second overlaps.  tests/test_gpu_dist.py
-runs it with EEGAN_GRAD_OVERLAP=1 and =0 (two ranks sharing one GPU over gloo)
-and requires bit-identical parameters."""
+runs it with EEGAN_GRAD_OVERLAP=1 and =0, and with the generator's second
+stream (trainer.GEN_SIDE) and the communication lanes (trainer.COMM_LANES)
+off (DP_GEN_SIDE=0, DP_COMM_LANES=0), two ranks sharing one GPU over gloo, and
+requires bit-identical parameters."""
 import os
 import sys
 
@@ -23,7 +25,10 @@ def main(out, tag):
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     import bench
+    from eegan_hip import trainer as TR
     from eegan_hip import dist as D
+    TR.GEN_SIDE = os.environ.get('DP_GEN_SIDE', '1') == '1'
+    TR.COMM_LANES = os.environ.get('DP_COMM_LANES', '1') == '1'
     from eegan_hip import optim as O
     from eegan_hip.synthetic import make_batch
     rank, world = D.init_from_env()
@@ -63,7 +68,8 @@ def main(out, tag):
                  for need, e, _ in pl]),
                 flush=True)
     torch.save({'params': [o.flat.cpu() for o in opts], 'early': [early.get(id(o), 0) for o in opts],
-                'buckets': [len(o.buckets) for o in opts]}, os.path.join(out, 'rank%d_%s.pt' % (rank, tag)))
+                'buckets': [len(o.buckets) for o in opts],
+                'comm_lanes': [o.comm_stream is not None for o in opts]}, os.path.join(out, 'rank%d_%s.pt' % (rank, tag)))
 
 
 if __name__ == '__main__':

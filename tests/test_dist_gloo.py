@@ -246,7 +246,8 @@ def _case_syncbn_peer_combine(rank):
     from eegan_hip import functional as Fn
     from eegan_hip.peer import PeerAllReduce
     W = dist.get_world_size()
-    D.PEER = True
+    assert not D.peer_syncbn()        # unset: on only for GPU ranks over RCCL, not for gloo
+    D.PEER = '1'
     try:
         D.install_syncbn_hook()
         assert isinstance(Fn.SYNC_BN_ALLREDUCE, PeerAllReduce) and Fn.SYNC_BN_WORLD == W
@@ -266,7 +267,7 @@ def _case_syncbn_peer_combine(rank):
             dist.all_reduce(ref)
             assert torch.allclose(t, ref, rtol=1e-14, atol=0)
     finally:
-        D.PEER = False
+        D.PEER = None
         D.install_syncbn_hook()
 
 

@@ -93,22 +93,53 @@ def test_flat_adam_overlapped_allreduce_two_ranks(gpu, tmp_path):
     buckets all-reduced during the backward (EEGAN_GRAD_OVERLAP=1, default)
     give parameters bit-identical to reducing everything at step() (=0), the
     two ranks agree, and the overlap actually happened (buckets reduced from
-    inside the backward for every optimizer of the third step)."""
+    inside the backward for every optimizer of the third step).  The default
+    step runs the largest D's and the generator's reductions on communication
+    lanes (trainer.COMM_LANES) and the generator's stage 2-3 branches on a
+    second stream (trainer.GEN_SIDE); both off ('plain') gives the same bits."""
     res = {}
-    for tag, ov in (('ov', '1'), ('seq', '0')):
+    for tag, ov, extra in (('ov', '1', {}), ('seq', '0', {}),
+                           ('plain', '1', {'DP_GEN_SIDE': '0', 'DP_COMM_LANES': '0'})):
         cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
                '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
                os.path.join(HERE, 'dp_trainer_worker.py'), str(tmp_path), tag]
-        env = dict(os.environ, OMP_NUM_THREADS='2', EEGAN_GRAD_OVERLAP=ov)
+        env = dict(os.environ, OMP_NUM_THREADS='2', EEGAN_GRAD_OVERLAP=ov, **extra)
         r = subprocess.run(cmd, env=env, timeout=240, capture_output=True, text=True)
         assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
         res[tag] = [torch.load(os.path.join(tmp_path, 'rank%d_%s.pt' % (i, tag))) for i in range(2)]
     for tag in res:
         for a, b in zip(res[tag][0]['params'], res[tag][1]['params']):
             assert torch.equal(a, b), tag
-    for a, b in zip(res['ov'][0]['params'], res['seq'][0]['params']):
-        assert torch.equal(a, b)
+    for tag in ('seq', 'plain'):
+        for a, b in zip(res['ov'][0]['params'], res[tag][0]['params']):
+            assert torch.equal(a, b), tag
     print('overlap: buckets reduced inside backward per optimizer', res['ov'][0]['early'],
-          'of', res['ov'][0]['buckets'])
+          'of', res['ov'][0]['buckets'], 'comm lanes', res['ov'][0]['comm_lanes'])
     assert all(e > 0 for e in res['ov'][0]['early']), res['ov'][0]['early']
     assert all(e == 0 for e in res['seq'][0]['early'])
+    assert res['ov'][0]['comm_lanes'] == [True, False, False, True]      # optimizerG, D64, D128, D256
+    assert not any(res['plain'][0]['comm_lanes'])
+
+
+def test_force_dist_captured_step_with_comm_lanes(gpu, tmp_path):
+    """EEGAN_FORCE_DIST=1 (one rank, RCCL): the data-parallel step with every
+    collective issued on its lane's own communicator -- the gradient buckets of
+    the largest D and of the generator on their communication lanes
+    (trainer.COMM_LANES) -- captures and replays bit-identical to the eager
+    step and to the step with the buckets reduced in their writing lanes."""
+    res = {}
+    for tag, mode, lanes in (('eager', 'eager', '1'), ('graph', 'graph', '1'), ('inlane', 'graph', '0')):
+        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '1',
+               '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
+               os.path.join(HERE, 'dp_force_worker.py'), str(tmp_path), tag, mode]
+        env = dict(os.environ, OMP_NUM_THREADS='2', EEGAN_FORCE_DIST='1', DP_COMM_LANES=lanes)
+        env.pop('EEGAN_DIST_BACKEND', None)
+        r = subprocess.run(cmd, env=env, timeout=240, capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        res[tag] = torch.load(os.path.join(tmp_path, 'force_%s.pt' % tag))
+    assert res['graph']['comm_lanes'] == [True, False, False, True]
+    assert not any(res['inlane']['comm_lanes'])
+    d = (res['graph']['state'] - res['eager']['state']).abs().max()
+    print('FORCE_DIST max |graph - eager| %.3e' % float(d))
+    assert torch.equal(res['graph']['state'], res['eager']['state'])
+    assert torch.equal(res['graph']['state'], res['inlane']['state'])
