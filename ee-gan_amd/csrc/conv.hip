@@ -87,6 +87,7 @@ struct ConvArgs {
   int res_vec;  // res rows 8-byte aligned (ldres % 4 == 0, aligned base): vector residual loads
   int wide;     // conv_fast_kernel pairs: one 64-channel stage of whole 128-B lines per K-step pair
   int stage_epi;  // conv_fast_kernel: LDS-staged epilogue (unsplit bf16 output, 16-B aligned rows; host-checked)
+  int* ctr;       // conv_fast_kernel split-K: per-tile arrival counters (zero on entry and exit) -> in-kernel finish
 };
 
 // K step kt, 8-channel chunk kc -> kernel tap and channel.  Normal mode: the
@@ -801,6 +802,118 @@ EE_DEV void lds_dma16s(rsrc_t rsrc, int lds_addr, unsigned voff, int soff) {
                : "memory", "m0");
 }
 
+// Split-K finished inside conv_fast_kernel (a.ctr set; host-checked: Mrows % 4 == 0, the
+// vector reduce's alignment, slab < 2 GB): every split stores its fp32 partial tile with
+// sc1 16-B stores (written through, not parked in its XCD's L2); every storing wave waits
+// for its stores (vmcnt 0), the workgroup barriers, one lane adds 1 to the tile's counter
+// (agent-scope atomic) -- the workgroup whose add returns nsplit - 1 arrived last.  It
+// resets the counter, reads every split's partial back with sc1 loads (L1/L2 bypassed:
+// the hand-off form of MI355X_MICROARCH.md's cross-workgroup table, no fences), sums them
+// in split order 0..nsplit-1 and applies the epilogue exactly as splitk_item4: the same
+// bits as the separate reduce launch, which it replaces (one launch boundary and its
+// dispatch latency less per split conv).  The other splits exit.
+EE_DEV void out_pixel(const ConvArgs& a, int pc, int CH, int CW, int qy, int qx, int stc, bool cls_map, long& p,
+                      long& rpix) {
+  p = pc;
+  rpix = pc;
+  if (cls_map) {
+    const int hw = CH * CW;
+    const int n = pc / hw, rem = pc - n * hw;
+    const int yy = rem / CW, xx = rem - yy * CW;
+    const int y = qy + stc * yy, x = qx + stc * xx;
+    p = ((long)n * a.OH + y) * a.OW + x;
+    if (a.res_up2) rpix = ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
+  } else if (a.res_up2) {
+    const unsigned hw = (unsigned)a.OH * (unsigned)a.OW;
+    const unsigned n = (unsigned)pc / hw, rem = (unsigned)pc - n * hw;
+    const unsigned y = rem / (unsigned)a.OW, x = rem - y * (unsigned)a.OW;
+    rpix = ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1);
+  }
+}
+
+constexpr int SC1 = 16;   // buffer-op cache policy: sc1 (gfx950)
+
+template <int MODE, int TCO, int TPIX, int FI, int FJ, int WT_CO, int WT_PIX>
+EE_DEV void splitk_fused_finish(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ], int pix0, int co0, int wi, int wj,
+                                int lane, int tid, int split, int tile, int Pc, int CH, int CW, int qy, int qx,
+                                int stc) {
+  const bool cls_map = MODE == MODE_BWDD && a.ncls > 1;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(a.part, (short)0, (int)((long)a.nsplit * a.P * a.Mrows * 4), 0x00020000);
+  const int fr = lane & 15;
+  const unsigned zoff = (unsigned)split * (unsigned)a.P * (unsigned)a.Mrows;
+#pragma unroll
+  for (int j = 0; j < FJ; ++j) {
+    const int pc = pix0 + wj * WT_PIX + j * 16 + fr;
+    if (pc >= Pc) continue;
+    long p, rpix;
+    out_pixel(a, pc, CH, CW, qy, qx, stc, cls_map, p, rpix);
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const int co = co0 + wi * WT_CO + i * 16 + (lane >> 4) * 4;
+      if (co >= a.Mrows) continue;
+      __builtin_amdgcn_raw_buffer_store_b128(acc[i][j], rs, (zoff + (unsigned)p * (unsigned)a.Mrows + co) * 4u, 0,
+                                             SC1);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __shared__ int s_last;
+  __syncthreads();
+  if (tid == 0) {
+    int* c = a.ctr + tile;
+    const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == a.nsplit - 1;
+    if (old == a.nsplit - 1) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // the last split: 4 channels of one pixel per item, the slab row of each split read back
+  constexpr int CQ = TCO / 4, ITEMS = TPIX * CQ;
+  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
+  const unsigned zstride = (unsigned)a.P * (unsigned)a.Mrows * 4u;
+  for (int item = tid; item < ITEMS; item += 256) {
+    const int pc = pix0 + item / CQ, co = co0 + 4 * (item % CQ);
+    if (pc >= Pc || co >= a.Mrows) continue;
+    long p, rpix;
+    out_pixel(a, pc, CH, CW, qy, qx, stc, cls_map, p, rpix);
+    uint2 gv = make_uint2(0, 0), rv = make_uint2(0, 0);
+    if (MODE == MODE_BWDD && a.gate) gv = *reinterpret_cast<const uint2*>(a.gate + p * a.ldgate + co);
+    if (a.res) rv = *reinterpret_cast<const uint2*>(a.res + (a.res_up2 ? rpix : p) * a.ldres + co);
+    f32x4_t bv = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias) bv = f32x4_t{a.bias[co], a.bias[co + 1], a.bias[co + 2], a.bias[co + 3]};
+    const unsigned off = ((unsigned)p * (unsigned)a.Mrows + co) * 4u;
+    f32x4_t sum = {0.f, 0.f, 0.f, 0.f};
+    int z = 0;
+    for (; z + 8 <= a.nsplit; z += 8) {
+      f32x4_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + (unsigned)(z + k) * zstride, 0, SC1);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sum += v[k];   // split order, as the reduce kernel
+    }
+    for (; z < a.nsplit; ++z) sum += __builtin_amdgcn_raw_buffer_load_b128(rs, off + (unsigned)z * zstride, 0, SC1);
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = act_fwd(sum[r] + bv[r], a.act, a.slope);
+    if (MODE == MODE_BWDD && a.gate) {
+      const float gg[4] = {lo_f(gv.x), hi_f(gv.x), lo_f(gv.y), hi_f(gv.y)};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] *= act_dgrad_from_y(gg[r], a.gate_act, a.gate_slope);
+    }
+    if (a.res) {
+      const float rr[4] = {lo_f(rv.x), hi_f(rv.x), lo_f(rv.y), hi_f(rv.y)};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = res_combine(a.res_scale, rr[r], gam, v[r]);
+    }
+    if (a.out_f32) {
+      *reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(a.out) + p * a.ldo + co) = {v[0], v[1], v[2], v[3]};
+    } else {
+      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(a.out) + p * a.ldo + co) =
+          make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    }
+  }
+}
+
 template <int MODE, int TCO, int TPIX, int KS = 1, int S = CONV_STAGES, int VAR = 0>
 __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_bytes, long w_bytes) {
   constexpr int WCO = TCO >= 64 ? 2 : 1, WPIX = 4 / WCO;
@@ -1114,6 +1227,12 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
   if (a.stage_epi) {
     staged_epilogue<MODE, TCO, TPIX, FI, FJ, WT_CO, WT_PIX>(a, acc, reinterpret_cast<float4*>(lds), pix0, co0, wi, wj,
                                                             lane, tid, Pc, CH, CW, qy, qx, stc);
+    return;
+  }
+  if (a.ctr) {   // split-K finished here (block-uniform)
+    const int tile = (cls * (int)gridDim.y + (int)blockIdx.y) * (int)gridDim.x + (int)blockIdx.x;
+    splitk_fused_finish<MODE, TCO, TPIX, FI, FJ, WT_CO, WT_PIX>(a, acc, pix0, co0, wi, wj, lane, tid, split, tile, Pc,
+                                                                CH, CW, qy, qx, stc);
     return;
   }
   igemm_epilogue<MODE, FI, FJ, WT_CO, WT_PIX>(a, acc, pix0, co0, wi, wj, lane, split, Pc, CH, CW, qy, qx, stc);
@@ -3082,7 +3201,8 @@ int try_1x1(const ConvArgs& a, hipStream_t s, long src_bytes) {
 }
 
 template <int MODE>
-int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src_bytes) {
+int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src_bytes, int* ctr = nullptr,
+                 int ctr_n = 0) {
   if (const int th = try_thin<MODE>(a, s, src_bytes)) return th > 0 ? 0 : th;
   if (const int pw = try_1x1<MODE>(a, s, src_bytes)) return pw > 0 ? 0 : pw;
   if (MODE == MODE_BWDD)
@@ -3122,6 +3242,9 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
                  knob("red_vec4", 1);
   }
   const long w_bytes = (long)ee_round_up(a.Mrows, 128) * a.Kw * 2;
+  if (p.nsplit > 1 && a.red_vec4 && ctr && (long)grid.x * grid.y * a.ncls <= ctr_n &&
+      (long)p.nsplit * total * 4 < 0x7fffffffL && knob("splitk_fused", 1))
+    a.ctr = ctr;   // conv_fast_kernel finishes the split itself (below: only when `fast`)
 #define GL(TC, TP) ee_launch(conv_glds_kernel<MODE, TC, TP>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
 #define FA(TC, TP) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 4, 2>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
 #define IG(TC, TP, WC) ee_launch(conv_igemm_kernel<MODE, TC, TP, WC>, grid, dim3(256), 0, s, a)
@@ -3132,6 +3255,7 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   int tr_ = a.R, ts_ = a.S;
   if (MODE == MODE_BWDD && a.st > 1) tr_ = ee_cdiv(a.R, a.st), ts_ = ee_cdiv(a.S, a.st);
   const bool fast = glds && a.Cgp % BK == 0 && !a.up2 && tr_ * ts_ <= 32 && knob("fast", 1);
+  if (!fast) a.ctr = nullptr;
   if (fast) {
     if (p.tco == 128) { if (p.tpix == 128) FA(128, 128); else FA(128, 64); }
     else if (p.tco == 64) { if (p.tpix == 128) FA(64, 128); else FA(64, 64); }
@@ -3152,7 +3276,7 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
 #undef GL
 #undef FA
   int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd" : "conv_bwd_data");
-  if (rc || a.nsplit == 1) return rc;
+  if (rc || a.nsplit == 1 || a.ctr) return rc;
   const long work = a.red_vec4 ? total / 4 : total;
   ee_launch(conv_splitk_reduce_kernel<MODE>, dim3((int)std::min<long>((work + 255) / 256, 4096)), dim3(256), 0, s, a);
   return ee_check_launch("conv_splitk_reduce");
@@ -3288,7 +3412,8 @@ int eegan_conv_fwd(const eegan_conv_desc* d, const bf16_t* x, const bf16_t* wpac
     ee_set_error("conv_fwd: input channel stride %d must be a multiple of 8 (16-B aligned rows)", d->ldx);
     return -22;
   }
-  return launch_igemm<MODE_FWD>(a, a.P, ws, stream, (long)d->N * (d->H >> d->up2) * (d->W >> d->up2) * d->ldx * 2);
+  return launch_igemm<MODE_FWD>(a, a.P, ws, stream, (long)d->N * (d->H >> d->up2) * (d->W >> d->up2) * d->ldx * 2,
+                                d->splitk_ctr, d->splitk_ctr_n);
 }
 
 int eegan_conv_bwd_data(const eegan_conv_desc* d, const bf16_t* dy, const bf16_t* wpackT, void* dx, int lddx,
@@ -3338,7 +3463,8 @@ int eegan_conv_bwd_data_ex(const eegan_conv_desc* d, const bf16_t* dy, const bf1
     ee_set_error("conv_bwd_data: dy channel stride %d must be a multiple of 8", d->ldy);
     return -22;
   }
-  return launch_igemm<MODE_BWDD>(a, bwdd_pc_max(d), ws, stream, (long)d->N * d->Ho * d->Wo * d->ldy * 2);
+  return launch_igemm<MODE_BWDD>(a, bwdd_pc_max(d), ws, stream, (long)d->N * d->Ho * d->Wo * d->ldy * 2,
+                                 d->splitk_ctr, d->splitk_ctr_n);
 }
 
 static long wgrad_x_bytes(const eegan_conv_desc* d) {

@@ -193,12 +193,40 @@ class Geom:
                         Ho, Wo, ldy)
 
 
-def _desc_io(g, x_shape, ldx, ldy):
+# Split-K counters (eegan_conv_desc.splitk_ctr): one zeroed int array per stream, so
+# the kernels finish a split-K launch themselves (csrc/conv.hip splitk_fused_finish;
+# every counter used is zero again when the launch completes) and launches on
+# different stream lanes never share a counter.  Created outside graph capture (the
+# step's eager warm-up reaches every lane first); a stream first seen inside a
+# capture keeps the two-launch reduce.  SPLITK_FUSED = False: always two launches.
+SPLITK_FUSED = True
+SPLITK_CTR_N = 1 << 15
+_SPLITK_CTR = {}
+
+
+def _splitk_ctr(device):
+    if not SPLITK_FUSED:
+        return None
+    s = torch.cuda.current_stream(device).cuda_stream
+    t = _SPLITK_CTR.get((device, s))
+    if t is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        t = _SPLITK_CTR[(device, s)] = torch.zeros(SPLITK_CTR_N, dtype=torch.int32, device=device)
+    return t
+
+
+def _desc_io(g, x_shape, ldx, ldy, device=None):
     N, C, H, W = x_shape
     Hl, Wl = (H * 2, W * 2) if g.up2 else (H, W)
     Ho = (Hl + 2 * g.ph - g.R) // g.stride + 1
     Wo = (Wl + 2 * g.pw - g.S) // g.stride + 1
-    return ConvDesc(N, Hl, Wl, C, ldx, g.K, g.R, g.S, g.stride, g.ph, g.pw, g.up2, Ho, Wo, ldy)
+    d = ConvDesc(N, Hl, Wl, C, ldx, g.K, g.R, g.S, g.stride, g.ph, g.pw, g.up2, Ho, Wo, ldy)
+    if device is not None and device.type == 'cuda':
+        ctr = _splitk_ctr(device)
+        if ctr is not None:
+            d.splitk_ctr, d.splitk_ctr_n = ctr.data_ptr(), ctr.numel()
+    return d
 
 
 # ====================================================== launch timing ====
@@ -296,7 +324,7 @@ def conv_fwd_raw(x, W, b, g, act=0, slope=0.2, out_f32=False, cache=None, res=No
     N, C, H, Wd = x.shape
     Ho, Wo = g.out_hw(H, Wd)
     y = empty_nhwc(N, g.K, Ho, Wo, x.device, dtype=F32 if out_f32 else BF16)
-    d = _desc_io(g, x.shape, ld_of(x), ld_of(y))
+    d = _desc_io(g, x.shape, ld_of(x), ld_of(y), x.device)
     wp = _pack(W, cache, False)
     wsb = ops.conv_fwd_workspace(d)
     ws = workspace(wsb, x.device) if wsb else None
@@ -319,7 +347,7 @@ def conv_bwd_data_raw(dz, W, g, x_shape, cache=None, gate=None, gate_act=0, gate
     Hl, Wl = (H * 2, Wd * 2) if g.up2 else (H, Wd)
     dx = empty_nhwc(N, C, Hl, Wl, dz.device)
     dz = to_nhwc_bf16(dz)
-    d = _desc_io(g, x_shape, T.ld_for(C), ld_of(dz))
+    d = _desc_io(g, x_shape, T.ld_for(C), ld_of(dz), dz.device)
     if g.up2:
         d.H, d.W, d.up2 = Hl, Wl, 0
     wp = _pack(W, cache, True)

@@ -108,6 +108,7 @@ class FlatAdam(torch.optim.Optimizer):
         self._late = set()       # params whose gradient went through autograd at least once
         self._win = None
         self.comm_stream = None  # bucket all-reduces on this stream (the trainer's communication lane)
+        self.comm_origin = None  # the stream the lane was forked from (the step's origin stream)
         self._comm_used = False
 
     # ------------------------------------------------------ overlapped DP --
@@ -274,7 +275,18 @@ class FlatAdam(torch.optim.Optimizer):
         for p in self.params:
             p._eegan_track = None
         if self._comm_used:
-            torch.cuda.current_stream().wait_stream(self.comm_stream)
+            cur = torch.cuda.current_stream()
+            org = self.comm_origin
+            if org is None or org.cuda_stream == cur.cuda_stream:
+                cur.wait_stream(self.comm_stream)
+            else:
+                # a lane forked from the origin never waits on the communication lane
+                # itself: lane <-> lane waits make the runtime's end-of-capture walk
+                # over forked streams recurse without end (stack overflow inside
+                # hipStreamEndCapture); the origin joins the lane and this stream
+                # waits on the origin, which it was forked from anyway
+                org.wait_stream(self.comm_stream)
+                cur.wait_stream(org)
             self._comm_used = False
         self.gflat.mul_(1.0 / world)
 

@@ -439,14 +439,16 @@ class Trainer(object):
         if Fn.STAMPS is not None:   # diagnostics: when each fake image's gradient is complete
             for i, f in enumerate(fake_imgs):
                 f.register_hook(lambda g, i=i: (Fn.stamp('dfake%d ready' % i), g)[1])
-        self.optimizerG.zero_grad()
+        gen = getattr(self.netG, 'module', self.netG)
+        if not getattr(self, '_g_zeroed', False):
+            self.zero_grad_G()
+        self._g_zeroed = False
         # only the optimised parameters' gradients are formed: train.py's
         # g_loss.backward() also fills the D parameters' .grad, but d_update
         # zeroes those before every use (train.py:451,457), and the GP's
         # interpolated-image gradient is never read -- skipping them changes no
         # parameter and saves the D weight-gradient passes
         self._g_backward(terms, dfake, g_adv, g_loss, s_loss, w_loss, a_loss)
-        gen = getattr(self.netG, 'module', self.netG)
         if getattr(gen, 'side_stream', None) is not None:
             # the branch's backward nodes ran on the lane: their direct p.grad writes
             # (functional._grad_sink) are not among autograd's leaf-stream syncs
@@ -455,6 +457,19 @@ class Trainer(object):
         self.optimizerG.step()
         Fn.stamp('G adam')
         return g_loss.detach()
+
+    def zero_grad_G(self):
+        """optimizerG.zero_grad() (train.py:498), ordered before the generator
+        branch's lane as well: that lane's backward nodes write parameter
+        gradients straight into the flat buffer (functional._grad_sink), and
+        autograd syncs a node only with the producers of its input gradients --
+        a node whose input gradient was made on the lane itself (the 64-px
+        image's, GTERM_GRAD_EARLY) would otherwise accumulate before the zero
+        fill on the main stream lands."""
+        self.optimizerG.zero_grad()
+        gen = getattr(self.netG, 'module', self.netG)
+        if getattr(gen, 'side_stream', None) is not None:
+            gen.side_stream.wait_stream(torch.cuda.current_stream())
 
     def _g_backward(self, terms, dfake, g_adv, g_loss, s_loss, w_loss, a_loss):
         if any(isinstance(t, EarlyTerm) for t in terms):
@@ -529,6 +544,8 @@ class Trainer(object):
         main = torch.cuda.current_stream()
         for cs in comm:   # forked from the origin stream at the start (graph capture: never from a lane)
             cs.wait_stream(main)
+        for o in (self.optimizerDs[-1], self.optimizerG) if comm else ():
+            o.comm_origin = main
         words, sent, attrs, unpair = emb if emb is not None else self.encode_text(batch)
         Fn.stamp('text encode')
         class_labels = None
@@ -543,6 +560,13 @@ class Trainer(object):
             # stage 2-3 Cum_Block / image branches on D64's lane, idle until d_update forks
             gen.side_stream = self._side_streams(len(self.netsD) + 1, fork=False)[0] if GEN_SIDE else None
         fake_imgs = self.netG(noise, sent, attn_attr_emb)
+        if getattr(gen, 'side_stream', None) is not None:
+            # the generator's gradients are zeroed now (nothing before g_update
+            # writes them), so g_update's backward nodes on the branch's lane can
+            # start as soon as their input gradients are ready -- beside the
+            # largest discriminator's update -- instead of after it
+            self.zero_grad_G()
+            self._g_zeroed = True
         Fn.stamp('ATTR + G forward')
         _, _, match_labels = prepare_labels(B, dev)
         cls_ids = batch.get('cls_ids')  # train.py:490 passes class ids to DAMSM_loss even without USE_CLASS

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 12  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
+#define EEGAN_ABI_VERSION 13  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
                                 4: rectangular (local x global) DAMSM words / sentence blocks on MFMA;
                                 5: GlobalAttentionGeneral (eegan_gag_*), words backward reuses the forward's prep;
                                 6: device input pipeline (eegan_pipe_*);
@@ -36,7 +36,8 @@ extern "C" {
                                 9: SyncBN peer-write all-reduce (eegan_peer_*);
                                 10: FID generator-sample input (eegan_fid_samples);
                                 11: BN forward with the finalize folded in (eegan_bnmod_fwd_fin);
-                                12: ScaleAdd double backward in one pass (eegan_scale_dot_res) */
+                                12: ScaleAdd double backward in one pass (eegan_scale_dot_res);
+                                13: split-K counters in the conv descriptor, for the in-kernel split-K finish */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
@@ -69,6 +70,13 @@ typedef struct eegan_conv_desc {
   int stride, pad_h, pad_w;
   int up2;              /* 1: input is nearest-2x upsampled on the fly (F.interpolate(x, 2)) */
   int Ho, Wo, ldy;      /* output grid and channel stride */
+  /* optional (ABI 13): zero-initialised int counters the forward / data-gradient kernels may use to
+   * finish a split-K launch inside the kernel (the last-arriving split of each output tile sums the
+   * partials in split order and applies the epilogue -- no separate reduce launch); every counter
+   * used is zero again when the launch completes.  Launches that may run concurrently need disjoint
+   * arrays (one per stream).  NULL: split-K launches reduce in a second kernel. */
+  int* splitk_ctr;
+  int splitk_ctr_n;
 } eegan_conv_desc;
 
 /* elements of the packed bf16 weight image (rows padded to 128, each tap's channel run to 32) */

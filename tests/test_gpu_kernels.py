@@ -209,6 +209,54 @@ def test_splitk_reduce_vector_path_bit_identical(gpu, monkeypatch):
             assert torch.equal(a, c)
 
 
+def test_splitk_fused_finish_bit_identical(gpu, monkeypatch):
+    """The in-kernel split-K finish (eegan_conv_desc.splitk_ctr; the last-
+    arriving split of each tile sums the sc1-written partials in split order)
+    against the separate reduce launch (EEGAN_CONV splitk_fused=0): torch.equal
+    over forward and backward-data epilogues (bias / act / residual, gate,
+    half-resolution residual, stride-2 parity classes), repeated launches and
+    two streams at once; every counter is back at zero afterwards."""
+    Fn, T, _ = _mods()
+    conv_knob(monkeypatch, 'target', '4096')
+    conv_knob(monkeypatch, 'mink', '2')
+    lrelu = Fn.ACT_CODES['lrelu']
+
+    def run(x, Wt, b, g, gam, res, dz, gate, halfres):
+        return [Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, res=res, gamma=gam).float().cpu(),
+                Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, out_f32=True).cpu(),
+                Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), gate=gate, gate_act=lrelu).float().cpu(),
+                Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), res=halfres, res_up2=1, res_scale=0.25).float().cpu()]
+
+    side = torch.cuda.Stream()
+    for N, Cin, H, W, Cout, k, st, pad in [(2, 256, 4, 4, 128, 3, 1, 1), (2, 96, 8, 8, 64, 4, 2, 1),
+                                            (16, 512, 4, 4, 512, 3, 1, 1), (4, 512, 8, 8, 512, 4, 2, 1)]:
+        torch.manual_seed(N * Cin + Cout)
+        g = Fn.Geom(Cout, k, k, st, pad, pad, 0)
+        x = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        Wt = (torch.randn(Cout, Cin, k, k) * 0.05).to(gpu)
+        b = torch.randn(Cout).to(gpu)
+        gam = torch.tensor([0.7]).to(gpu)
+        Ho, Wo = g.out_hw(H, W)
+        args = (x, Wt, b, g, gam, _nhwc(torch.randn(N, Cout, Ho, Wo), gpu), _nhwc(torch.randn(N, Cout, Ho, Wo), gpu),
+                _nhwc(torch.randn(N, Cin, H, W), gpu), _nhwc(torch.randn(N, Cin, H // 2, W // 2), gpu))
+        conv_knob(monkeypatch, 'splitk_fused', '0')
+        ref = run(*args)
+        conv_knob(monkeypatch, 'splitk_fused', '1')
+        for rep in range(2):
+            for a_, c_ in zip(ref, run(*args)):
+                assert torch.equal(a_, c_), (N, Cin, Cout, k, rep)
+        with torch.cuda.stream(side):   # a second lane with its own counters, concurrently
+            side.wait_stream(torch.cuda.default_stream())
+            o_side = run(*args)
+        o_main = run(*args)
+        torch.cuda.synchronize()
+        for a_, c_, e_ in zip(ref, o_side, o_main):
+            assert torch.equal(a_, c_) and torch.equal(a_, e_)
+    assert len(Fn._SPLITK_CTR) >= 2
+    for ctr in Fn._SPLITK_CTR.values():
+        assert int(ctr.abs().sum()) == 0
+
+
 @pytest.mark.parametrize('target', ['512', '4096'])
 def test_conv_wide_stages_bit_identical(gpu, monkeypatch, target):
     """Wide pair stages (one 64-channel stage of whole 128-B lines per K-step

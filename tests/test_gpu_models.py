@@ -975,6 +975,34 @@ def test_config_step_graph_matches_eager(gpu, cfg):
         assert torch.equal(a, b)
 
 
+def test_step_deterministic_with_lanes(gpu):
+    """The C2 step on its stream lanes is deterministic run to run: three
+    fresh trainers from the same seeds end two eager steps with identical
+    parameters and Adam moments.  (The generator branch's lane once
+    accumulated its first parameter gradients before the main stream's zero
+    fill could land -- a race that showed as run-to-run differences only;
+    Trainer.zero_grad_G orders the fill before the lane.)"""
+    import bench
+    from eegan_hip.synthetic import make_batch
+    ref = None
+    for r in range(3):
+        T, B, ncls = bench.build('C2', gpu, sim_coe=0.05)
+        assert T.use_streams
+        batch = make_batch(B, gpu, seed=11, class_num=ncls, with_class=True)
+        noise = seeded_tensor('graph:noise', (B, 100), 1).to(gpu)
+        for _ in range(2):
+            T.train_step(batch, noise=noise)
+        torch.cuda.synchronize()
+        st = torch.cat([o.flat for o in [T.optimizerG] + list(T.optimizerDs)] +
+                       [o.v for o in [T.optimizerG] + list(T.optimizerDs)])
+        if ref is None:
+            ref = st
+        else:
+            print('DETERMINISM run %d max |diff| %.3e' % (r, float((st - ref).abs().max())))
+            assert torch.equal(st, ref), r
+        del T
+
+
 def test_damsm_grad_early_trains_attr_enhance(gpu, monkeypatch):
     """The DAMSM branch differentiated on its own lane (trainer.DAMSM_GRAD_EARLY,
     the default) must give ATTR_Enhance the same gradient as the joint
