@@ -495,23 +495,71 @@ __global__ void bnmod_bwd_sums_kernel(const double* __restrict__ tmp, int N, int
 }
 
 // ------------------------------------------------------ backward, pass 2 --
+// The dx pass keeps round 4's scalar form: a packed-fp32 rewrite (v_pk_*, 32-bit
+// offsets, four blocks per CU) was 15-25 % faster in isolation but made the
+// generator's backward on two streams (Gen.forward_branched) non-deterministic
+// run to run -- identical forward, the block-5 conv_c1 gradient different in ~1
+// of 5 repetitions under a concurrent lane (tools/gen_determinism.py; the scalar
+// form: 0 of 117) -- and the cause was not found, so it is not shipped.
+struct ChanParamsS {
+  float mean[8], istd[8], pm[8], pa[8];  // mode 0: w, b ; mode 1: gam[n], bet[n]
+};
+
+EE_DEV void load_params_s(const ModArgs& a, int n, int c0, ChanParamsS& q) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = min(c0 + j, a.C - 1);
+    q.mean[j] = a.stats[c];
+    q.istd[j] = a.stats[a.C + c];
+    if (a.mode == 0) {
+      q.pm[j] = a.w ? a.w[c] : 1.f;
+      q.pa[j] = a.b ? a.b[c] : 0.f;
+    } else {
+      q.pm[j] = a.gam[(long)n * a.C + c];
+      q.pa[j] = a.bet[(long)n * a.C + c];
+    }
+  }
+}
+
+EE_DEV void coeffs_s(const ModArgs& a, const ChanParamsS& q, int j, float m, float& mul, float& add) {
+  if (a.mode == 0) {
+    mul = q.pm[j];
+    add = q.pa[j];
+  } else {
+    mul = q.pm[j] * m + 1.f;
+    add = q.pa[j] * m;
+  }
+}
+
+EE_DEV void unpack8_s(uint4 v, float (&f)[8]) {
+  const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[2 * j] = lo_f(w4[j]);
+    f[2 * j + 1] = hi_f(w4[j]);
+  }
+}
+
+EE_DEV void store8_s(bf16_t* dst, const float (&o)[8], int nvalid) {
+  if (nvalid >= 8) {
+    *reinterpret_cast<uint4*>(dst) = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < nvalid) dst[j] = f2bf(o[j]);
+  }
+}
+
 // dx (physical input grid) = istd * (dxhat - mean(dxhat) - xhat*mean(dxhat*xhat)), summed
 // over the 2x2 children when the forward upsampled.  grid (chunks, N) over
 // input pixels of sample n.
 // DXU input pixels x NCH (1, or the 4 upsampled) output children per iteration, loads first
 template <int DXU, int NCH>
 EE_DEV void bwd_dx_body(const ModArgs& a, const bf16_t* __restrict__ dt, int lddt, bf16_t* __restrict__ dx, int lddx,
-                        int ppc, const ChanParams& P, const f2_t (&vg)[4], const f2_t (&m1)[4], const f2_t (&m2)[4],
+                        int ppc, const ChanParamsS& P, const float (&vg)[8], const float (&m1)[8], const float (&m2)[8],
                         int n, int c0, int nv, int row, int rows, int q1) {
-  const int Wo = a.W << a.up2;
+  const int Ho = a.H << a.up2, Wo = a.W << a.up2;
   const int HW = a.H * a.W;
-  const int wish = a.wsh >= 0 ? a.wsh - a.up2 : -1;   // log2 of the input width
-  const bf16_t* xs = a.x + (unsigned)(n * HW) * (unsigned)a.ldx + c0;
-  const bf16_t* gs = dt + (unsigned)(n * (HW << (2 * a.up2))) * (unsigned)lddt + c0;
-  const float* ms = a.mask + (long)n * (HW << (2 * a.up2));
-  bf16_t* ds = dx + (unsigned)(n * HW) * (unsigned)lddx + c0;
-  const float ns = a.nslope;
-  const bool ssa = a.mode == 1;
   for (int qb = (int)blockIdx.x * ppc + row; qb < q1; qb += DXU * rows) {
     uint4 xr[DXU], gr[DXU][NCH];
     float mr[DXU][NCH];
@@ -519,22 +567,16 @@ EE_DEV void bwd_dx_body(const ModArgs& a, const bf16_t* __restrict__ dt, int ldd
     for (int u = 0; u < DXU; ++u) {
       const int q = qb + u * rows;
       if (q < q1) {
-        xr[u] = *reinterpret_cast<const uint4*>(xs + (unsigned)q * (unsigned)a.ldx);
-        int iy = 0, ix = q;
-        if (NCH > 1) {
-          if (wish >= 0) {
-            iy = q >> wish;
-            ix = q & (a.W - 1);
-          } else {
-            iy = (unsigned)q / (unsigned)a.W;
-            ix = q - iy * a.W;
-          }
-        }
+        const int iy = (unsigned)q / (unsigned)a.W, ix = q - iy * a.W;
+        xr[u] = *reinterpret_cast<const uint4*>(a.x + ((long)n * HW + q) * a.ldx + c0);
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
-          const int op = NCH > 1 ? ((iy << a.up2) + (ch >> 1)) * Wo + (ix << a.up2) + (ch & 1) : q;
-          gr[u][ch] = *reinterpret_cast<const uint4*>(gs + (unsigned)op * (unsigned)lddt);
-          mr[u][ch] = ssa ? ms[op] : 0.f;
+          {
+            const int oy = (iy << a.up2) + (ch >> 1), ox = (ix << a.up2) + (ch & 1);
+            const long op = ((long)n * Ho + oy) * Wo + ox;
+            gr[u][ch] = *reinterpret_cast<const uint4*>(dt + op * lddt + c0);
+            mr[u][ch] = a.mode == 1 ? a.mask[op] : 0.f;
+          }
         }
       }
     }
@@ -542,32 +584,34 @@ EE_DEV void bwd_dx_body(const ModArgs& a, const bf16_t* __restrict__ dt, int ldd
     for (int u = 0; u < DXU; ++u) {
       const int q = qb + u * rows;
       if (q >= q1) break;
-      f2_t xh[4], o[4];
-      unpack8(xr[u], xh);
+      float xh[8], o[8];
+      unpack8_s(xr[u], xh);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        xh[k] = (xh[k] - P.mean[k]) * P.istd[k];
-        o[k] = splat2(0.f);
+      for (int j = 0; j < 8; ++j) {
+        xh[j] = (xh[j] - P.mean[j]) * P.istd[j];
+        o[j] = 0.f;
       }
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
-        f2_t gv[4];
-        unpack8(gr[u][ch], gv);
-        const f2_t mm = splat2(mr[u][ch]);
+        float gv[8];
+        unpack8_s(gr[u][ch], gv);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const f2_t mul = ssa ? P.pm[k] * mm + splat2(1.f) : P.pm[k];
-          const f2_t add = ssa ? P.pa[k] * mm : P.pa[k];
-          const f2_t g = gact2(gv[k], xh[k] * mul + add, ns);
-          o[k] += P.istd[k] * (g * mul - m1[k] - vg[k] * xh[k] * m2[k]);
+        for (int j = 0; j < 8; ++j) {
+          float mul, add;
+          coeffs_s(a, P, j, mr[u][ch], mul, add);
+          const float tv = xh[j] * mul + add;
+          float g = gv[j];
+          if (a.act == ACT_RELU) g = tv > 0.f ? g : 0.f;
+          else if (a.act == ACT_LRELU) g = tv > 0.f ? g : g * a.slope;
+          o[j] += P.istd[j] * (g * mul - m1[j] - vg[j] * xh[j] * m2[j]);
         }
       }
-      store8(ds + (unsigned)q * (unsigned)lddx, o, nv);
+      store8_s(dx + ((long)n * HW + q) * lddx + c0, o, nv);
     }
   }
 }
 
-__global__ __launch_bounds__(NT, 4) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_t* __restrict__ dt, int lddt,
+__global__ __launch_bounds__(NT) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_t* __restrict__ dt, int lddt,
                                                           const double* __restrict__ chan, double count,
                                                           bf16_t* __restrict__ dx, int lddx, int ppc) {
   const int C8 = (a.C + 7) / 8, rows = NT / C8;
@@ -575,18 +619,18 @@ __global__ __launch_bounds__(NT, 4) void bnmod_bwd_dx_kernel(ModArgs a, const bf
   if (row >= rows) return;
   const int n = blockIdx.y, c0 = cg * 8, nv = a.C - c0;
   const int q1 = min(a.H * a.W, ((int)blockIdx.x + 1) * ppc);
-  ChanParams P;
-  load_params(a, n, c0, P);
-  f2_t vg[4], m1[4], m2[4];
+  ChanParamsS P;
+  load_params_s(a, n, c0, P);
+  float vg[8], m1[8], m2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = min(c0 + j, a.C - 1);
-    vg[j >> 1][j & 1] = a.stats[2 * a.C + c];
-    m1[j >> 1][j & 1] = (float)(chan[c] / count);
-    m2[j >> 1][j & 1] = (float)(chan[a.C + c] / count);
+    vg[j] = a.stats[2 * a.C + c];
+    m1[j] = (float)(chan[c] / count);
+    m2[j] = (float)(chan[a.C + c] / count);
   }
-  if (a.up2) bwd_dx_body<1, 4>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
-  else bwd_dx_body<2, 1>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
+  if (a.up2) bwd_dx_body<2, 4>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
+  else bwd_dx_body<4, 1>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
 }
 
 ModArgs make_args(const eegan_bnmod_desc* d) {

@@ -761,6 +761,27 @@ class AvgPool2AdjFn(torch.autograd.Function):
         return AvgPool2Fn.apply(_as_bf16_grad(gg))
 
 
+class StreamHandoffFn(torch.autograd.Function):
+    """Identity at a point where a tensor made on one stream is read on the
+    current one (the generator's branch lane, models.Gen.forward_branched).
+    Its backward runs on the current (reading) stream and produces the
+    gradient that the OTHER stream's backward consumes: the gradient is
+    recorded on that stream, so the caching allocator does not hand its memory
+    to this stream's next allocation before the other stream's queued reads
+    ran (autograd orders the streams, it does not guard the memory)."""
+
+    @staticmethod
+    def forward(ctx, x, other):
+        ctx.other = other
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is not None and g.is_cuda:
+            g.record_stream(ctx.other)
+        return g, None
+
+
 class Upsample2Fn(torch.autograd.Function):
     """F.interpolate(x, scale_factor=2) (nearest); adjoint = 2x2 sum-pool."""
 

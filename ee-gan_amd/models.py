@@ -301,34 +301,38 @@ class Gen(nn.Module):
         the stream of their forward (autograd), so the generator's backward
         splits the same way."""
         main, side = torch.cuda.current_stream(), self.side_stream
-        # tensors made on one stream and read on the other are recorded on the reader:
-        # they are saved for backward, and when a backward node on one stream frees
-        # the last reference the caching allocator must not hand the memory to the
-        # other stream's next allocation before this stream's queued reads ran
+        # Every tensor crossing between the streams is (1) recorded on its reader, since
+        # it is saved for backward and the last reference may drop on the other stream,
+        # and (2) read through Fn.StreamHandoffFn, whose backward records the gradient
+        # flowing back across on the stream that consumes it: the caching allocator
+        # must not hand either memory to the producing stream's next allocation
+        # before the other stream's queued reads ran.
+        hand = Fn.StreamHandoffFn.apply
         x_32.record_stream(side)
         u_64 = None
         if GEN_SIDE_U64:
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                u_64 = self.cum_64.up(x_32)
+                u_64 = self.cum_64.up(hand(x_32, main))
         x_64, stage_mask = self.SAGB_progress(x_32, [sent, attrs], stage_mask, 64, self.blocks[4], gb[4])
         x_64.record_stream(side)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            cum_x_64 = self.cum_64.fuse(u_64 if u_64 is not None else self.cum_64.up(x_32), x_64)
+            cum_x_64 = self.cum_64.fuse(u_64 if u_64 is not None else self.cum_64.up(hand(x_32, main)),
+                                        hand(x_64, main))
             img_64 = self.get_image_64(cum_x_64)
             u_128 = self.cum_128.up(cum_x_64)
         x_128, stage_mask = self.SAGB_progress(x_64, [sent, attrs], stage_mask, 128, self.blocks[5], gb[5])
         x_128.record_stream(side)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            cum_x_128 = self.cum_128.fuse(u_128, x_128)
+            cum_x_128 = self.cum_128.fuse(u_128, hand(x_128, main))
             img_128 = self.get_image_128(cum_x_128)
             u_256 = self.cum_256.up(cum_x_128)
         x_256, _ = self.SAGB_progress(x_128, [sent, attrs], stage_mask, 256, self.blocks[6], gb[6])
         main.wait_stream(side)
         u_256.record_stream(main)
-        cum_x_256 = self.cum_256.fuse(u_256, x_256)
+        cum_x_256 = self.cum_256.fuse(hand(u_256, side), x_256)
         img_256 = self.get_image_256(cum_x_256)
         return [img_64, img_128, img_256]
 

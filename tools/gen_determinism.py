@@ -35,8 +35,14 @@ def main():
     rs = [seeded_tensor('g:r%d' % k, (16, 3, 64 << k, 64 << k), 2).to(dev) for k in range(3)]
     G.side_stream = None if args.single else torch.cuda.Stream()
     ref, bad = None, 0
+    bg = torch.cuda.Stream()
+    big = torch.randn(32 << 20, device=dev)
     for r in range(args.reps):
         G.zero_grad(set_to_none=True)
+        if args.load:   # a stream hammering memory beside the whole pass
+            with torch.cuda.stream(bg):
+                for _ in range(60):
+                    big.mul_(1.0000001)
         imgs = G(z, s, a)
         loss = sum((im.float() * rk).sum() for im, rk in zip(imgs, rs))
         loss.backward()
@@ -50,6 +56,13 @@ def main():
         diff = sorted(((float((gr[n] - ref[0][n]).abs().max()), n) for n in gr), reverse=True)
         nb = sum(1 for e, _ in diff if e > 0)
         if nb or any(dimg):
+            if bad == 0:
+                same = sorted({n.rsplit('.', 1)[0].split('.affine')[0] for e, n in diff if e == 0})
+                dif = sorted({n.rsplit('.', 1)[0].split('.affine')[0] for e, n in diff if e > 0})
+                print('gen determinism: identical modules %s' % same)
+                print('gen determinism: differing modules %s' % dif)
+                print('gen determinism: blocks.5/6 params: %s' % ['%s %s' % (n, 'DIFF' if e > 0 else 'same')
+                                                             for e, n in diff if n.startswith(('blocks.5', 'blocks.4.c2', 'blocks.4.gamma'))])
             bad += 1
             print('gen determinism rep %d: images max|d| %s; %d params differ, top %s' % (
                 r, ['%.1e' % d for d in dimg], nb, ', '.join('%s %.1e' % (n, e) for e, n in diff[:6])), flush=True)
