@@ -1466,6 +1466,195 @@ __global__ __launch_bounds__(64 * WPX, NBUF == 1 ? (TH == 4 ? 3 : 2) : 1) void c
 }
 
 
+// ------------------- 3x3 stride-1 convs on 64 input channels: resident weights --
+// conv_halo3_kernel for the 64-channel inputs (D256's 64-ch 128^2 resD conv, the
+// generator's 64-ch layers and their data gradients), where its per-slice
+// weight slabs (9 taps x 64 x 32, 37 KB) outweigh the halo (13 KB) 3 : 1.  Here
+// a workgroup stages ALL 9 x 64 x 64 weights of its output-channel tile once
+// (72 KB, resident for its lifetime) and walks TPB horizontally consecutive
+// 4 x 32-pixel tiles; per tile only the 6 x 34 source halo moves, as whole
+// 128-B lines (64 channels of a pixel = one line, against the half-line 64-B
+// pieces of 32-channel slices), double-buffered: tile k + 1's halo streams in
+// under tile k's 144 MFMAs per wave.  LDS: 72 KB weights + 2 x 32 KB buffers
+// (halo, then that tile's fp32 epilogue tile) -- one workgroup per CU.
+// 16-B chunk q of a 128-B row r (halo column / weight row) sits at slot
+// q ^ (r & 6): conflict-free ds_read_b128 for any 16 consecutive rows in
+// gfx950's b128 lane groups (brute-forced over all window starts, both 32-
+// channel halves); a fragment read is a base register (tap column shift x
+// channel half) + an immediate.  K order as conv_halo3_kernel (32-channel half
+// outer, tap inner): the same bits.  Host-checked: Cgp == Cvalid == 64, Mrows
+// % 64 == 0 (every thread stores exactly NIT chunks per tile, which the
+// counted wait at the next tile's top relies on).
+template <int MODE>
+__global__ __launch_bounds__(256, 1) void conv_halo3r_kernel(ConvArgs a, long src_bytes, long w_bytes, int tpb) {
+  constexpr int NT = 256, TH = 4, TW = HALO_TW, TCO = HALO_TCO, FI = TCO / 16, CB = TW / 16, FJ = CB;
+  constexpr int HW2 = TW + 2, HP = (TH + 2) * HW2, HOPS = (HP * 8 + NT - 1) / NT;
+  constexpr int WSL = 9 * TCO * 8, WOPS = WSL / NT, WBYTES = WSL * 16;
+  constexpr int TPIX = TH * TW, NCK = TCO / 4, NIT = TPIX * (TCO / 8) / NT;
+  constexpr int BUFB = TPIX * TCO * 4;   // 32 KB: >= the halo's HOPS * NT * 16 (28 KB)
+  static_assert(HOPS * NT * 16 <= BUFB && WSL % NT == 0 && NIT == 4, "halo3r tile");
+  __shared__ __attribute__((aligned(16))) char lds[WBYTES + 2 * BUFB];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wj = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_x = a.OW / TW, tiles_y = a.OH / TH, ntiles = a.N * tiles_x * tiles_y;
+  const int t0 = blockIdx.x * tpb, t1 = min(ntiles, t0 + tpb);
+  const int co0 = blockIdx.y * TCO;
+  const int lds0 = (int)(uintptr_t)(lds_void_t*)lds;
+  const rsrc_t rs_src = make_rsrc(a.src, src_bytes);
+  const rsrc_t rs_w = make_rsrc(a.wp, w_bytes);
+  const int PH = a.IH >> a.up2, PW = a.IW >> a.up2;
+
+  // weights once: slot L = (tap, row, chunk q) holds source chunk q ^ (row & 6)
+#pragma unroll
+  for (int i = 0; i < WOPS; ++i) {
+    const int L = i * NT + tid, t = L / (TCO * 8), rem = L - t * (TCO * 8);
+    const int row = rem >> 3, q = (rem & 7) ^ (row & 6);
+    lds_dma16s(rs_w, lds0 + (i * NT + wj * 64) * 16, (unsigned)(((co0 + row) * a.Kw + t * 64 + q * 8) * 2), 0);
+  }
+  auto issue_halo = [&](int tile, int buf) {
+    int b = tile;
+    const int tx = b % tiles_x;
+    b /= tiles_x;
+    const int ty = b % tiles_y, n = b / tiles_y;
+    const int oy0 = ty * TH, ox0 = tx * TW;
+#pragma unroll
+    for (int i = 0; i < HOPS; ++i) {
+      const int L = i * NT + tid, h = L >> 3;
+      const int hy = h / HW2, hx = h - hy * HW2, q = (L & 7) ^ (hx & 6);
+      const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
+      const unsigned off = (h < HP && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW)
+                               ? (unsigned)((((n * PH + (iy >> a.up2)) * PW + (ix >> a.up2)) * a.lds_src + q * 8) * 2)
+                               : OOB;
+      lds_dma16s(rs_src, lds0 + WBYTES + buf * BUFB + (i * NT + wj * 64) * 16, off, 0);
+    }
+  };
+
+  const int fr = lane & 15, fq = lane >> 4;
+  // A fragment (row i * 16 + fr, chunk kh * 4 + fq) of tap t: wbase[kh] + t * 8192 + i * 2048
+  int wbase[2];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) wbase[kh] = fr * 128 + (((kh * 4 + fq) ^ (fr & 6)) << 4);
+  // B fragment (halo row wj + oyh + 0, column block jc, tap column shift sx, half kh):
+  // hbase[sx][kh] + (wj + oyh) * HW2 * 128 + jc * 2048 (columns c and c + 16 share the swizzle)
+  int hbase[3][2];
+#pragma unroll
+  for (int sx = 0; sx < 3; ++sx)
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+      hbase[sx][kh] = (wj * HW2 + fr + sx) * 128 + (((kh * 4 + fq) ^ ((fr + sx) & 6)) << 4);
+
+  // this thread's epilogue chunk: output channels co0 + 8e .. + 7 of pixels p = (k * NT + tid) / 8
+  const int e = tid & 7, co = co0 + 8 * e;
+  float bias8[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) bias8[r] = a.bias ? a.bias[co + r] : 0.f;
+  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
+
+  if (t0 < t1) issue_halo(t0, 0);
+  for (int tile = t0, k = 0; tile < t1; ++tile, ++k) {
+    int b = tile;
+    const int tx = b % tiles_x;
+    b /= tiles_x;
+    const int ty = b % tiles_y, n = b / tiles_y;
+    const int oy0 = ty * TH, ox0 = tx * TW;
+    const int buf = k & 1;
+    // this tile's gate / residual chunks first (their latency runs under the MFMAs; loads
+    // issued before the next halo, so the epilogue's wait for them does not wait for it)
+    uint4 gpre[NIT], rpre[NIT];
+#pragma unroll
+    for (int j = 0; j < NIT; ++j) {
+      const int p = (j * NT + tid) >> 3;
+      const int y = oy0 + p / TW, x = ox0 + p % TW;
+      const long gp = ((long)n * a.OH + y) * a.OW + x;
+      gpre[j] = rpre[j] = make_uint4(0, 0, 0, 0);
+      if (MODE == MODE_BWDD && a.gate) gpre[j] = *reinterpret_cast<const uint4*>(a.gate + gp * a.ldgate + co);
+      if (a.res) {
+        const long rp = a.res_up2 ? ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1) : gp;
+        rpre[j] = *reinterpret_cast<const uint4*>(a.res + rp * a.ldres + co);
+      }
+    }
+    // tile k's halo landed (and at k = 0 the weights): every older piece of this wave but
+    // the previous tile's NIT output stores, then the barrier for every wave's pieces
+    if (k == 0) wait_vmcnt_barrier<0>();
+    else wait_vmcnt_barrier<NIT>();
+    if (tile + 1 < t1) issue_halo(tile + 1, buf ^ 1);   // that buffer's last readers passed the barrier
+
+    f32x4_t acc[FI][FJ];
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const char* hb = lds + WBYTES + buf * BUFB;
+    auto rd = [&](int kh, int t, bf16x8_t (&fa)[FI], bf16x8_t (&fb)[FJ]) {
+      const int ta = t / 3, tb = t - ta * 3;
+      const int oyh = MODE == MODE_FWD ? ta : 2 - ta, oxh = MODE == MODE_FWD ? tb : 2 - tb;
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+        fa[i] = as_frag(*reinterpret_cast<const uint4*>(lds + wbase[kh] + t * (TCO * 128) + i * 2048));
+#pragma unroll
+      for (int j = 0; j < FJ; ++j)
+        fb[j] = as_frag(*reinterpret_cast<const uint4*>(hb + hbase[oxh][kh] + oyh * (HW2 * 128) + j * 2048));
+    };
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      bf16x8_t fa[2][FI], fb[2][FJ];
+      rd(kh, 0, fa[0], fb[0]);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (t + 1 < 9) rd(kh, t + 1, fa[(t + 1) & 1], fb[(t + 1) & 1]);
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+#pragma unroll
+          for (int j = 0; j < FJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t & 1][i], fb[t & 1][j], acc[i][j], 0, 0, 0);
+      }
+    }
+    // epilogue through this tile's buffer (every wave is done with its halo): fp32 tile
+    // [pixel][16 chunks of 4 channels], chunk c of pixel p at c ^ (p & 15)
+    __syncthreads();
+    float4* st = reinterpret_cast<float4*>(lds + WBYTES + buf * BUFB);
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const int p = wj * TW + j * 16 + fr;
+#pragma unroll
+      for (int i = 0; i < FI; ++i) {
+        const int c = i * 4 + fq;
+        st[p * NCK + (c ^ (p & 15))] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NIT; ++j) {
+      const int p = (j * NT + tid) >> 3;
+      const float4 lo = st[p * NCK + ((2 * e) ^ (p & 15))];
+      const float4 hi = st[p * NCK + ((2 * e + 1) ^ (p & 15))];
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = act_fwd(v[r] + bias8[r], a.act, a.slope);
+      if (MODE == MODE_BWDD && a.gate) {
+        const uint32_t gw[4] = {gpre[j].x, gpre[j].y, gpre[j].z, gpre[j].w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[2 * r] *= act_dgrad_from_y(lo_f(gw[r]), a.gate_act, a.gate_slope);
+          v[2 * r + 1] *= act_dgrad_from_y(hi_f(gw[r]), a.gate_act, a.gate_slope);
+        }
+      }
+      if (a.res) {
+        const uint32_t rw[4] = {rpre[j].x, rpre[j].y, rpre[j].z, rpre[j].w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[2 * r] = res_combine(a.res_scale, lo_f(rw[r]), gam, v[2 * r]);
+          v[2 * r + 1] = res_combine(a.res_scale, hi_f(rw[r]), gam, v[2 * r + 1]);
+        }
+      }
+      const int y = oy0 + p / TW, x = ox0 + p % TW;
+      const long gp = ((long)n * a.OH + y) * a.OW + x;
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + gp * a.ldo + co) =
+          make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+    }
+  }
+}
 
 // ----------------------------- 4x4 / stride-2 forward convs on 32 channels --
 // FWD of the first resD block's 4x4 / stride-2 / pad-1 conv of every D (32 -> 64
@@ -3092,6 +3281,19 @@ int try_halo3(const ConvArgs& a, hipStream_t s, long src_bytes, long w_bytes) {
   if (a.res && ((a.ldres & 7) || ((uintptr_t)a.res & 15))) return 0;
   if (a.OW % HALO_TW || a.OH % 8 || a.OH != a.IH || a.OW != a.IW) return 0;
   const int co_t = ee_cdiv(a.Mrows, HALO_TCO);
+  if (a.Cgp == 64 && a.Cvalid == 64 && a.Mrows % HALO_TCO == 0 && knob("halo_r", 1)) {
+    // 64-channel inputs: resident weights, TPB consecutive tiles per workgroup (grid ~ 2 per CU)
+    const long tiles = (long)a.N * (a.OH / 4) * (a.OW / HALO_TW);
+    int tpb = knob("halo_r_tpb", 0);
+    if (tpb <= 0) {
+      const long t = tiles * co_t / 512;
+      tpb = t < 1 ? 1 : t > 16 ? 16 : (int)t;
+    }
+    const dim3 grid((unsigned)ee_cdiv(tiles, (long)tpb), co_t);
+    ee_launch(conv_halo3r_kernel<MODE>, grid, dim3(256), 0, s, a, src_bytes, w_bytes, tpb);
+    const int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd(halo3r)" : "conv_bwd_data(halo3r)");
+    return rc ? rc : 1;
+  }
   const long tiles16 = a.OH % 16 ? 0 : (long)a.N * (a.OH / 16) * (a.OW / HALO_TW) * co_t;
   const int big = knob("halo_th", 0);   // 16 / 8: force the tile height (tests, sweeps)
   const bool th16 = big == 16 || (big != 8 && tiles16 >= 256);

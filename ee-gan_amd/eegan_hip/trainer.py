@@ -66,6 +66,25 @@ GEN_SIDE = True
 # backward kernels do not queue behind the reductions; each optimizer's step
 # waits for its lane (FlatAdam.comm_stream).  Module constant for A/B.
 COMM_LANES = True
+# EEGAN_DREAL_EARLY: discriminators (comma-separated indices, '' = none) whose
+# real-image share of d_loss -- the real and mismatch heads, train.py:338-341 /
+# 357-364, which read the real images, the text embeddings and D's weights as
+# they are at the step's start, nothing the generator makes -- is computed and
+# back-propagated on the D's lane right after the text encoder, beside the
+# generator's forward; d_update then only adds the fake-image share before the
+# first Adam step.  d_loss is a sum over the three heads, so the gradient is the
+# same sum in another accumulation order.
+DREAL_EARLY = tuple(int(i) for i in os.environ.get('EEGAN_DREAL_EARLY', '').split(',') if i.strip())
+# EEGAN_DREAL_LANE: 'own' (the D's lane) or 'damsm' (the DAMSM lane, joined by the
+# origin stream before d_update forks)
+DREAL_LANE = os.environ.get('EEGAN_DREAL_LANE', 'own')
+# EEGAN_LANE_GATE: 'i:j:phase,...' -- D i's lane is forked from the origin stream only
+# once D j's lane has issued `phase` (one of LANE_PHASES), so its kernels do not share
+# the GPU with D j's earlier phases (A/B of the lanes' overlap; '' = all lanes forked
+# together at d_update's start)
+LANE_PHASES = ('loss', 'adam', 'gp', 'gpadam', 'gterm')
+LANE_GATE = {int(g.split(':')[0]): (int(g.split(':')[1]), g.split(':')[2])
+             for g in os.environ.get('EEGAN_LANE_GATE', '').split(',') if g.strip()}
 
 # a g_update term already differentiated w.r.t. its fake image on its lane
 # (GTERM_GRAD_EARLY): its value, the image alias and the gradient there
@@ -220,6 +239,46 @@ class Trainer(object):
         return errD_real, errD_fake, errD_mismatch, errD_real_class, errD_fake_class, errD_mismatch_class
 
     @staticmethod
+    def d_loss_real(imgs, sent_emb, wrong_sent_emb, class_labels, netD, disc_class):
+        """The real-image heads of d_loss / d_loss_class (train.py:338-341,
+        357-364): (errD_real, errD_mismatch[, errD_real_class, errD_mismatch_class])
+        from ONE pass of D over the real images."""
+        B = imgs.shape[0]
+        feat = netD(imgs)
+        heads = Fn.BatchCatFn.apply(feat, feat)   # [real; real]: sentence / mismatched sentence
+        cond = torch.cat([sent_emb.reshape(B, -1), wrong_sent_emb.reshape(B, -1)], 0)
+        out = netD.module.COND_DNET(heads, cond)
+        if disc_class:
+            s, c = out
+            return (Fn.DoutReduceFn.apply(s[:B], 0), Fn.DoutReduceFn.apply(s[B:], 1),
+                    Fn.BceLogitsFn.apply(c[:B], class_labels), Fn.BceLogitsFn.apply(c[B:], class_labels))
+        return Fn.DoutReduceFn.apply(out[:B], 0), Fn.DoutReduceFn.apply(out[B:], 1)
+
+    @staticmethod
+    def d_loss_fake(fake_imgs, sent_emb, class_labels, netD, disc_class):
+        """The fake-image head of d_loss / d_loss_class (train.py:342-344,
+        365-368): (errD_fake[, errD_fake_class])."""
+        out = netD.module.COND_DNET(netD(fake_imgs.detach()), sent_emb)
+        if disc_class:
+            return Fn.DoutReduceFn.apply(out[0], 1), Fn.BceLogitsFn.apply(out[1], class_labels)
+        return (Fn.DoutReduceFn.apply(out, 1),)
+
+    def d_real_early(self, i, imgs, sent_emb, unpair_sent_emb, class_labels):
+        """D i's real-image share of d_loss, differentiated into its zeroed
+        gradient on the current stream (DREAL_EARLY); returns the head values."""
+        disc_class = self.disc_class and i == 2
+        optD = self.optimizerDs[i]
+        Fn.stamp('D%d real start' % i)
+        vals = self.d_loss_real(imgs[i], sent_emb, unpair_sent_emb, class_labels, self.netsD[i], disc_class)
+        part = vals[0] + vals[1] / 2.0
+        if disc_class:
+            part = part + (vals[2] + vals[3]) / 3.0 * self.d_class_coe
+        optD.zero_grad()
+        part.backward(inputs=optD.params)
+        Fn.stamp('D%d real forward + backward' % i)
+        return tuple(v.detach() for v in vals)
+
+    @staticmethod
     def MA_gradient_penalty(imgs, sent_emb, netD, disc_class):
         """train.py:378-402: 2 * mean(||d D(x,s) / d(x,s)||^6), double backward."""
         interpolated = imgs.detach().requires_grad_()
@@ -273,37 +332,84 @@ class Trainer(object):
 
     # ----------------------------------------------------------- updates --
     def d_update(self, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec=False, g_early=None,
-                 before_join=None):
+                 before_join=None, real=None):
         """train.py:437-469: per D a hinge(+class) step, then a GP step (each D
         on its own stream).  `g_early` (a list): also run g_update's generator
-        loss term through each D right after that D's update, into the list."""
+        loss term through each D right after that D's update, into the list.
+        `real`: {D index: real-image head values} of d_real_early."""
         nD = len(self.netsD)
         streams = self._side_streams(nD)
         g_terms = [None] * nD
         order = range(nD)
         if LANE_ORDER == 'rev':
             order = reversed(order)
-        for i in order:
+        order = list(order)
+        gates = {i: g for i, g in LANE_GATE.items() if i < nD and g[0] < nD and g[0] != i} if self.use_streams else {}
+        gens, pos = {}, {}
+
+        def lane(i):
+            Fn.stamp('D%d start' % i)
+            yield from self._d_update_one(i, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec,
+                                          real=(real or {}).get(i))
+            if g_early is not None:
+                # g_update's pass through this D (train.py:477-489) reads only this D's
+                # final parameters and the fake images: it runs on the lane as soon as
+                # the update is done, while the larger D's update still runs
+                g_terms[i] = self._g_term(i, fake_imgs, sent_emb, class_labels, iter_rec)
+            yield 'gterm'
+
+        def advance(i, until=None):
+            """Issue lane i's phases up to and including `until` (None: all)."""
+            if i not in gens:
+                gens[i], pos[i] = lane(i), -1
+            if until is not None and pos[i] >= LANE_PHASES.index(until):
+                return
             with self._on(streams[i]):
-                Fn.stamp('D%d start' % i)
-                self._d_update_one(i, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec)
-                if g_early is not None:
-                    # g_update's pass through this D (train.py:477-489) reads only this D's
-                    # final parameters and the fake images: it runs on the lane as soon as
-                    # the update is done, while the larger D's update still runs
-                    g_terms[i] = self._g_term(i, fake_imgs, sent_emb, class_labels, iter_rec)
+                for ph in gens[i]:
+                    pos[i] = LANE_PHASES.index(ph)
+                    if ph == until:
+                        return
+
+        # ungated lanes up to the phases other lanes wait for, the DAMSM lane, then each
+        # gated lane forked from the origin stream once its source lane's phase is issued
+        # (a fork from the origin, never lane -> lane: see _comm / FlatAdam._allreduce)
+        for i in order:
+            if i not in gates:
+                need = [LANE_PHASES.index(g[1]) for k, g in gates.items() if g[0] == i]
+                advance(i, LANE_PHASES[min(need)] if need else None)
         if before_join is not None:
             before_join()
+        main = torch.cuda.current_stream()
+        for i in order:
+            if i in gates:
+                j, ph = gates[i]
+                advance(j, ph)
+                main.wait_stream(streams[j])
+                streams[i].wait_stream(main)
+                advance(i)
+        for i in order:
+            advance(i)
         self._join(streams)
         Fn.stamp('d_update joined')
         if g_early is not None:
             g_early[:] = g_terms
 
-    def _d_update_one(self, i, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec):
-        """One D of d_update (train.py:439-466)."""
+    def _d_update_one(self, i, imgs, fake_imgs, sent_emb, unpair_sent_emb, class_labels, iter_rec, real=None):
+        """One D of d_update (train.py:439-466), a generator yielding after each
+        phase (LANE_PHASES) so d_update can fork other lanes behind it; `real`:
+        the real-image heads' values when d_real_early already added their
+        gradient."""
         real_img, fake_img, netD, optD = imgs[i], fake_imgs[i], self.netsD[i], self.optimizerDs[i]
         disc_class = self.disc_class and i == 2
-        if disc_class:
+        if real is not None:
+            # the real-image heads were differentiated by d_real_early: add the fake share
+            fk = self.d_loss_fake(fake_img, sent_emb, class_labels, netD, disc_class)
+            e_real, e_unpair, e_fake = real[0], real[1], fk[0]
+            d_loss = fk[0] / 2.0
+            if disc_class:
+                c_real, c_unpair, c_fake = real[2], real[3], fk[1]
+                d_loss = d_loss + fk[1] / 3.0 * self.d_class_coe
+        elif disc_class:
             e_real, e_fake, e_unpair, c_real, c_fake, c_unpair = self.d_loss_class(
                 real_img, fake_img, sent_emb, unpair_sent_emb, class_labels, netD)
             d_loss = e_real + (e_fake + e_unpair) / 2.0 + (c_real + c_fake + c_unpair) / 3.0 * self.d_class_coe
@@ -311,18 +417,23 @@ class Trainer(object):
             e_real, e_fake, e_unpair = self.d_loss(real_img, fake_img, sent_emb, unpair_sent_emb, netD)
             d_loss = e_real + (e_fake + e_unpair) / 2.0
         Fn.stamp('D%d loss forward' % i)
-        optD.zero_grad()
+        if real is None:
+            optD.zero_grad()
         d_loss.backward(inputs=optD.params)
         Fn.stamp('D%d loss backward' % i)
+        yield 'loss'
         optD.step()
         Fn.stamp('D%d adam' % i)
+        yield 'adam'
         d_loss_gp = self.MA_gradient_penalty(real_img, sent_emb, netD, disc_class)
         Fn.stamp('D%d gp forward + grad' % i)
         optD.zero_grad()
         d_loss_gp.backward(inputs=optD.params)
         Fn.stamp('D%d gp backward' % i)
+        yield 'gp'
         optD.step()
         Fn.stamp('D%d gp adam' % i)
+        yield 'gpadam'
         if iter_rec:
             self.records['errD_%d/real_sent' % i] = e_real.detach()
             self.records['errD_%d/fake_sent' % i] = e_fake.detach()
@@ -553,6 +664,17 @@ class Trainer(object):
             class_labels = prepare_class_labels(B, self.class_nums, batch['cls_ids'], dev)
         if noise is None:
             noise = torch.randn(B, 100, device=dev)
+        real = {}
+        if DREAL_EARLY and self.use_streams:
+            lanes = self._side_streams(len(self.netsD) + 1, fork=False)   # (the full set: never re-created mid-step)
+            for i in DREAL_EARLY:
+                if 0 <= i < len(self.netsD):
+                    # on the D's own lane, or on the DAMSM lane (idle until the generator's
+                    # images exist) with d_update's fork ordered behind it
+                    lane = lanes[i] if DREAL_LANE == 'own' else lanes[-1]
+                    lane.wait_stream(main)
+                    with self._on(lane):
+                        real[i] = self.d_real_early(i, batch['imgs'], sent, unpair, class_labels)
         _, attn_attr_emb = self.attr_enhance(sent, attrs)
         attn_attr_emb = self.attr_enhance.module.attr_merge(attn_attr_emb)
         gen = getattr(self.netG, 'module', self.netG)
@@ -568,6 +690,8 @@ class Trainer(object):
             self.zero_grad_G()
             self._g_zeroed = True
         Fn.stamp('ATTR + G forward')
+        if real and DREAL_LANE != 'own':
+            main.wait_stream(self._side_streams(len(self.netsD) + 1, fork=False)[-1])
         _, _, match_labels = prepare_labels(B, dev)
         cls_ids = batch.get('cls_ids')  # train.py:490 passes class ids to DAMSM_loss even without USE_CLASS
         damsm = []
@@ -580,7 +704,7 @@ class Trainer(object):
             issue_damsm()
         terms = [] if (G_EARLY and self.use_streams) else None
         self.d_update(batch['imgs'], fake_imgs, sent, unpair, class_labels, iter_rec, g_early=terms,
-                      before_join=issue_damsm if early and LANE_ORDER == 'rev' else None)
+                      before_join=issue_damsm if early and LANE_ORDER == 'rev' else None, real=real)
         damsm = damsm or None
         g = self.g_update(fake_imgs, sent, words, attn_attr_emb, cls_ids, B, match_labels, batch['cap_lens'],
                           class_labels, iter_rec, damsm=damsm, terms=terms)

@@ -1009,6 +1009,52 @@ def test_conv_halo3_matches_tile_kernel(gpu, monkeypatch, th):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('tpb', [0, 1, 3, 7])
+def test_conv_halo3r_matches_halo3(gpu, monkeypatch, tpb):
+    """64-channel 3x3 convs on the resident-weight halo kernel (conv_halo3r_kernel,
+    EEGAN_CONV halo_r=1, default) against conv_halo3_kernel (halo_r=0): the same
+    K order, so the same bits -- forward with bias / act / residual + gain, the
+    fused nearest-2x upsample, backward-data plain / gated / with the half-
+    resolution residual; two output-channel tiles (128), and tiles per workgroup
+    auto / 1 / 3 / 7 (ragged last workgroups, tile walks crossing image rows and
+    images)."""
+    Fn, T, _ = _mods()
+    conv_knob(monkeypatch, 'halo_r_tpb', tpb)
+    lrelu = Fn.ACT_CODES['lrelu']
+    for N, Cin, H, W, Cout, up2 in [(2, 64, 32, 64, 64, 0), (2, 64, 16, 32, 128, 0), (3, 64, 16, 64, 64, 1),
+                                    (5, 64, 8, 32, 64, 0), (2, 128, 16, 32, 64, 0)]:
+        torch.manual_seed(N * Cin + Cout + H + up2)
+        g = Fn.Geom(Cout, 3, 3, 1, 1, 1, up2)
+        xs = torch.randn(N, Cin, H // 2, W // 2) if up2 else torch.randn(N, Cin, H, W)
+        x = _nhwc(xs, gpu)
+        Wt = (torch.randn(Cout, Cin, 3, 3) * (1.0 / (9 * Cin) ** 0.5)).to(gpu)
+        b = torch.randn(Cout).to(gpu) * 0.1
+        gam = torch.tensor([0.7]).to(gpu)
+        res = _nhwc(torch.randn(N, Cout, H, W), gpu)
+        dz = _nhwc(torch.randn(N, Cout, H, W), gpu)
+        gate = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        halfres = _nhwc(torch.randn(N, Cin, H // 2, W // 2), gpu)
+        outs = {}
+        for on in ('0', '1'):
+            conv_knob(monkeypatch, 'halo_r', on)
+            o = [Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, res=res, gamma=gam).float().cpu(),
+                 Fn.conv_fwd_raw(x, Wt, None, g).float().cpu()]
+            if not up2:
+                o += [Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape)).float().cpu(),
+                      Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), gate=gate, gate_act=lrelu).float().cpu(),
+                      Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), res=halfres, res_up2=1,
+                                           res_scale=0.25).float().cpu()]
+            outs[on] = o
+        for k, (a, c) in enumerate(zip(outs['1'], outs['0'])):
+            assert torch.equal(a, c), (N, Cin, H, W, Cout, up2, k, float((a - c).abs().max()))
+        xin = xs.to(torch.bfloat16).float()
+        if up2:
+            xin = F.interpolate(xin, scale_factor=2, mode='nearest')
+        ref = F.conv2d(xin, Wt.cpu().to(torch.bfloat16).float(), None, 1, 1)
+        assert rel_l2(outs['1'][1], ref) <= 1e-2
+
+
+@pytest.mark.gpu
 def test_conv_halo3_ragged_channels(gpu, monkeypatch):
     """The halo kernel on get_mask's 100-channel conv (models.py:34-41): the
     forward's 100 output rows end in a partial 8-channel chunk (its valid

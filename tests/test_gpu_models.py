@@ -562,6 +562,58 @@ def test_discriminator_and_gradient_penalty(gpu, kind):
     _grads(tag + '_gp', D, TOL_DEEP)
 
 
+@pytest.mark.parametrize('disc_class', [True, False])
+def test_d_loss_real_early_matches_batched(gpu, disc_class):
+    """trainer.DREAL_EARLY: d_loss split into its real-image share (one D pass
+    over the real images, real + mismatch heads) and its fake-image share,
+    back-propagated one after the other into the same FlatAdam gradient, gives
+    the loss values and the parameter gradient of the batched d_loss
+    (train.py:336-376) -- the same per-sample sums in another accumulation
+    order.  Full-size Dis256 (DF=32, batch 16)."""
+    import models
+    from eegan_hip import functional as Fn
+    from eegan_hip.trainer import Trainer
+    from eegan_hip.optim import FlatAdam
+    from sync_batchnorm import DataParallelWithCallback
+    torch.manual_seed(5)
+    B, ncls = 16, 200
+    D = models.Dis256(32, disc_class, ncls).to(gpu)
+    netD = DataParallelWithCallback(D)
+    opt = FlatAdam([p for p in D.parameters() if p.requires_grad], lr=4e-4, betas=(0.0, 0.9))
+    real = Fn.ImageToNhwcFn.apply(seeded_tensor('dre:x', (B, 3, 256, 256), 1, 'uniform').to(gpu))
+    fake = Fn.ImageToNhwcFn.apply(seeded_tensor('dre:f', (B, 3, 256, 256), 2, 'uniform').to(gpu))
+    sent = seeded_tensor('dre:s', (B, 256), 1).to(gpu)
+    wrong = seeded_tensor('dre:w', (B, 256), 2).to(gpu)
+    labels = torch.zeros(B, ncls, device=gpu)
+    labels[torch.arange(B), torch.arange(B) * 7 % ncls] = 1
+    opt.zero_grad()
+    if disc_class:
+        v = Trainer.d_loss_class(real, fake, sent, wrong, labels, netD)
+        loss = v[0] + (v[1] + v[2]) / 2.0 + (v[3] + v[4] + v[5]) / 3.0 * 10.0
+        ref_vals = [v[0], v[2], v[1], v[3], v[5], v[4]]   # real, mismatch, fake per kind
+    else:
+        v = Trainer.d_loss(real, fake, sent, wrong, netD)
+        loss = v[0] + (v[1] + v[2]) / 2.0
+        ref_vals = [v[0], v[2], v[1]]
+    loss.backward(inputs=opt.params)
+    g_ref = opt.gflat.clone()
+    opt.zero_grad()
+    r = Trainer.d_loss_real(real, sent, wrong, labels, netD, disc_class)
+    part = r[0] + r[1] / 2.0 + ((r[2] + r[3]) / 3.0 * 10.0 if disc_class else 0.0)
+    part.backward(inputs=opt.params)
+    f = Trainer.d_loss_fake(fake, sent, labels, netD, disc_class)
+    (f[0] / 2.0 + (f[1] / 3.0 * 10.0 if disc_class else 0.0)).backward(inputs=opt.params)
+    torch.cuda.synchronize()
+    vals = [r[0], r[1], f[0]] + ([r[2], r[3], f[1]] if disc_class else [])
+    for a, b in zip(vals, ref_vals):
+        a, b = float(a.detach()), float(b.detach())
+        assert abs(a - b) <= 1e-3 * max(1.0, abs(b)), (a, b)
+    a, b = opt.gflat.cpu().double(), g_ref.cpu().double()
+    err = float((a - b).norm() / b.norm())
+    print('d_loss real-early vs batched: gradient rel-L2 %.2e' % err)
+    assert err < 5e-3
+
+
 # DAMSM words similarity on bf16 MFMA (csrc/damsm.hip): the attention logits
 # S = ctx q^T use split-bf16 products (hi*hi + lo*hi + hi*lo, ~fp32), the
 # context C = A2 ctx and the backward contractions plain bf16 with fp32

@@ -39,7 +39,8 @@ def run(args):
         fakes = T.netG(torch.randn(B, 100, device=dev), sent, T.attr_enhance.module.attr_merge(att))
     fakes = [f.detach() for f in fakes]
     if args.d >= 0:
-        T._d_update_one(args.d, batch['imgs'], fakes, sent, unpair, class_labels, False)
+        for _ in T._d_update_one(args.d, batch['imgs'], fakes, sent, unpair, class_labels, False):
+            pass
     torch.cuda.synchronize()
     Fn.STAMP_BUF = torch.zeros(4096, dtype=torch.int64, device=dev)
     names = []
@@ -49,7 +50,8 @@ def run(args):
             T.train_step(batch)
         else:
             Fn.stamp('start')
-            T._d_update_one(args.d, batch['imgs'], fakes, sent, unpair, class_labels, False)
+            for _ in T._d_update_one(args.d, batch['imgs'], fakes, sent, unpair, class_labels, False):
+                pass
         names = [n for n, _ in Fn.STAMPS]
         Fn.STAMPS = None
     torch.cuda.synchronize()
