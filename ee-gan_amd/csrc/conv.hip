@@ -1475,25 +1475,39 @@ __global__ __launch_bounds__(64 * WPX, NBUF == 1 ? (TH == 4 ? 3 : 2) : 1) void c
 // 4 x 32-pixel tiles; per tile only the 6 x 34 source halo moves, as whole
 // 128-B lines (64 channels of a pixel = one line, against the half-line 64-B
 // pieces of 32-channel slices), double-buffered: tile k + 1's halo streams in
-// under tile k's 144 MFMAs per wave.  LDS: 72 KB weights + 2 x 32 KB buffers
-// (halo, then that tile's fp32 epilogue tile) -- one workgroup per CU.
-// 16-B chunk q of a 128-B row r (halo column / weight row) sits at slot
-// q ^ (r & 6): conflict-free ds_read_b128 for any 16 consecutive rows in
-// gfx950's b128 lane groups (brute-forced over all window starts, both 32-
-// channel halves); a fragment read is a base register (tap column shift x
-// channel half) + an immediate.  K order as conv_halo3_kernel (32-channel half
-// outer, tap inner): the same bits.  Host-checked: Cgp == Cvalid == 64, Mrows
-// % 64 == 0 (every thread stores exactly NIT chunks per tile, which the
-// counted wait at the next tile's top relies on).
+// under tile k's 144 MFMAs per wave, its fragment reads interleaved one per
+// MFMA gap (one wave per SIMD: nothing else hides a read the compiler would
+// sink to its first use).  The epilogue runs on the MFMA fragments: bias,
+// activation (none / relu / leaky relu, branch-free), the gate and residual
+// tiles -- LDS-DMA'd beside the next halo, so no compiler-counted load waits on
+// the in-flight halo -- then bf16 through LDS for 16-B row stores.  LDS: 72 KB
+// weights + 2 x 28 KB halo buffers + 2 x 16 KB gate / residual tiles = 160 KB,
+// one workgroup per CU.
+// Swizzles (brute-forced over gfx950's b128 / b64 lane groups): halo and weight
+// rows (128 B) hold 16-B chunk q at slot q ^ (r & 6) -- conflict-free
+// ds_read_b128 for any 16 consecutive rows, both 32-channel halves, so a
+// fragment read is a base register (tap column shift x half) + an immediate;
+// the 128-pixel gate / residual / output tiles hold chunk q of pixel p at
+// q ^ ((p >> 1) & 7) -- conflict-free ds_read_b64 of a fragment's 4 channels
+// and ds_read_b128 of a store's 8.  K order as conv_halo3_kernel (32-channel half
+// outer, tap inner) and the same epilogue arithmetic: the same bits.
+// Host-checked: Cgp == Cvalid == 64, Mrows % 64 == 0, act / gate_act in {none,
+// relu, lrelu}, 16-B aligned rows.
+#ifndef HALO_R_PIN
+#define HALO_R_PIN 1
+#endif
+EE_DEV int tile_swz(int p) { return (p >> 1) & 7; }
+
 template <int MODE>
-__global__ __launch_bounds__(256, 1) void conv_halo3r_kernel(ConvArgs a, long src_bytes, long w_bytes, int tpb) {
+__global__ __launch_bounds__(256, 1) void conv_halo3r_kernel(ConvArgs a, long src_bytes, long w_bytes, int tpb,
+                                                             int knock) {
   constexpr int NT = 256, TH = 4, TW = HALO_TW, TCO = HALO_TCO, FI = TCO / 16, CB = TW / 16, FJ = CB;
-  constexpr int HW2 = TW + 2, HP = (TH + 2) * HW2, HOPS = (HP * 8 + NT - 1) / NT;
+  constexpr int HW2 = TW + 2, HP = (TH + 2) * HW2, HOPS = (HP * 8 + NT - 1) / NT, HBUF = HOPS * NT * 16;
   constexpr int WSL = 9 * TCO * 8, WOPS = WSL / NT, WBYTES = WSL * 16;
-  constexpr int TPIX = TH * TW, NCK = TCO / 4, NIT = TPIX * (TCO / 8) / NT;
-  constexpr int BUFB = TPIX * TCO * 4;   // 32 KB: >= the halo's HOPS * NT * 16 (28 KB)
-  static_assert(HOPS * NT * 16 <= BUFB && WSL % NT == 0 && NIT == 4, "halo3r tile");
-  __shared__ __attribute__((aligned(16))) char lds[WBYTES + 2 * BUFB];
+  constexpr int TPIX = TH * TW, GRB = TPIX * TCO * 2, NIT = GRB / 16 / NT;
+  constexpr int GOFF = WBYTES + 2 * HBUF, ROFF = GOFF + GRB;
+  static_assert(WSL % NT == 0 && NIT == 4 && GRB <= HBUF && ROFF + GRB <= 163840, "halo3r tile");
+  __shared__ __attribute__((aligned(16))) char lds[ROFF + GRB];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wj = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1503,6 +1517,9 @@ __global__ __launch_bounds__(256, 1) void conv_halo3r_kernel(ConvArgs a, long sr
   const int lds0 = (int)(uintptr_t)(lds_void_t*)lds;
   const rsrc_t rs_src = make_rsrc(a.src, src_bytes);
   const rsrc_t rs_w = make_rsrc(a.wp, w_bytes);
+  const bool has_gate = MODE == MODE_BWDD && a.gate, has_res = a.res != nullptr;
+  const rsrc_t rs_g = make_rsrc(has_gate ? (const void*)a.gate : a.src, 0x7fffffffL);
+  const rsrc_t rs_r = make_rsrc(has_res ? (const void*)a.res : a.src, 0x7fffffffL);
   const int PH = a.IH >> a.up2, PW = a.IW >> a.up2;
 
   // weights once: slot L = (tap, row, chunk q) holds source chunk q ^ (row & 6)
@@ -1512,12 +1529,18 @@ __global__ __launch_bounds__(256, 1) void conv_halo3r_kernel(ConvArgs a, long sr
     const int row = rem >> 3, q = (rem & 7) ^ (row & 6);
     lds_dma16s(rs_w, lds0 + (i * NT + wj * 64) * 16, (unsigned)(((co0 + row) * a.Kw + t * 64 + q * 8) * 2), 0);
   }
-  auto issue_halo = [&](int tile, int buf) {
+  auto tile_origin = [&](int tile, int& n, int& oy0, int& ox0) {
     int b = tile;
     const int tx = b % tiles_x;
     b /= tiles_x;
-    const int ty = b % tiles_y, n = b / tiles_y;
-    const int oy0 = ty * TH, ox0 = tx * TW;
+    const int ty = b % tiles_y;
+    n = b / tiles_y;
+    oy0 = ty * TH;
+    ox0 = tx * TW;
+  };
+  auto issue_halo = [&](int tile, int buf) {
+    int n, oy0, ox0;
+    tile_origin(tile, n, oy0, ox0);
 #pragma unroll
     for (int i = 0; i < HOPS; ++i) {
       const int L = i * NT + tid, h = L >> 3;
@@ -1526,7 +1549,24 @@ __global__ __launch_bounds__(256, 1) void conv_halo3r_kernel(ConvArgs a, long sr
       const unsigned off = (h < HP && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW)
                                ? (unsigned)((((n * PH + (iy >> a.up2)) * PW + (ix >> a.up2)) * a.lds_src + q * 8) * 2)
                                : OOB;
-      lds_dma16s(rs_src, lds0 + WBYTES + buf * BUFB + (i * NT + wj * 64) * 16, off, 0);
+      lds_dma16s(rs_src, lds0 + WBYTES + buf * HBUF + (i * NT + wj * 64) * 16, off, 0);
+    }
+  };
+  // the tile's gate / residual chunks: slot L = (pixel p, chunk q) holds chunk q ^ tile_swz(p)
+  auto issue_gr = [&](int tile) {
+    int n, oy0, ox0;
+    tile_origin(tile, n, oy0, ox0);
+#pragma unroll
+    for (int j = 0; j < NIT; ++j) {
+      const int L = j * NT + tid, p = L >> 3, q = (L & 7) ^ tile_swz(p);
+      const int y = oy0 + p / TW, x = ox0 + p % TW;
+      const int dst = (j * NT + wj * 64) * 16;
+      if (has_gate)
+        lds_dma16s(rs_g, lds0 + GOFF + dst, (unsigned)((((n * a.OH + y) * a.OW + x) * a.ldgate + co0 + q * 8) * 2), 0);
+      if (has_res) {
+        const int rp = a.res_up2 ? (n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1) : (n * a.OH + y) * a.OW + x;
+        lds_dma16s(rs_r, lds0 + ROFF + dst, (unsigned)((rp * a.ldres + co0 + q * 8) * 2), 0);
+      }
     }
   };
 
@@ -1535,57 +1575,54 @@ __global__ __launch_bounds__(256, 1) void conv_halo3r_kernel(ConvArgs a, long sr
   int wbase[2];
 #pragma unroll
   for (int kh = 0; kh < 2; ++kh) wbase[kh] = fr * 128 + (((kh * 4 + fq) ^ (fr & 6)) << 4);
-  // B fragment (halo row wj + oyh + 0, column block jc, tap column shift sx, half kh):
-  // hbase[sx][kh] + (wj + oyh) * HW2 * 128 + jc * 2048 (columns c and c + 16 share the swizzle)
+  // B fragment (halo row wj + oyh, column block j, tap column shift sx, half kh):
+  // hbase[sx][kh] + oyh * HW2 * 128 + j * 2048 (columns c and c + 16 share the swizzle)
   int hbase[3][2];
 #pragma unroll
   for (int sx = 0; sx < 3; ++sx)
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
       hbase[sx][kh] = (wj * HW2 + fr + sx) * 128 + (((kh * 4 + fq) ^ ((fr + sx) & 6)) << 4);
-
-  // this thread's epilogue chunk: output channels co0 + 8e .. + 7 of pixels p = (k * NT + tid) / 8
-  const int e = tid & 7, co = co0 + 8 * e;
-  float bias8[8];
+  // fragment (i, j) = 4 channels i * 16 + 4 fq .. of pixel wj * 32 + j * 16 + fr: its 8-B
+  // piece in the 128-pixel tiles
+  int tslot[FI][FJ];
+  float bias[FI][4];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) bias8[r] = a.bias ? a.bias[co + r] : 0.f;
-  const float gam = (a.res && a.gamma) ? *a.gamma : 1.f;
+  for (int i = 0; i < FI; ++i) {
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const int p = wj * TW + j * 16 + fr, c = 2 * i + (fq >> 1);
+      tslot[i][j] = p * 128 + ((c ^ tile_swz(p)) << 4) + (fq & 1) * 8;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[i][r] = a.bias ? a.bias[co0 + i * 16 + fq * 4 + r] : 0.f;
+  }
+  const bool relu = a.act == ACT_RELU;
+  const float sl1 = a.act == ACT_LRELU ? a.slope : 1.f;
+  const float gneg = a.gate_act == ACT_RELU ? 0.f : a.gate_act == ACT_LRELU ? a.gate_slope : 1.f;
+  const float gam = (has_res && a.gamma) ? *a.gamma : 1.f;
+  const float rsc = a.res_scale;
 
   if (t0 < t1) issue_halo(t0, 0);
   for (int tile = t0, k = 0; tile < t1; ++tile, ++k) {
-    int b = tile;
-    const int tx = b % tiles_x;
-    b /= tiles_x;
-    const int ty = b % tiles_y, n = b / tiles_y;
-    const int oy0 = ty * TH, ox0 = tx * TW;
+    int n, oy0, ox0;
+    tile_origin(tile, n, oy0, ox0);
     const int buf = k & 1;
-    // this tile's gate / residual chunks first (their latency runs under the MFMAs; loads
-    // issued before the next halo, so the epilogue's wait for them does not wait for it)
-    uint4 gpre[NIT], rpre[NIT];
-#pragma unroll
-    for (int j = 0; j < NIT; ++j) {
-      const int p = (j * NT + tid) >> 3;
-      const int y = oy0 + p / TW, x = ox0 + p % TW;
-      const long gp = ((long)n * a.OH + y) * a.OW + x;
-      gpre[j] = rpre[j] = make_uint4(0, 0, 0, 0);
-      if (MODE == MODE_BWDD && a.gate) gpre[j] = *reinterpret_cast<const uint4*>(a.gate + gp * a.ldgate + co);
-      if (a.res) {
-        const long rp = a.res_up2 ? ((long)n * (a.OH >> 1) + (y >> 1)) * (a.OW >> 1) + (x >> 1) : gp;
-        rpre[j] = *reinterpret_cast<const uint4*>(a.res + rp * a.ldres + co);
-      }
-    }
     // tile k's halo landed (and at k = 0 the weights): every older piece of this wave but
-    // the previous tile's NIT output stores, then the barrier for every wave's pieces
+    // the previous tile's NIT output stores, then the barrier for every wave's pieces;
+    // past it every wave is done with tile k - 1 (its buffers and gate / residual tiles)
     if (k == 0) wait_vmcnt_barrier<0>();
     else wait_vmcnt_barrier<NIT>();
-    if (tile + 1 < t1) issue_halo(tile + 1, buf ^ 1);   // that buffer's last readers passed the barrier
+    issue_gr(tile);
+    const bool more = tile + 1 < t1 && !(knock & 1);
+    if (more) issue_halo(tile + 1, buf ^ 1);
 
     f32x4_t acc[FI][FJ];
 #pragma unroll
     for (int i = 0; i < FI; ++i)
 #pragma unroll
       for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    const char* hb = lds + WBYTES + buf * BUFB;
+    const char* hb = lds + WBYTES + buf * HBUF;
     auto rd = [&](int kh, int t, bf16x8_t (&fa)[FI], bf16x8_t (&fb)[FJ]) {
       const int ta = t / 3, tb = t - ta * 3;
       const int oyh = MODE == MODE_FWD ? ta : 2 - ta, oxh = MODE == MODE_FWD ? tb : 2 - tb;
@@ -1596,62 +1633,69 @@ __global__ __launch_bounds__(256, 1) void conv_halo3r_kernel(ConvArgs a, long sr
       for (int j = 0; j < FJ; ++j)
         fb[j] = as_frag(*reinterpret_cast<const uint4*>(hb + hbase[oxh][kh] + oyh * (HW2 * 128) + j * 2048));
     };
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
+    // 18 K-steps (channel half kh outer, tap inner); step s + 1's 6 fragment reads are
+    // interleaved one per MFMA gap with step s's 8 MFMAs
+    {
       bf16x8_t fa[2][FI], fb[2][FJ];
-      rd(kh, 0, fa[0], fb[0]);
+      rd(0, 0, fa[0], fb[0]);
+      if (HALO_R_PIN) __builtin_amdgcn_sched_group_barrier(0x100, FI + FJ, 0);   // step 0's reads first
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        if (t + 1 < 9) rd(kh, t + 1, fa[(t + 1) & 1], fb[(t + 1) & 1]);
+      for (int s = 0; s < 18; ++s) {
+        if (s + 1 < 18) rd((s + 1) / 9, (s + 1) % 9, fa[(s + 1) & 1], fb[(s + 1) & 1]);
 #pragma unroll
         for (int i = 0; i < FI; ++i)
 #pragma unroll
           for (int j = 0; j < FJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t & 1][i], fb[t & 1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s & 1][i], fb[s & 1][j], acc[i][j], 0, 0, 0);
+        if (HALO_R_PIN) {
+#pragma unroll
+          for (int m = 0; m < FI * FJ; ++m) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+            if (s + 1 < 18 && m < FI + FJ) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one DS read
+          }
+        }
       }
     }
-    // epilogue through this tile's buffer (every wave is done with its halo): fp32 tile
-    // [pixel][16 chunks of 4 channels], chunk c of pixel p at c ^ (p & 15)
-    __syncthreads();
-    float4* st = reinterpret_cast<float4*>(lds + WBYTES + buf * BUFB);
-#pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-      const int p = wj * TW + j * 16 + fr;
-#pragma unroll
-      for (int i = 0; i < FI; ++i) {
-        const int c = i * 4 + fq;
-        st[p * NCK + (c ^ (p & 15))] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-      }
+    if (knock & 2) {   // diagnostics: no epilogue (one store keeps the MFMAs live)
+      if (acc[0][0][0] == 1234.5f) a.part[tid] = acc[0][1][1] + acc[1][0][2];
+      continue;
     }
+    // the gate / residual pieces landed (the next halo's HOPS pieces may still fly) and
+    // every wave is done reading this tile's halo buffer, which now takes the bf16 output
+    if (more) wait_vmcnt_barrier<HOPS>();
+    else wait_vmcnt_barrier<0>();
+    char* ob = lds + WBYTES + buf * HBUF;
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = acc[i][j][r] + bias[i][r];
+          v[r] = x > 0.f ? x : (relu ? 0.f : x * sl1);   // act_fwd for none / relu / lrelu
+        }
+        if (has_gate) {
+          const uint2 gv = *reinterpret_cast<const uint2*>(lds + GOFF + tslot[i][j]);
+          const float gy[4] = {lo_f(gv.x), hi_f(gv.x), lo_f(gv.y), hi_f(gv.y)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] *= gy[r] > 0.f ? 1.f : gneg;   // act_dgrad_from_y
+        }
+        if (has_res) {
+          const uint2 rv = *reinterpret_cast<const uint2*>(lds + ROFF + tslot[i][j]);
+          const float ry[4] = {lo_f(rv.x), hi_f(rv.x), lo_f(rv.y), hi_f(rv.y)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = res_combine(rsc, ry[r], gam, v[r]);
+        }
+        *reinterpret_cast<uint2*>(ob + tslot[i][j]) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < NIT; ++j) {
-      const int p = (j * NT + tid) >> 3;
-      const float4 lo = st[p * NCK + ((2 * e) ^ (p & 15))];
-      const float4 hi = st[p * NCK + ((2 * e + 1) ^ (p & 15))];
-      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-#pragma unroll
-      for (int r = 0; r < 8; ++r) v[r] = act_fwd(v[r] + bias8[r], a.act, a.slope);
-      if (MODE == MODE_BWDD && a.gate) {
-        const uint32_t gw[4] = {gpre[j].x, gpre[j].y, gpre[j].z, gpre[j].w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[2 * r] *= act_dgrad_from_y(lo_f(gw[r]), a.gate_act, a.gate_slope);
-          v[2 * r + 1] *= act_dgrad_from_y(hi_f(gw[r]), a.gate_act, a.gate_slope);
-        }
-      }
-      if (a.res) {
-        const uint32_t rw[4] = {rpre[j].x, rpre[j].y, rpre[j].z, rpre[j].w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[2 * r] = res_combine(a.res_scale, lo_f(rw[r]), gam, v[2 * r]);
-          v[2 * r + 1] = res_combine(a.res_scale, hi_f(rw[r]), gam, v[2 * r + 1]);
-        }
-      }
-      const int y = oy0 + p / TW, x = ox0 + p % TW;
-      const long gp = ((long)n * a.OH + y) * a.OW + x;
-      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + gp * a.ldo + co) =
-          make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+      const int L = j * NT + tid, p = L >> 3, e = L & 7;
+      const uint4 o = *reinterpret_cast<const uint4*>(ob + p * 128 + ((e ^ tile_swz(p)) << 4));
+      const long gp = ((long)n * a.OH + oy0 + p / TW) * a.OW + ox0 + p % TW;
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + gp * a.ldo + co0 + 8 * e) = o;
     }
   }
 }
@@ -3281,16 +3325,21 @@ int try_halo3(const ConvArgs& a, hipStream_t s, long src_bytes, long w_bytes) {
   if (a.res && ((a.ldres & 7) || ((uintptr_t)a.res & 15))) return 0;
   if (a.OW % HALO_TW || a.OH % 8 || a.OH != a.IH || a.OW != a.IW) return 0;
   const int co_t = ee_cdiv(a.Mrows, HALO_TCO);
-  if (a.Cgp == 64 && a.Cvalid == 64 && a.Mrows % HALO_TCO == 0 && knob("halo_r", 1)) {
-    // 64-channel inputs: resident weights, TPB consecutive tiles per workgroup (grid ~ 2 per CU)
+  const auto simple_act = [](int act) { return act == ACT_NONE || act == ACT_RELU || act == ACT_LRELU; };
+  if (a.Cgp == 64 && a.Cvalid == 64 && a.Mrows % HALO_TCO == 0 && simple_act(a.act) &&
+      (MODE == MODE_FWD || !a.gate || simple_act(a.gate_act)) && knob("halo_r", 1)) {
+    // 64-channel inputs: resident weights, TPB consecutive tiles per workgroup -- one
+    // workgroup per CU (its 160 KB of LDS), up to 16 tiles each (tools/conv_bench.py: D256
+    // b0 at N = 32 fwd / bwdd 54 / 58 us at 16 tiles vs 56 / 62 at 8; 64-ch 128^2 N = 16
+    // 28 / 29 us at 8 vs 30 / 32 at 4)
     const long tiles = (long)a.N * (a.OH / 4) * (a.OW / HALO_TW);
     int tpb = knob("halo_r_tpb", 0);
     if (tpb <= 0) {
-      const long t = tiles * co_t / 512;
+      const long t = tiles * co_t / 256;
       tpb = t < 1 ? 1 : t > 16 ? 16 : (int)t;
     }
     const dim3 grid((unsigned)ee_cdiv(tiles, (long)tpb), co_t);
-    ee_launch(conv_halo3r_kernel<MODE>, grid, dim3(256), 0, s, a, src_bytes, w_bytes, tpb);
+    ee_launch(conv_halo3r_kernel<MODE>, grid, dim3(256), 0, s, a, src_bytes, w_bytes, tpb, knob("halo_r_knock", 0));
     const int rc = ee_check_launch(MODE == MODE_FWD ? "conv_fwd(halo3r)" : "conv_bwd_data(halo3r)");
     return rc ? rc : 1;
   }
