@@ -168,8 +168,14 @@ def main():
     total_ns = sum(o['ns'] for o in fams.values())
     res = {'families': out, 'gpu_busy_ms_total': round(total_ns * 1e-6, 3), 'config': a.config}
     res.update(_provenance())
+    if a.steps <= 0:   # counted: one adam_tick_kernel per optimizer step, 7 per C2 train step
+        ticks = fams.get('adam_tick_kernel', {}).get('calls', 0)
+        a.steps = round(ticks / 7) if ticks else 0
     if a.steps:
+        res['steps'] = a.steps
         res['gpu_busy_ms_per_step'] = round(total_ns * 1e-6 / a.steps, 3)
+        for e in out.values():
+            e['ms_per_step'] = round(e['total_ms'] / a.steps, 3)
     txt = json.dumps(res, indent=1)
     if a.out:
         with open(a.out, 'w') as f:
