@@ -3494,7 +3494,7 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   }
   const long w_bytes = (long)ee_round_up(a.Mrows, 128) * a.Kw * 2;
   if (p.nsplit > 1 && a.red_vec4 && ctr && (long)grid.x * grid.y * a.ncls <= ctr_n &&
-      (long)p.nsplit * total * 4 < 0x7fffffffL && knob("splitk_fused", 1))
+      (long)p.nsplit * total * 4 < 0x7fffffffL && knob("splitk_fused", 0))
     a.ctr = ctr;   // conv_fast_kernel finishes the split itself (below: only when `fast`)
 #define GL(TC, TP) ee_launch(conv_glds_kernel<MODE, TC, TP>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
 #define FA(TC, TP) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 4, 2>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)

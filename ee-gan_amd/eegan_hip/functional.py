@@ -199,6 +199,9 @@ class Geom:
 # different stream lanes never share a counter.  Created outside graph capture (the
 # step's eager warm-up reaches every lane first); a stream first seen inside a
 # capture keeps the two-launch reduce.  SPLITK_FUSED = False: always two launches.
+# The library uses the counters only with EEGAN_CONV splitk_fused=1: on the replayed
+# C2 step the in-kernel finish measured -0.7 % against the separate reduce launch
+# (in-process A/B, profiles/r05_inproc_ab.txt), so the reduce launch is the default.
 SPLITK_FUSED = True
 SPLITK_CTR_N = 1 << 15
 _SPLITK_CTR = {}
