@@ -10,6 +10,7 @@ Generator-side Functions (BN modulation, upsample-fused convs, linears,
 mask resize) are first-order, as the reference only differentiates G once.
 """
 import ctypes
+import contextlib
 import os
 import math
 
@@ -469,7 +470,8 @@ class Conv2dFn(torch.autograd.Function):
         gy = _as_bf16_grad(gy)
         fused = FUSE_ACT_BWD and not torch.is_grad_enabled()
         cg = FUSE_ACT_BWD and FUSE_GP_ACT and torch.is_grad_enabled()
-        dz = ActBwdFn.apply(gy, y, ctx.act, ctx.slope) if ctx.act and not _act_deferred(ctx, fused, cg) else gy
+        dz = (ActBwdFn.apply(gy, _mask_src(y, ctx.act), ctx.act, ctx.slope)
+              if ctx.act and not _act_deferred(ctx, fused, cg) else gy)
         dx = dW = db = None
         if _needed(ctx, 0):
             if g.up2:
@@ -478,7 +480,8 @@ class Conv2dFn(torch.autograd.Function):
                 dx = conv_bwd_data_raw(dz, W, g, ctx.x_shape, ctx.cache, gate=x, gate_act=ctx.in_act,
                                        gate_slope=ctx.in_slope)
             elif cg and ctx.in_act:
-                dx = GatedConvBwdDataFn.apply(dz, W, x, g, ctx.x_shape, ctx.cache, ctx.in_act, ctx.in_slope)
+                dx = GatedConvBwdDataFn.apply(dz, W, _mask_src(x, ctx.in_act), g, ctx.x_shape, ctx.cache, ctx.in_act,
+                                              ctx.in_slope)
             else:
                 dx = ConvBwdDataFn.apply(dz, W, g, ctx.x_shape, ctx.cache)
         if _needed(ctx, 1) and not _sink_wgrad(ctx, 1, x, dz, g, W.shape):
@@ -523,7 +526,8 @@ class PoolConvFn(torch.autograd.Function):
         dz = None
         if gy is not None:
             gy = _as_bf16_grad(gy)
-            dz = ActBwdFn.apply(gy, y, ctx.act, ctx.slope) if ctx.act and not _act_deferred(ctx, fused, cg) else gy
+            dz = (ActBwdFn.apply(gy, _mask_src(y, ctx.act), ctx.act, ctx.slope)
+              if ctx.act and not _act_deferred(ctx, fused, cg) else gy)
         if _needed(ctx, 0):
             if fused and gp is not None and dz is not None:
                 dx = conv_bwd_data_raw(dz, W, g, ctx.x_shape, ctx.cache, res=_as_bf16_grad(gp), res_up2=1,
@@ -647,6 +651,40 @@ class ConvBwdWeightFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             gdz = Conv2dFn.apply(x, gW, None, ctx.g, 0, 0.0, False, None)
         return gx, gdz, None
+
+
+def _mask_src(t, act):
+    """The activation tensor an act' mask is read from, as a first-backward
+    Function's input: detached when act' is piecewise constant (relu / leaky
+    relu -- no gradient flows into it), so the gradient penalty's second
+    backward has no edge back into the forward graph.  Attached, autograd ran
+    every forward conv's backward there on zero-filled gradients (custom
+    Functions materialise the missing ones): a data and a weight gradient per
+    conv of the discriminator, all adding zeros (tools/gp_trace.py)."""
+    if not DETACH_MASK_SRC:
+        return t
+    return t.detach() if t is not None and act in (0, ACT_CODES['relu'], ACT_CODES['lrelu']) else t
+
+
+# On inside Trainer.MA_gradient_penalty's first backward (detached_mask_sources), where
+# every parameter's gradient lives in a FlatAdam buffer zeroed before the backward, so a
+# bias the second backward no longer reaches keeps its exact-zero gradient as in the
+# reference.  Off elsewhere: under the reference's own train.py (torch Adam, zero_grad
+# to None) such a bias would get no .grad and Adam would skip its moment update.
+# tools/ab_inproc.py "py:eegan_hip.functional.GP_DETACH_MASKS=False" A/Bs the trainer's use.
+DETACH_MASK_SRC = False
+GP_DETACH_MASKS = True
+
+
+@contextlib.contextmanager
+def detached_mask_sources(on=True):
+    global DETACH_MASK_SRC
+    prev = DETACH_MASK_SRC
+    DETACH_MASK_SRC = bool(on)
+    try:
+        yield
+    finally:
+        DETACH_MASK_SRC = prev
 
 
 class ActBwdFn(torch.autograd.Function):

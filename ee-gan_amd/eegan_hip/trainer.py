@@ -288,8 +288,13 @@ class Trainer(object):
             out, _ = netD.module.COND_DNET(features, sent_inter)
         else:
             out = netD.module.COND_DNET(features, sent_inter)
-        grads = torch.autograd.grad(outputs=out, inputs=(interpolated, sent_inter), grad_outputs=torch.ones_like(out),
-                                    retain_graph=True, create_graph=True, only_inputs=True)
+        # the first backward's act' masks read their activations detached (piecewise
+        # constant: no gradient flows into them), so the second backward never walks
+        # the forward graph with zero-filled gradients (functional._mask_src)
+        with Fn.detached_mask_sources(Fn.GP_DETACH_MASKS):
+            grads = torch.autograd.grad(outputs=out, inputs=(interpolated, sent_inter),
+                                        grad_outputs=torch.ones_like(out), retain_graph=True, create_graph=True,
+                                        only_inputs=True)
         return Fn.GradPenaltyFn.apply(grads[0], grads[1])
 
     @staticmethod
