@@ -3208,6 +3208,102 @@ __global__ __launch_bounds__(256) void conv_wgrad_thin_kernel(WgradArgs w, int x
   }
 }
 
+// Weight gradient of 3x3 / stride-1 / pad-1 convs with 32 or 64 input channels and
+// output channels in 32-channel tiles (the generator's 32/64-channel 128^2 / 256^2
+// layers, D256's 64-channel 128^2 resD conv): conv_wgrad_thin_kernel's halo staging
+// for full MFMA tiles.  A block walks `tiles_per_block` 4 x 32-pixel tiles; per tile
+// the 6 x 34 x CI source halo and the 128-pixel x 32-channel dy tile are staged in
+// LDS once ([16-channel block][pixel][16 ch], transposed reads conflict-free), and
+// each of the 9 taps reads its B fragments from the SAME halo at a column / row
+// shift -- the tile kernels gather every x pixel once per tap through L2.  Wave w
+// owns output-channel fragment w & 1 and input-channel fragment(s) of w >> 1 for all
+// 9 taps (A = dy^T shared by the taps); K = pixels, each 32-pixel step read in the
+// thin kernel's permuted order (rows 4 kg + q and + 16).  One fp32 partial per
+// block into the split slab [nsplit][Cout][9 * CI], reduced in split order.
+template <int CI>
+__global__ __launch_bounds__(256) void conv_wgrad_halo3_kernel(WgradArgs w, int x_bytes, int dy_bytes,
+                                                               int tiles_per_block) {
+  constexpr int TH = 4, TW = 32, PW = TW + 2, XPIX = (TH + 2) * PW, CB = CI / 16, NF = CI / 32;
+  constexpr int XCH = XPIX * CI / 8, XLD = (XCH + 255) / 256;   // 16-B chunks of the halo, per thread
+  constexpr int DCH = TH * TW * 4, DLD = DCH / 256;              // of the dy tile (32 channels)
+  __shared__ __attribute__((aligned(16))) bf16_t xs[CB * XPIX * 16];   // [cb][pixel][16 ch]
+  __shared__ __attribute__((aligned(16))) bf16_t dys[2 * TH * TW * 16];  // [cb][pixel][16 ch]
+  const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4, li = lane & 15, q = li >> 2, pq = li & 3;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cf = wv & 1, nf0 = (wv >> 1) * NF;   // this wave's output / input channel fragments
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (b & 7) * (nb >> 3) + (b >> 3);   // a block's consecutive tiles share one XCD (nb % 8 == 0)
+  const int co0 = blockIdx.y * 32;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)w.x, (short)0, x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)w.dy, (short)0, dy_bytes, 0x00020000);
+  f32x4_t acc[NF][9];
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[f][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int tiles_x = w.OW / TW, tiles_y = w.OH / TH, tiles = w.N * tiles_x * tiles_y;
+  const int t0 = lb * tiles_per_block, t1 = min(t0 + tiles_per_block, tiles);
+  for (int tt = t0; tt < t1; ++tt) {
+    const int n = tt / (tiles_x * tiles_y), rem = tt - n * tiles_x * tiles_y;
+    const int y0 = (rem / tiles_x) * TH, x0 = (rem - (rem / tiles_x) * tiles_x) * TW;
+    uint4 xv[XLD], dv[DLD];
+#pragma unroll
+    for (int i = 0; i < XLD; ++i) {
+      const int e = tid + 256 * i;
+      const int pix = e / (CI / 8), ch = e - pix * (CI / 8);
+      const int pr = pix / PW, pc = pix - pr * PW;
+      const int iy = y0 + pr - 1, ix = x0 + pc - 1;
+      const bool ok = e < XCH && (unsigned)iy < (unsigned)w.IH && (unsigned)ix < (unsigned)w.IW;
+      const int off = (((n * w.IH + iy) * w.IW + ix) * w.ldx + ch * 8) * 2;
+      xv[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? off : 0x80000000, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < DLD; ++i) {
+      const int e = tid + 256 * i, pix = e >> 2, ch = e & 3;
+      const int off = ((((n * w.OH + y0 + pix / TW) * w.OW) + x0 + pix % TW) * w.lddy + co0 + ch * 8) * 2;
+      dv[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, 0));
+    }
+    __syncthreads();   // the previous tile's fragment reads are done
+#pragma unroll
+    for (int i = 0; i < XLD; ++i) {
+      const int e = tid + 256 * i;
+      if (e < XCH) {
+        const int pix = e / (CI / 8), ch = e - pix * (CI / 8);
+        *reinterpret_cast<uint4*>(&xs[((ch >> 1) * XPIX + pix) * 16 + (ch & 1) * 8]) = xv[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < DLD; ++i) {
+      const int e = tid + 256 * i, pix = e >> 2, ch = e & 3;
+      *reinterpret_cast<uint4*>(&dys[((ch >> 1) * (TH * TW) + pix) * 16 + (ch & 1) * 8]) = dv[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < TH; ++rr) {
+      const int p1 = 4 * kg + q, p2 = p1 + 16;
+      const bf16_t* da = &dys[(cf * (TH * TW) + rr * TW) * 16 + 4 * pq];
+      const bf16x8_t fa = tr_pair(lds_tr16(da + p1 * 16), lds_tr16(da + p2 * 16));
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int ta = t / 3, tb = t - 3 * ta;
+          const bf16_t* xb = &xs[((nf0 + f) * XPIX + (rr + ta) * PW + tb) * 16 + 4 * pq];
+          const bf16x8_t fb = tr_pair(lds_tr16(xb + p1 * 16), lds_tr16(xb + p2 * 16));
+          acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[f][t], 0, 0, 0);
+        }
+      }
+    }
+  }
+  float* slab = w.ws + ((long)b * w.Cout + co0 + 16 * cf) * w.K;
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) slab[(4 * kg + j) * w.K + t * CI + 16 * (nf0 + f) + li] = acc[f][t][j];
+}
+
 // ------------------------------------------------------------ dispatch --
 int cgp_of(int C) { return C <= 8 ? 8 : ee_round_up(C, BK); }
 int kw_of(int R, int S, int Cgp) { return ee_round_up(R * S * Cgp, BK); }
@@ -3740,9 +3836,28 @@ static int wgrad_thin_blocks(const eegan_conv_desc* d) {
   return ee_round_up(std::min(tiles, 512), 8);
 }
 
+// 4 x 32-pixel tiles of conv_wgrad_halo3_kernel for this shape, or 0 when it does not apply
+static int wgrad_halo_tiles(const eegan_conv_desc* d) {
+  if (!knob("wgrad_halo", 1) || wgrad_thin_blocks(d)) return 0;
+  if (d->R != 3 || d->S != 3 || d->stride != 1 || d->pad_h != 1 || d->pad_w != 1 || d->up2) return 0;
+  if ((d->C != 32 && d->C != 64) || d->K % 32 || d->Wo % 32 || d->Ho % 4 || d->Ho != d->H || d->Wo != d->W) return 0;
+  if (wgrad_x_bytes(d) >= 0x7fffffffL || wgrad_dy_bytes(d) >= 0x7fffffffL) return 0;
+  return d->N * (d->Ho / 4) * (d->Wo / 32);
+}
+
 static void wgrad_plan(const eegan_conv_desc* d, int& TCO, int& TK, int& nsplit, int& pps, int& K) {
   const int Cg = ee_round_up(d->C, 8);
   K = d->R * d->S * Cg;
+  if (const int ht = wgrad_halo_tiles(d)) {
+    // ~`wgrad_halo_blocks` blocks over the output-channel tiles, a multiple of 8 per tile (XCD-contiguous walks)
+    const int co_t = d->K / 32;
+    const int want = std::max(8, knob("wgrad_halo_blocks", 512) / co_t);
+    pps = ee_cdiv(ht, std::min(want, ht));   // tiles per block
+    nsplit = ee_round_up(ee_cdiv(ht, pps), 8);
+    TCO = 32;
+    TK = 0;
+    return;
+  }
   if (const int tb = wgrad_thin_blocks(d)) {
     TCO = 16;
     TK = 64;
@@ -3819,7 +3934,18 @@ int eegan_conv_bwd_weight(const eegan_conv_desc* d, const bf16_t* x, const bf16_
     // wgrad_stage_epi: 0 off, 1 unsplit dW only, 2 (default) also the row-major split slabs
     w.stage = d->C % 4 == 0 && ((uintptr_t)dw & 15) == 0 && knob("wgrad_stage_epi", 2);
   }
-  if (w.P > 0 && wgrad_thin_blocks(d)) {
+  if (w.P > 0 && wgrad_halo_tiles(d)) {
+    w.dw = nullptr;   // always through the slab (one partial per block)
+    const dim3 grid(nsplit, d->K / 32);
+    if (d->C == 32)
+      ee_launch(conv_wgrad_halo3_kernel<32>, grid, dim3(256), 0, stream, w, (int)wgrad_x_bytes(d),
+                (int)wgrad_dy_bytes(d), pps);
+    else
+      ee_launch(conv_wgrad_halo3_kernel<64>, grid, dim3(256), 0, stream, w, (int)wgrad_x_bytes(d),
+                (int)wgrad_dy_bytes(d), pps);
+    const int rc = ee_check_launch("conv_wgrad(halo3)");
+    if (rc) return rc;
+  } else if (w.P > 0 && wgrad_thin_blocks(d)) {
     const int tiles = d->N * (d->Ho / WTH_H) * (d->Wo / WTH_W);
     const dim3 grid(nsplit, ee_cdiv(d->K, 8));
     if (w.Cg == 32)

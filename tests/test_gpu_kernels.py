@@ -148,6 +148,39 @@ def test_conv_thin_wgrad(gpu, monkeypatch):
         assert torch.allclose(outs[0], outs[1], rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize('blocks', ['0', '16'])
+def test_conv_wgrad_halo3(gpu, monkeypatch, blocks):
+    """Weight gradient of 3x3 / stride-1 convs with 32 / 64 input channels and
+    32-channel output tiles on the halo-staged kernel (conv_wgrad_halo3_kernel,
+    EEGAN_CONV wgrad_halo=1, default) against torch fp32 and the tile path
+    (wgrad_halo=0; another fp32 summation order): one, two and three output
+    tiles, blocks with several tiles (wgrad_halo_blocks=16) and blocks past the
+    last tile (their zero partials), accumulation into an existing gradient."""
+    Fn, T, _ = _mods()
+    if blocks != '0':
+        conv_knob(monkeypatch, 'wgrad_halo_blocks', blocks)
+    for N, Cin, H, W, Cout in [(2, 32, 8, 64, 32), (1, 64, 12, 128, 64), (2, 32, 4, 32, 64), (3, 64, 8, 32, 32),
+                               (2, 64, 16, 64, 96)]:
+        torch.manual_seed(N + Cin + H + Cout)
+        g = Fn.Geom(Cout, 3, 3, 1, 1, 1, 0)
+        xl = _bf(torch.randn(N, Cin, H, W))
+        dzl = _bf(torch.randn(N, Cout, H, W))
+        x, dz = _nhwc(xl, gpu), _nhwc(dzl, gpu)
+        outs = []
+        for on in ('0', '1'):
+            conv_knob(monkeypatch, 'wgrad_halo', on)
+            outs.append(Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, 3, 3)).cpu())
+        wr = torch.zeros(Cout, Cin, 3, 3, requires_grad=True)
+        F.conv2d(xl, wr, None, 1, 1).backward(dzl)
+        assert rel_l2(outs[1], wr.grad) < 1e-4, (N, Cin, H, Cout)
+        assert torch.allclose(outs[0], outs[1], rtol=1e-5, atol=1e-4)
+        conv_knob(monkeypatch, 'wgrad_halo', '1')
+        base = (torch.randn(Cout, Cin, 3, 3) * 0.1).to(gpu).contiguous(memory_format=torch.channels_last)
+        acc = base.clone()
+        Fn.conv_bwd_weight_raw(x, dz, g, (Cout, Cin, 3, 3), out=acc)
+        assert torch.allclose(acc.cpu(), base.cpu() + outs[1], rtol=1e-5, atol=1e-4)
+
+
 def test_conv_thin_wgrad_channel_groups(gpu, monkeypatch):
     """The thin weight-gradient kernel for up to 64 output channels, in
     8-channel groups on the grid's y axis (EEGAN_CONV wgrad_thin_maxk): against
