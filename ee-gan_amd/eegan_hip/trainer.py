@@ -66,25 +66,22 @@ GEN_SIDE = True
 # backward kernels do not queue behind the reductions; each optimizer's step
 # waits for its lane (FlatAdam.comm_stream).  Module constant for A/B.
 COMM_LANES = True
-# EEGAN_DREAL_EARLY: discriminators (comma-separated indices, '' = none) whose
-# real-image share of d_loss -- the real and mismatch heads, train.py:338-341 /
-# 357-364, which read the real images, the text embeddings and D's weights as
-# they are at the step's start, nothing the generator makes -- is computed and
-# back-propagated on the D's lane right after the text encoder, beside the
-# generator's forward; d_update then only adds the fake-image share before the
-# first Adam step.  d_loss is a sum over the three heads, so the gradient is the
-# same sum in another accumulation order.
-DREAL_EARLY = tuple(int(i) for i in os.environ.get('EEGAN_DREAL_EARLY', '').split(',') if i.strip())
-# EEGAN_DREAL_LANE: 'own' (the D's lane) or 'damsm' (the DAMSM lane, joined by the
-# origin stream before d_update forks)
-DREAL_LANE = os.environ.get('EEGAN_DREAL_LANE', 'own')
-# EEGAN_LANE_GATE: 'i:j:phase,...' -- D i's lane is forked from the origin stream only
-# once D j's lane has issued `phase` (one of LANE_PHASES), so its kernels do not share
-# the GPU with D j's earlier phases (A/B of the lanes' overlap; '' = all lanes forked
-# together at d_update's start)
+# Measured alternatives kept as module constants (A/B: tools/ab_inproc.py
+# "py:eegan_hip.trainer.NAME=value"; DESIGN.md §3, round 5, all behind the default):
+# DREAL_EARLY -- discriminators whose real-image share of d_loss (the real and
+# mismatch heads, train.py:338-341 / 357-364: they read the real images, the text
+# embeddings and D's weights as they are at the step's start, nothing the generator
+# makes) is computed and back-propagated right after the text encoder, beside the
+# generator's forward, d_update then adding only the fake-image share before the
+# first Adam step (d_loss is a sum over the heads: the same gradient in another
+# accumulation order); DREAL_LANE -- on the D's own lane ('own') or the DAMSM lane
+# ('damsm', joined by the origin stream before d_update forks);
+# LANE_GATE -- {i: (j, phase)}: D i's lane forked from the origin stream only once
+# D j's lane has issued `phase` (one of LANE_PHASES).
+DREAL_EARLY = ()
+DREAL_LANE = 'own'
 LANE_PHASES = ('loss', 'adam', 'gp', 'gpadam', 'gterm')
-LANE_GATE = {int(g.split(':')[0]): (int(g.split(':')[1]), g.split(':')[2])
-             for g in os.environ.get('EEGAN_LANE_GATE', '').split(',') if g.strip()}
+LANE_GATE = {}
 
 # a g_update term already differentiated w.r.t. its fake image on its lane
 # (GTERM_GRAD_EARLY): its value, the image alias and the gradient there
