@@ -148,3 +148,32 @@ def test_words_loss_refuses_wide_captions():
     words = torch.zeros(2, 256, 33)
     with pytest.raises(ValueError, match='up to 32 words'):
         WordsSimFn.apply(regions, words, torch.tensor([33, 5]), False, 0)
+
+
+def test_gradient_penalty_mask_sources_detached_only_inside_the_scope():
+    """functional._mask_src: an act' mask's source activation is detached only
+    inside detached_mask_sources (Trainer.MA_gradient_penalty's first backward)
+    and only for piecewise-constant activations (none / relu / leaky relu); a
+    tanh / sigmoid source keeps its graph (its second derivative is not zero),
+    and the flag is restored on exit, also after an exception."""
+    import torch
+    from eegan_hip import functional as Fn
+    from eegan_hip._lib import ACT_CODES
+    t = torch.ones(3, requires_grad=True) * 2.0
+    assert Fn._mask_src(t, ACT_CODES['lrelu']) is t
+    with Fn.detached_mask_sources():
+        for act in ('relu', 'lrelu', 'none'):
+            d = Fn._mask_src(t, ACT_CODES[act])
+            assert not d.requires_grad and d.data_ptr() == t.data_ptr()
+        for act in ('tanh', 'sigmoid'):
+            assert Fn._mask_src(t, ACT_CODES[act]) is t
+        assert Fn._mask_src(None, ACT_CODES['relu']) is None
+    assert not Fn.DETACH_MASK_SRC
+    try:
+        with Fn.detached_mask_sources():
+            raise KeyError('x')
+    except KeyError:
+        pass
+    assert not Fn.DETACH_MASK_SRC
+    with Fn.detached_mask_sources(False):
+        assert Fn._mask_src(t, ACT_CODES['relu']) is t
