@@ -9,6 +9,8 @@ per GPU, bf16 activations / fp32 master weights, synthetic data, random
 initialised weights (no datasets/checkpoints offline).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
+        (N > 1: starts `torch.distributed.run --standalone --nproc-per-node N
+        bench.py ...` as a child job, one rank per GPU, and relays rank 0's line)
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
 Prints ONE JSON line on rank 0 (see the repo README / task contract), with a
@@ -154,7 +156,7 @@ def cpu_baseline(seconds_budget=30.0):
     timed on the host: BASELINE.md's CPU plan -- W=32, B=4, the five frozen
     text-encoder calls (train.py:169-184) inside the step, the full 3-stage
     step (incl. the Inception-v3 restatement) and the C1 stage-1 slice;
-    warm-ups until two consecutive steps agree within 10 %, then the median of
+    warm-ups until three consecutive steps agree within 5 % (at most 15), then the median of
     at least 10 steps; threads = the affinity set capped by the box's CPU
     share (stated as `threads_reason`)."""
     from oracle import eegan_oracle as O
@@ -165,7 +167,7 @@ def cpu_baseline(seconds_budget=30.0):
     # the host cores this process may use: the affinity set, capped by the
     # scheduler's share when the environment states one (OMP_NUM_THREADS: the
     # GPU box's affinity mask spans the whole machine, its CPU share is 16)
-    share = int(os.environ.get('OMP_NUM_THREADS') or 0)
+    share = int(os.environ.get('EEGAN_CPU_SHARE') or os.environ.get('OMP_NUM_THREADS') or 0)
     torch.set_num_threads(min(affinity, share) if share > 0 else affinity)
     B, W, ncls = 4, 32, 200
     spec = lambda m: [(k, tuple(v.shape)) for k, v in m.state_dict().items()]  # noqa: E731
@@ -190,19 +192,18 @@ def cpu_baseline(seconds_budget=30.0):
                                                                       models.Dis256(W, True, ncls)][:nd])]
         nets = O.OracleNets(sd_g, sd_a, sd_ds, W, W, True, ncls)
         og, ods = O.make_adams(nets)
-        # warm-ups until two consecutive steps agree within 10 % (the first steps run up to
-        # 2x slower: allocator and thread-pool warm-up), at most 8
-        prev, warm = None, 0
-        while warm < 8:
+        # warm-ups until three consecutive steps agree within 5 % (the first steps run up to
+        # 2x slower: allocator, thread-pool and page warm-up), at most 15
+        hist, warm = [], 0
+        while warm < 15:
             t0 = time.time()
             O.train_step(nets, og, ods, batch, encode_text(), enc, stages=stages)
-            dt = time.time() - t0
+            hist.append(time.time() - t0)
             warm += 1
             print('bench: cpu baseline (%d stage%s) warm-up %d: %.2f s' % (stages, 's' if stages > 1 else '', warm,
-                                                                         dt), file=sys.stderr, flush=True)
-            if prev is not None and abs(dt - prev) <= 0.1 * prev:
+                                                                         hist[-1]), file=sys.stderr, flush=True)
+            if len(hist) >= 3 and max(hist[-3:]) <= 1.05 * min(hist[-3:]):
                 break
-            prev = dt
         times = []
         t_end = time.time() + budget
         while len(times) < 10 or (time.time() < t_end and len(times) < 20):
@@ -218,6 +219,10 @@ def cpu_baseline(seconds_budget=30.0):
         return B / times[len(times) // 2], len(times)
 
     warmups = {}
+    try:   # before the first parallel op (the child process runs nothing else first)
+        torch.set_num_interop_threads(1)
+    except RuntimeError:
+        pass
     full, n_full = timed(3, seconds_budget)
     c1, n_c1 = timed(1, 0.25 * seconds_budget)
     return {'value': full, 'unit': 'images/sec', 'cores': torch.get_num_threads(), 'kind': 'port',
@@ -227,11 +232,71 @@ def cpu_baseline(seconds_budget=30.0):
             if 0 < share < affinity else 'all affinity cores',
             'sample': 'oracle train_step (full 3-stage, W=32, B=4: 5 text-encoder calls, G, 3 x d_update incl. '
                       'the gradient penalty, g_update incl. the Inception-v3 restatement), median of %d steps after '
-                      '%d warm-ups (until two consecutive steps agreed within 10%%); max/min spread of the timed '
+                      '%d warm-ups (until three consecutive steps agreed within 5%%); max/min spread of the timed '
                       'steps %.2f' % (n_full, warmups[3][0], warmups[3][1]),
+            'binding': 'own process; OMP_PROC_BIND=%s OMP_PLACES=%s, %d intra-op threads, %d inter-op' % (
+                os.environ.get('OMP_PROC_BIND', 'unset'), os.environ.get('OMP_PLACES', 'unset'),
+                torch.get_num_threads(), torch.get_num_interop_threads()),
+            'timed_spread': round(warmups[3][1], 4),
             'c1_stage1': {'value': c1, 'unit': 'images/sec', 'sample': 'C1 stage-1 slice (img_64, Dis64, DAMSM on '
                                                                        'img_64), B=4, median of %d steps after %d '
                                                                        'warm-ups' % (n_c1, warmups[1][0])}}
+
+
+def launcher_argv(n, argv):
+    """The child job `python bench.py --gpus N` starts when no launcher set
+    WORLD_SIZE: torch.distributed.run with one rank per GPU of this node and
+    a rendezvous store that binds its own port (--standalone: c10d on port 0)
+    on 127.0.0.1 -- the same per-rank bench.py, unchanged arguments."""
+    return [sys.executable, '-m', 'torch.distributed.run', '--standalone', '--local-addr', '127.0.0.1',
+            '--nnodes=1', '--nproc-per-node', str(n), os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n, argv):
+    """Run the N-rank job as a child process (never exec: nothing here has
+    touched the GPU, and the child is a fresh interpreter), relay rank 0's
+    JSON line to stdout (anything else the ranks print to stdout goes to
+    stderr) and return the job's exit status."""
+    import subprocess
+    cmd = launcher_argv(n, argv)
+    print('bench: --gpus %d without WORLD_SIZE: launching %s' % (n, ' '.join(cmd)), file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    line = None
+    for raw in p.stdout:
+        try:
+            rec = json.loads(raw)
+        except ValueError:
+            rec = None
+        if isinstance(rec, dict) and 'metric' in rec:
+            line = raw.strip()
+        else:
+            sys.stderr.write(raw)
+            sys.stderr.flush()
+    rc = p.wait()
+    if line is not None:
+        print(line, flush=True)
+    if rc == 0 and line is None:
+        print('bench: the %d-rank job printed no result line' % n, file=sys.stderr, flush=True)
+        return 1
+    return rc
+
+
+def cpu_baseline_child(seconds):
+    """cpu_baseline() in a fresh process of its own (no HIP runtime threads,
+    OpenMP threads bound to cores from the start: OMP_PROC_BIND / OMP_PLACES
+    only act before OpenMP starts, which in this process happened long ago),
+    started after the GPU measurement; returns its JSON object."""
+    import subprocess
+    env = dict(os.environ, OMP_PROC_BIND='close', OMP_PLACES='cores')
+    share = int(os.environ.get('OMP_NUM_THREADS') or 0)
+    if share > 0:
+        env['EEGAN_CPU_SHARE'] = str(share)
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), '--cpu-baseline-only',
+                        '--cpu-seconds', str(seconds)], env=env, stdout=subprocess.PIPE, text=True, timeout=900)
+    lines = [l for l in r.stdout.splitlines() if l.startswith('{')]
+    if r.returncode != 0 or not lines:
+        return {'error': 'cpu baseline child exited %d' % r.returncode}
+    return json.loads(lines[-1])
 
 
 def main():
@@ -242,11 +307,22 @@ def main():
     ap.add_argument('--config', default='C2', choices=sorted(CONFIGS))
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=30.0)
+    ap.add_argument('--cpu-baseline-only', action='store_true', help=argparse.SUPPRESS)
     ap.add_argument('--no-timer', action='store_true', help='diagnostic: skip the roofline timing pass')
     ap.add_argument('--timing-steps', type=int, default=2, help='eager steps of the roofline timing pass')
     ap.add_argument('--graph', default='auto', choices=['auto', 'on', 'off'],
                     help='replay the step as one captured HIP graph (auto: on; N > 1 needs the own RCCL communicators)')
     args = ap.parse_args()
+    if args.cpu_baseline_only:   # the child of cpu_baseline_child(): no GPU
+        print(json.dumps(cpu_baseline(args.cpu_seconds)), flush=True)
+        return
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        # `python bench.py --gpus N` without a launcher: start the N ranks as a child job
+        # (one process per GPU, RCCL) before this process touches the GPU; no exec
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if int(os.environ.get('WORLD_SIZE', '1')) != args.gpus:
+        raise SystemExit('bench: --gpus %d but WORLD_SIZE=%s: refusing to report a number for another GPU '
+                         'count' % (args.gpus, os.environ.get('WORLD_SIZE', '1')))
 
     from eegan_hip import dist as D
     from eegan_hip import functional as Fn
@@ -257,6 +333,9 @@ def main():
     torch.cuda.set_device(local_rank)
     device = torch.device('cuda', local_rank)
     rank, world = D.init_from_env()
+    if world != args.gpus:
+        raise SystemExit('bench: --gpus %d but the job has %d rank(s) (WORLD_SIZE=%s): refusing to report a '
+                         'number for another GPU count' % (args.gpus, world, os.environ.get('WORLD_SIZE')))
     T, B, ncls = build(args.config, device)
     batch = make_batch(B, device, seed=3407 + rank, class_num=ncls, with_class=True, id_offset=rank * B)
 
@@ -404,7 +483,7 @@ def main():
         out['graph_capture_error'] = graph_error
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            out['cpu_baseline'] = cpu_baseline(args.cpu_seconds)
+            out['cpu_baseline'] = cpu_baseline_child(args.cpu_seconds)
         except Exception as e:  # baseline is reported, never fatal for the GPU measurement
             out['cpu_baseline'] = {'error': repr(e)}
     if rank == 0:

@@ -861,7 +861,9 @@ EE_DEV void splitk_fused_finish(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ],
   __syncthreads();
   if (tid == 0) {
     int* c = a.ctr + tile;
-    const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // release: this block's partial tile is visible device-wide before its ticket;
+    // acquire: the last arriver sees every other split's partial (across XCD L2s)
+    const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     s_last = old == a.nsplit - 1;
     if (old == a.nsplit - 1) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }

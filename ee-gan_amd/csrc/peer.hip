@@ -10,6 +10,7 @@
 //   [0, 256)     flags[2][16] uint64   flags[parity][src] = epoch of src's slice
 //   [256, 264)   counter uint64        epoch of the last completed call (local)
 //   [264, 268)   error   uint32        set when a wait timed out (local)
+//   [268, 272)   wait    uint32        the wait bound in seconds (0: 30 s); eegan_peer_set_wait
 //   [512, ...)   data[2][16][cap] fp64 data[parity][src][i]
 //
 // A call (one 256-thread block): read epoch e = counter + 1, write this rank's
@@ -22,7 +23,8 @@
 // parity of epoch e.  The epoch lives on the device, so a captured call keeps
 // counting when the step graph is replayed.
 //
-// Every wait is bounded (30 s of the 100 MHz wall clock): a rank whose peer
+// Every wait is bounded (30 s of the 100 MHz wall clock by default, per region
+// eegan_peer_set_wait / EEGAN_PEER_WAIT_S): a rank whose peer
 // never arrives records an error and exits, so the grid always drains;
 // eegan_peer_status reports it.  A call that finds the error word set in the
 // own region or in any peer's (a wait of this lane already gave up on some
@@ -37,14 +39,15 @@
 namespace {
 
 constexpr int PEER_MAXW = 16;
-constexpr long OFF_CTR = 256, OFF_ERR = 264, OFF_DATA = 512;
+constexpr long OFF_CTR = 256, OFF_ERR = 264, OFF_WAIT = 268, OFF_DATA = 512;
 // bounded wait for the peers' slices: long enough for host-side skew between
 // ranks (a checkpoint save or an evaluation on one rank while the others wait
 // in their next step), short enough that a dead peer ends the job: on timeout
 // the error word is set and the result is poisoned with NaN (visible in the BN
 // statistics at once); the trainer checks the error word and raises
 // (eegan_hip.peer.PeerAllReduce.check, Trainer.check_collectives)
-constexpr unsigned long long WAIT_TICKS = 3000000000ull;  // 30 s at 100 MHz
+constexpr unsigned long long TICKS_PER_S = 100000000ull;  // wall_clock64: 100 MHz
+constexpr unsigned DEFAULT_WAIT_S = 30;
 
 struct PeerSet {
   char* base[PEER_MAXW];
@@ -62,7 +65,7 @@ __global__ __launch_bounds__(256) void peer_allreduce_kernel(double* t, int n, i
   const int tid = threadIdx.x;
   char* own = ps.base[rank];
   unsigned long long* ctr = reinterpret_cast<unsigned long long*>(own + OFF_CTR);
-  __shared__ unsigned long long s_ep;
+  __shared__ unsigned long long s_ep, s_wait;
   __shared__ int s_timeout;
   if (tid == 0) {
     s_ep = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1ull;
@@ -71,11 +74,15 @@ __global__ __launch_bounds__(256) void peer_allreduce_kernel(double* t, int n, i
       err |= __hip_atomic_load(reinterpret_cast<unsigned*>(ps.base[p] + OFF_ERR), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
     s_timeout = err != 0u;   // an earlier call of this lane gave up on a rank: poison at once
+    const unsigned ws = __hip_atomic_load(reinterpret_cast<unsigned*>(own + OFF_WAIT), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_SYSTEM);
+    s_wait = (unsigned long long)(ws ? ws : DEFAULT_WAIT_S) * TICKS_PER_S;
   }
   __syncthreads();
   const unsigned long long ep = s_ep;
   const int par = (int)(ep & 1ull);
   const bool live = s_timeout == 0;
+  const unsigned long long wait_ticks = s_wait;
 
   // push this rank's message into every rank's slot [par][rank]
   for (int p = 0; p < world && live; ++p) {
@@ -92,7 +99,7 @@ __global__ __launch_bounds__(256) void peer_allreduce_kernel(double* t, int n, i
     const unsigned long long t0 = wall_clock64();
     unsigned long long* f = flag_at(own, par, tid);
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != ep) {
-      if (wall_clock64() - t0 > WAIT_TICKS) {
+      if (wall_clock64() - t0 > wait_ticks) {
         __hip_atomic_store(reinterpret_cast<unsigned*>(own + OFF_ERR), 1u + (unsigned)tid, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
         s_timeout = 1;
@@ -197,6 +204,20 @@ int eegan_peer_allreduce_f64(double* t, int n, int cap, int rank, int world, voi
   }
   ee_launch(peer_allreduce_kernel, dim3(1), dim3(256), 0, s, t, n, cap, rank, world, ps);
   EE_LAUNCH_CHECK("peer_allreduce_kernel");
+}
+
+int eegan_peer_set_wait(void* own, int seconds) {
+  if (!own || seconds < 1 || seconds > 86400) {
+    ee_set_error("peer_set_wait: bad arguments (seconds=%d, 1..86400)", seconds);
+    return -1;
+  }
+  const unsigned v = (unsigned)seconds;
+  hipError_t e = hipMemcpy(static_cast<char*>(own) + OFF_WAIT, &v, sizeof(v), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    ee_set_error("peer_set_wait: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
 }
 
 int eegan_peer_status(void* own, int reset, int* timed_out) {

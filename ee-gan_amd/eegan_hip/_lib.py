@@ -146,6 +146,7 @@ _SIGS = {
     'eegan_peer_close': ([P], I),
     'eegan_peer_free': ([P], I),
     'eegan_peer_allreduce_f64': ([P, I, I, I, I, P, P], I),
+    'eegan_peer_set_wait': ([P, I], I),
     'eegan_peer_status': ([P, I, P], I),
     'eegan_pipe_workspace': ([I, I, I, I, P], L),
     'eegan_pipe_transform': ([P, P, I, I, I, P, P, I, P, P, P, I, P, P, P], I),
@@ -166,7 +167,7 @@ def _load():
 
 LIB = _load()
 ABI_VERSION = LIB.eegan_abi_version()
-EXPECTED_ABI = 13
+EXPECTED_ABI = 14
 if ABI_VERSION != EXPECTED_ABI:
     raise ImportError('%s has ABI %d, these bindings need %d: rebuild (make -C ee-gan_amd/csrc)'
                       % (LIB_PATH, ABI_VERSION, EXPECTED_ABI))

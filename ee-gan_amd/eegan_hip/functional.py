@@ -202,8 +202,9 @@ class Geom:
 # capture keeps the two-launch reduce.  SPLITK_FUSED = False: always two launches.
 # The library uses the counters only with EEGAN_CONV splitk_fused=1: on the replayed
 # C2 step the in-kernel finish measured -0.7 % against the separate reduce launch
-# (in-process A/B, profiles/r05_inproc_ab.txt), so the reduce launch is the default.
-SPLITK_FUSED = True
+# (in-process A/B, profiles/r05_inproc_ab.txt), so the reduce launch is the default
+# and no counters are allocated unless both switches are on (EEGAN_SPLITK_FUSED=1).
+SPLITK_FUSED = os.environ.get('EEGAN_SPLITK_FUSED', '0') == '1'
 SPLITK_CTR_N = 1 << 15
 _SPLITK_CTR = {}
 

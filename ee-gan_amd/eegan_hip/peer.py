@@ -24,6 +24,7 @@ group's regular all-reduce; host tensors (CPU process groups) take
 (the gloo tests): all-gather, then 0 + m_0 + ... + m_{W-1} in fp64.
 """
 import ctypes as C
+import os
 
 import torch
 import torch.distributed as dist
@@ -32,6 +33,14 @@ from ._lib import LIB, ops
 
 MAX_RANKS = 16
 CAP = 4096   # doubles per message: SyncBN sends 2C values, C <= 2048
+# how long a reduction waits for a peer's slice before it gives up, poisons its
+# result with NaN and sets the region's error word (Trainer.check_collectives then
+# raises within CHECK_EVERY steps, which ends the run).  Host-side skew beyond
+# this -- a rank writing a checkpoint, DataLoader workers respawning at an epoch
+# boundary while the others already wait in their next SyncBN call -- is
+# indistinguishable from a dead peer, so size it above the longest expected
+# stall (EEGAN_PEER_WAIT_S, seconds; RCCL itself waits without bound)
+WAIT_S = int(os.environ.get('EEGAN_PEER_WAIT_S', '30'))
 
 
 class PeerRegion(object):
@@ -52,6 +61,7 @@ class PeerRegion(object):
             with torch.cuda.device(device if device is not None else torch.cuda.current_device()):
                 ops.peer_alloc(nbytes, C.byref(own), handle)
             self.own = own.value
+            ops.peer_set_wait(self.own, WAIT_S)
         except Exception as e:
             err = str(e)
         self._opened = []
@@ -140,8 +150,13 @@ class PeerAllReduce(object):
                 return r
         elif why is None:
             why = 'another rank could not set up its region'
+        # every rank joins one more exchange before any region is unmapped (no peer may
+        # still be writing into it), whether or not it holds a region: a rank that
+        # failed in PeerRegion has none, and skipping the round there would leave the
+        # others waiting in it.  An exchange, not dist.barrier: on the default group it
+        # stays on the lane's own communicator (ProcessGroupNCCL is kept off this path)
+        _exchange(b'\x00', self.group)
         if r is not None:
-            dist.barrier(group=self.group)
             r.close()
         self.fallback = why or 'a peer rank failed the test exchange'
         import warnings
@@ -186,7 +201,8 @@ class PeerAllReduce(object):
         t = self.timed_out()
         if t:
             raise RuntimeError('eegan_hip.peer: a SyncBN peer-write all-reduce timed out waiting for rank %d '
-                               '(a rank died or stalled > 30 s); its BN statistics are NaN' % (t - 1))
+                               '(a rank died or stalled > %d s, EEGAN_PEER_WAIT_S); its BN statistics are NaN'
+                               % (t - 1, WAIT_S))
 
     def close(self):
         for r in self.regions.values():

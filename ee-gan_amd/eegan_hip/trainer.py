@@ -135,6 +135,9 @@ class Trainer(object):
     def _side_streams(self, n, fork=True):
         if not self.use_streams:
             return [None] * n
+        # lanes 4 / 5 carry the communication lanes' RCCL communicators (_comm_lanes): a
+        # compute lane bound to the same communicator would issue on it from a second stream
+        assert n <= 4, 'at most 4 compute lanes (communicators 4 and 5 are the comm lanes)'
         if self._streams is None or len(self._streams) < n:
             # the last discriminator's lane (the largest D: the step's critical
             # path through d_update and g_update) at high priority, the others

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 13  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
+#define EEGAN_ABI_VERSION 14  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
                                 4: rectangular (local x global) DAMSM words / sentence blocks on MFMA;
                                 5: GlobalAttentionGeneral (eegan_gag_*), words backward reuses the forward's prep;
                                 6: device input pipeline (eegan_pipe_*);
@@ -37,7 +37,8 @@ extern "C" {
                                 10: FID generator-sample input (eegan_fid_samples);
                                 11: BN forward with the finalize folded in (eegan_bnmod_fwd_fin);
                                 12: ScaleAdd double backward in one pass (eegan_scale_dot_res);
-                                13: split-K counters in the conv descriptor, for the in-kernel split-K finish */
+                                13: split-K counters in the conv descriptor, for the in-kernel split-K finish;
+                                14: per-region peer wait bound (eegan_peer_set_wait) */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
@@ -392,6 +393,7 @@ int eegan_fid_stats(const float* act, int N, int D, double* mu, double* sigma, v
  *   open(h, &base) / close   map / unmap a peer's region; free releases an own region;
  *   allreduce_f64(t, n, cap, rank, world, bases, s)  in-place sum of t[0..n) over the ranks; bases = host
  *                            array of `world` region pointers (own at [rank]); every wait is bounded;
+ *   set_wait(own, seconds)   the bound of every wait on this region (default 30 s);
  *   status(own, reset, &timed_out)  nonzero timed_out: a wait gave up (1 + the missing rank). */
 long eegan_peer_region_bytes(int cap);
 int eegan_peer_alloc(long bytes, void** base, void* handle);
@@ -399,6 +401,7 @@ int eegan_peer_open(const void* handle, void** base);
 int eegan_peer_close(void* base);
 int eegan_peer_free(void* base);
 int eegan_peer_allreduce_f64(double* t, int n, int cap, int rank, int world, void* const* bases, hipStream_t s);
+int eegan_peer_set_wait(void* own, int seconds);
 int eegan_peer_status(void* own, int reset, int* timed_out);
 
 /* -------------------------------------------------------------------- adam --

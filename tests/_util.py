@@ -15,6 +15,18 @@ for p in (REPO, PKG):
 
 from oracle.seeding import summary, seeded_state  # noqa: E402
 
+
+def torchrun_argv(nproc):
+    """`python -m torch.distributed.run` for one node with its rendezvous port
+    bound atomically: --standalone runs the c10d rendezvous on port 0 and the
+    agent's TCPStore binds it itself, so no test picks a port, releases it and
+    hands the number to a later bind (round 5's EADDRINUSE race).  The store
+    and the workers' MASTER_ADDR stay on 127.0.0.1 (the host name may not
+    resolve)."""
+    return [sys.executable, '-m', 'torch.distributed.run', '--standalone', '--local-addr', '127.0.0.1',
+            '--nnodes=1', '--nproc-per-node', str(nproc)]
+
+
 _GOLD = None
 
 

@@ -13,7 +13,6 @@ train.py -- disjoint images, different noise, an epoch that covers the split
 once, and identical weights after the broadcast."""
 import os
 import pickle
-import socket
 import subprocess
 import sys
 
@@ -21,15 +20,12 @@ import numpy as np
 import pytest
 import torch
 
+from _util import torchrun_argv  # noqa: E402
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import _pipeline_data as PD  # noqa: E402
 
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(('127.0.0.1', 0))
-        return s.getsockname()[1]
 
 
 @pytest.mark.parametrize('world', [1, 2, 3, 4])
@@ -183,9 +179,7 @@ def test_torchrun_ranks_draw_their_own_data(tmp_path):
     does; nothing in the script mentions ranks."""
     data = tmp_path / 'data'
     PD.build(str(data))
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
-           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
-           os.path.join(HERE, 'shard_worker.py'), str(data), str(tmp_path)]
+    cmd = torchrun_argv(2) + [os.path.join(HERE, 'shard_worker.py'), str(data), str(tmp_path)]
     env = dict(os.environ, OMP_NUM_THREADS='1', EEGAN_DIST_BACKEND='gloo')
     env.pop('EEGAN_AUTO_DIST', None)
     r = subprocess.run(cmd, env=env, timeout=240, capture_output=True, text=True)

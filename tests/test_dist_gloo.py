@@ -5,8 +5,9 @@ the differentiable all-gather behind global-batch DAMSM, gradient averaging
 statistics combine (fp64 sums all-reduced, then the reference's multi-device
 formula, sync_batchnorm/batchnorm.py:113-125) against the oracle."""
 import os
-import socket
+import shutil
 import sys
+import tempfile
 
 import numpy as np
 import pytest
@@ -19,23 +20,22 @@ from _util import REPO
 WORLD = 2
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(('127.0.0.1', 0))
-        return s.getsockname()[1]
-
-
 def _run(fn, *args, world=WORLD):
-    port = _free_port()
-    mp.spawn(_entry, args=(fn, port, args, world), nprocs=world, join=True)
+    # a file:// store under a fresh directory: no TCP port to pick and lose
+    # to another bind between the pick and the store's own bind
+    d = tempfile.mkdtemp(prefix='eegan_gloo_')
+    try:
+        mp.spawn(_entry, args=(fn, 'file://' + os.path.join(d, 'store'), args, world), nprocs=world, join=True)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
-def _entry(rank, fn, port, args, world):
+def _entry(rank, fn, init_method, args, world):
     sys.path.insert(0, os.path.join(REPO, 'ee-gan_amd'))
     sys.path.insert(0, REPO)
-    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world))
     torch.set_num_threads(1)
-    dist.init_process_group('gloo', rank=rank, world_size=world)
+    dist.init_process_group('gloo', init_method=init_method, rank=rank, world_size=world)
     try:
         fn(rank, *args)
     finally:
@@ -269,6 +269,46 @@ def _case_syncbn_peer_combine(rank):
     finally:
         D.PEER = None
         D.install_syncbn_hook()
+
+
+def _case_peer_build_fallback_one_rank_fails(rank):
+    """PeerAllReduce._build when only the last rank cannot map its peers'
+    regions (peer_open failing there): every rank must agree on the fallback,
+    no rank may block in a round the failing rank skips, and the ranks that
+    did build a region close it after the closing exchange."""
+    from eegan_hip import peer as P
+
+    closed = []
+
+    class FakeRegion(object):
+        def __init__(self, group, cap):
+            if dist.get_rank(group) == dist.get_world_size(group) - 1:
+                raise RuntimeError('peer_open: simulated failure')
+
+        def close(self):
+            closed.append(True)
+
+    real = P.PeerRegion
+    P.PeerRegion = FakeRegion
+    try:
+        red = P.PeerAllReduce(group=dist.group.WORLD)
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter('ignore')
+            assert red._build() is None
+    finally:
+        P.PeerRegion = real
+    assert red.fallback is not None
+    last = rank == dist.get_world_size() - 1
+    assert closed == ([] if last else [True]), (rank, closed)
+    # and the group is still in step: one more collective completes on every rank
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    assert float(t) == dist.get_world_size()
+
+
+def test_gloo_world3_peer_build_fallback():
+    _run(_case_peer_build_fallback_one_rank_fails, world=3)
 
 
 def test_gloo_world3_syncbn_peer_combine():

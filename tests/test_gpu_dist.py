@@ -10,8 +10,8 @@ post-accumulate-grad hooks), and they match ONE process stepping the whole
 batch (the reference's DataParallel semantics: global-batch SyncBN
 statistics with the multi-device numerics, global DAMSM similarity matrices,
 means over the global batch) within bf16 rounding."""
+import json
 import os
-import socket
 import subprocess
 import sys
 
@@ -20,13 +20,10 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
+from _util import torchrun_argv  # noqa: E402
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(('127.0.0.1', 0))
-        return s.getsockname()[1]
 
 
 def test_dropin_train_step_two_ranks(gpu, tmp_path, monkeypatch):
@@ -40,9 +37,7 @@ def test_dropin_train_step_two_ranks(gpu, tmp_path, monkeypatch):
     import _pipeline_data as PD
     data = tmp_path / 'data'
     PD.build(str(data))
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
-           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
-           os.path.join(HERE, 'dp_dropin_worker.py'), str(data), str(tmp_path)]
+    cmd = torchrun_argv(2) + [os.path.join(HERE, 'dp_dropin_worker.py'), str(data), str(tmp_path)]
     # the worker never calls torch.distributed / eegan_hip.dist: importing the drop-in
     # modules under torchrun pins each rank's GPU and starts the group (eegan_hip.launch);
     # gloo because both ranks share this box's one GPU (RCCL refuses that)
@@ -100,9 +95,7 @@ def test_flat_adam_overlapped_allreduce_two_ranks(gpu, tmp_path):
     res = {}
     for tag, ov, extra in (('ov', '1', {}), ('seq', '0', {}),
                            ('plain', '1', {'DP_GEN_SIDE': '0', 'DP_COMM_LANES': '0'})):
-        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
-               '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
-               os.path.join(HERE, 'dp_trainer_worker.py'), str(tmp_path), tag]
+        cmd = torchrun_argv(2) + [os.path.join(HERE, 'dp_trainer_worker.py'), str(tmp_path), tag]
         env = dict(os.environ, OMP_NUM_THREADS='2', EEGAN_GRAD_OVERLAP=ov, **extra)
         r = subprocess.run(cmd, env=env, timeout=240, capture_output=True, text=True)
         assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -129,9 +122,7 @@ def test_force_dist_captured_step_with_comm_lanes(gpu, tmp_path):
     step and to the step with the buckets reduced in their writing lanes."""
     res = {}
     for tag, mode, lanes in (('eager', 'eager', '1'), ('graph', 'graph', '1'), ('inlane', 'graph', '0')):
-        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '1',
-               '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
-               os.path.join(HERE, 'dp_force_worker.py'), str(tmp_path), tag, mode]
+        cmd = torchrun_argv(1) + [os.path.join(HERE, 'dp_force_worker.py'), str(tmp_path), tag, mode]
         env = dict(os.environ, OMP_NUM_THREADS='2', EEGAN_FORCE_DIST='1', DP_COMM_LANES=lanes)
         env.pop('EEGAN_DIST_BACKEND', None)
         r = subprocess.run(cmd, env=env, timeout=240, capture_output=True, text=True)
@@ -143,3 +134,23 @@ def test_force_dist_captured_step_with_comm_lanes(gpu, tmp_path):
     print('FORCE_DIST max |graph - eager| %.3e' % float(d))
     assert torch.equal(res['graph']['state'], res['eager']['state'])
     assert torch.equal(res['graph']['state'], res['inlane']['state'])
+
+
+def test_bench_gpus_2_launches_two_ranks(gpu):
+    """`python bench.py --gpus 2` with no launcher (the driver's N = 1 command
+    form with N = 2) starts a two-rank child job and relays rank 0's line for
+    2 GPUs and the global batch of both ranks.  Both ranks share this box's
+    one GPU (EEGAN_SHARE_GPU=1, gloo: RCCL refuses two ranks on one device),
+    so the number itself is a rehearsal, not a 2-GPU measurement."""
+    env = dict(os.environ, EEGAN_SHARE_GPU='1', EEGAN_DIST_BACKEND='gloo', OMP_NUM_THREADS='2')
+    env.pop('WORLD_SIZE', None)
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(HERE), 'bench.py'), '--gpus', '2',
+                        '--steps', '2', '--warmup', '1', '--no-cpu-baseline', '--timing-steps', '1'],
+                       env=env, timeout=400, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    print('bench --gpus 2 (two ranks on one GPU):', rec['value'], rec['unit'], rec['execution'])
+    assert rec['n_gpus'] == 2 and rec['config']['global_batch'] == 32 and rec['config']['parallelism'] == 'dp2'
+    assert rec['value'] > 0 and rec['steps'] == 2

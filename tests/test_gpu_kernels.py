@@ -213,6 +213,7 @@ def test_splitk_reduce_vector_path_bit_identical(gpu, monkeypatch):
     counts take the scalar path in both runs.  EEGAN_CONV target= forces the
     K split on these small grids."""
     Fn, T, _ = _mods()
+    monkeypatch.setattr(Fn, 'SPLITK_FUSED', True)   # counters off by default (the reduce launch is)
     conv_knob(monkeypatch, 'target', '4096')
     conv_knob(monkeypatch, 'mink', '2')
     lrelu = Fn.ACT_CODES['lrelu']
@@ -250,6 +251,7 @@ def test_splitk_fused_finish_bit_identical(gpu, monkeypatch):
     half-resolution residual, stride-2 parity classes), repeated launches and
     two streams at once; every counter is back at zero afterwards."""
     Fn, T, _ = _mods()
+    monkeypatch.setattr(Fn, 'SPLITK_FUSED', True)   # counters off by default (the reduce launch is)
     conv_knob(monkeypatch, 'target', '4096')
     conv_knob(monkeypatch, 'mink', '2')
     lrelu = Fn.ACT_CODES['lrelu']

@@ -15,15 +15,15 @@ import sys
 import pytest
 import torch
 
-from test_gpu_dist import _free_port
 
 pytestmark = pytest.mark.gpu
+from _util import torchrun_argv  # noqa: E402
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def _torchrun(script, *args, env=None):
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
-           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), os.path.join(HERE, script)] + list(args)
+    cmd = torchrun_argv(2) + [os.path.join(HERE, script)] + list(args)
     r = subprocess.run(cmd, env=dict(os.environ, OMP_NUM_THREADS='2', **(env or {})), timeout=240,
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

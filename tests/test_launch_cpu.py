@@ -3,20 +3,16 @@ visible-device environment, and an unchanged-train.py-shaped torchrun job
 whose ranks are joined by importing the drop-in modules alone (gloo), or,
 with the auto start switched off, refuse to train unsynchronised."""
 import os
-import socket
 import subprocess
 import sys
 
 import pytest
 import torch
 
+from _util import torchrun_argv  # noqa: E402
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(('127.0.0.1', 0))
-        return s.getsockname()[1]
 
 
 @pytest.mark.parametrize('env,n,want', [
@@ -62,9 +58,7 @@ def test_pin_sets_rank_device(monkeypatch):
 
 @pytest.mark.parametrize('auto', ['1', '0'])
 def test_torchrun_ranks_join_at_import(tmp_path, auto):
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
-           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
-           os.path.join(HERE, 'launch_worker.py'), str(tmp_path)]
+    cmd = torchrun_argv(2) + [os.path.join(HERE, 'launch_worker.py'), str(tmp_path)]
     env = dict(os.environ, OMP_NUM_THREADS='1', EEGAN_AUTO_DIST=auto, EEGAN_DIST_BACKEND='gloo')
     r = subprocess.run(cmd, env=env, timeout=180, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
