@@ -366,6 +366,15 @@ def main():
 
         for _ in range(args.warmup):
             step()
+    # window markers for tools/rocprof_families.py (a one-thread stamp kernel at both
+    # ends of the timed region and of the timing pass), outside the timed region
+    from eegan_hip._lib import ops as _ops
+    marks = torch.zeros(4, dtype=torch.int64, device=device)
+
+    def mark(i):
+        _ops.stamp(marks.data_ptr() + 8 * i, torch.cuda.current_stream().cuda_stream)
+
+    mark(0)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -379,6 +388,7 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    mark(1)
     if world > 1:
         t = torch.tensor([dt], device=device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -398,8 +408,10 @@ def main():
         # single stream while timing: a dispatch sharing the GPU with another
         # stream's kernels would read longer than its own work
         streams, T.use_streams = T.use_streams, False
+        mark(2)
         for _ in range(per):
             T.train_step(batch)
+        mark(3)
         T.use_streams = streams
         Fn.TIMER = None
     kern = timer.summary() if timer is not None else {'conv_fwd': [1, 0.0, 0.0, 1.0]}
@@ -459,6 +471,22 @@ def main():
             if traffic and pf.get('avg_call_us') else None,
             'conv_path_pmc_hbm_frac': conv_path_hbm_frac(pfams),
             'families': fam_out}
+    # the same family in the replayed step (rocprofv3 kernel trace of the timed replays,
+    # tools/rocprof_families.py): algorithmic FLOPs per step over in-step kernel time,
+    # read from the summary so that it recomputes from that file alone
+    if pf.get('frac_in_step') is not None:
+        roof['frac_in_step'] = pf['frac_in_step']
+        roof['in_step_ms_per_step'] = pf.get('ms_per_step')
+        roof['in_step_avg_call_us'] = pf.get('avg_call_us')
+        roof['pmc_over_algorithmic'] = pf.get('pmc_over_algorithmic', roof['pmc_over_algorithmic'])
+        tp = (summ or {}).get('timing_pass', {}).get(kind)
+        if tp:   # rocprof's view of the timing pass this line's `frac` comes from
+            roof['rocprof_timing_pass_avg_call_us'] = tp['avg_call_us']
+    cpath = (summ or {}).get('conv_path')
+    if cpath:
+        roof['conv_path_algorithmic_hbm_frac'] = cpath.get('algorithmic_hbm_frac')
+        roof['conv_path_pmc_hbm_frac'] = cpath.get('pmc_hbm_frac', roof['conv_path_pmc_hbm_frac'])
+        roof['conv_path_source'] = traffic_src
     out = {'metric': 'train images/sec at 256x256 CUB, G+D step', 'value': round(value, 3), 'unit': 'images/sec',
            'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16',

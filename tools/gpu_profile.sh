@@ -18,7 +18,7 @@ step 900 prof_write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -
 step 900 prof_mfma rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $O/mfma -o run -- \
   python3 bench.py --config $CFG --steps 1 --warmup 1 --no-cpu-baseline --graph off --no-timer
 python3 tools/rocprof_families.py --trace $O/trace --fetch $O/fetch --write $O/write --mfma $O/mfma \
-  --steps 0 --config $CFG --out $O/families.json > /dev/null
+  --bench-line gpurun_out/prof_trace.log --config $CFG --out $O/families.json > /dev/null
 python3 tools/dispatch_groups.py $O/trace --steps 0 --filter conv --top 60 > $O/conv_groups.txt
 python3 tools/dispatch_groups.py $O/trace --steps 0 --top 60 > $O/all_groups.txt
 for d in trace fetch write mfma; do find $O/$d -name '*.csv' -size +20M -delete; done

@@ -1,7 +1,8 @@
 #!/usr/bin/env python
 """Summarise rocprofv3 output of a bench.py run per kernel family.
 
-    python tools/rocprof_families.py --trace DIR [--fetch DIR] [--write DIR] [--steps K] [--out FILE]
+    python tools/rocprof_families.py --trace DIR [--fetch DIR] [--write DIR] [--mfma DIR]
+                                     [--bench-line LOG] [--steps K] [--out FILE]
 
 --trace: directory of a `rocprofv3 --kernel-trace --stats` run; the kernel
 trace gives, for each family, the dispatch count and the average duration of
@@ -24,6 +25,16 @@ shorter than ~0.3 ms it reads well above duration x clock (MI355X_MICROARCH.md,
 DVFS give-back), so it is not used as the denominator.
 The summary records the git commit and the sha256 of libeegan_hip.so it was
 taken with, so bench.py can flag a summary taken with other kernels.
+
+Windows: bench.py launches a marker kernel (stamp_kernel) at both ends of its
+timed region (the graph replays) and of its eager timing pass; the families
+are summed over the timed replays only (in-step durations, lanes running
+concurrently), `timing_pass` over the timing pass (single stream, what the
+line's HIP events time).  --bench-line adds each conv family's algorithmic
+FLOPs / bytes per call from the same run's line, and from them `frac_in_step`
+(algorithmic FLOPs per step / in-step kernel time / 2.5 PFLOP/s),
+`pmc_over_algorithmic` and the conv path's algorithmic and PMC HBM fractions
+-- the figures bench.py then quotes, recomputable from this file alone.
 Output JSON: {family: {calls, avg_call_us, total_ms, hbm_bytes_per_call,
 mfma_util}} plus totals (GPU busy time per step), read by bench.py for
 `traffic` and `mfma_busy`.
@@ -36,29 +47,29 @@ import os
 import re
 from collections import defaultdict
 
-# (family, is_primary): the primary kernel counts calls; secondaries add time
+# ONE kernel -> family table for every conv kernel in csrc/conv.hip, the same op
+# families bench.py's event timer uses (functional.conv_fwd_raw / conv_bwd_data_raw /
+# conv_bwd_weight_raw time every dispatch of one call: the GEMM kernel -- whichever
+# specialised form the planner picked -- and, with split-K, its reduce).  (regex,
+# family, is_primary): a primary kernel counts a call; secondaries add time and
+# bytes to the call.  Ordered: the first match wins (conv_s2bwd_lds_kernel<NT, NC>
+# and conv_wgrad_*<...> carry no mode argument, so they precede the mode rules).
+# An unclassified kernel whose name starts with conv_ is an error (check_complete).
 _FAMILIES = [
-    (re.compile(r'conv_fast_kernel<0,'), 'conv_fwd', True),
-    (re.compile(r'conv_fast_kernel<1,'), 'conv_bwd_data', True),
-    (re.compile(r'conv_wgrad_fast_kernel<'), 'conv_bwd_weight', True),
-    (re.compile(r'conv_glds_kernel<0,'), 'conv_fwd', True),
-    (re.compile(r'conv_glds_kernel<1,'), 'conv_bwd_data', True),
-    (re.compile(r'conv_wgrad_glds_kernel<'), 'conv_bwd_weight', True),
-    (re.compile(r'conv_igemm_kernel<0,'), 'conv_fwd', True),
     (re.compile(r'conv_splitk_reduce_kernel<0>'), 'conv_fwd', False),
-    (re.compile(r'conv_igemm_kernel<1,'), 'conv_bwd_data', True),
     (re.compile(r'conv_splitk_reduce_kernel<1>'), 'conv_bwd_data', False),
-    (re.compile(r'conv_wgrad_kernel<'), 'conv_bwd_weight', True),
-    (re.compile(r'conv_thin(_lds)?_kernel<0,'), 'conv_fwd', True),
-    (re.compile(r'conv_thin(_lds)?_kernel<1,'), 'conv_bwd_data', True),
-    (re.compile(r'conv_wgrad_thin_kernel<'), 'conv_bwd_weight', True),
-    (re.compile(r'conv_1x1_kernel<0,'), 'conv_fwd', True),
-    (re.compile(r'conv_1x1_kernel<1,'), 'conv_bwd_data', True),
+    (re.compile(r'conv_s2fwd_kernel'), 'conv_fwd', True),
     (re.compile(r'conv_s2bwd_lds_kernel<'), 'conv_bwd_data', True),
-    (re.compile(r'conv_halo3_kernel<0,'), 'conv_fwd', True),
-    (re.compile(r'conv_halo3_kernel<1,'), 'conv_bwd_data', True),
+    (re.compile(r'conv_wgrad_\w*kernel<'), 'conv_bwd_weight', True),
+    (re.compile(r'wgrad_quad_reduce_kernel<'), 'conv_bwd_weight', False),
     (re.compile(r'colsum_rows_kernel<.*WgradMap'), 'conv_bwd_weight', False),
+    (re.compile(r'conv_(fast|glds|igemm|thin|thin_lds|1x1|halo3|halo3r)_kernel<0[,>]'), 'conv_fwd', True),
+    (re.compile(r'conv_(fast|glds|igemm|thin|thin_lds|1x1|halo3|halo3r)_kernel<1[,>]'), 'conv_bwd_data', True),
 ]
+CONV_FAMILIES = ('conv_fwd', 'conv_bwd_data', 'conv_bwd_weight')
+MARKER = 'stamp_kernel'   # bench.py's window markers (eegan_stamp): timed region, then the timing pass
+MFMA_PEAK = 2.5e15        # dense bf16 FLOP/s (MI355X_MICROARCH.md)
+HBM_PEAK = 8.0e12         # B/s
 
 
 CLOCK_HZ = 2.4e9   # MI355X max clock (MI355X_MICROARCH.md): a lower bound on the busy fraction under DVFS
@@ -86,12 +97,23 @@ def _provenance():
     return {'lib_sha256_16': sha, 'git_head': head}
 
 
+def _short(name):
+    return name.replace('(anonymous namespace)::', '').replace('void ', '').strip()
+
+
 def family(name):
     for rx, fam, prim in _FAMILIES:
         if rx.search(name):
             return fam, prim
-    base = name.replace('(anonymous namespace)::', '').replace('void ', '')
-    return re.sub(r'[<(].*', '', base).strip(), True
+    return re.sub(r'[<(].*', '', _short(name)).strip(), True
+
+
+def check_complete(names):
+    """Every conv kernel of the run must be in the table (else the families
+    silently lose time and the bench's op families and these disagree)."""
+    bad = sorted({_short(n)[:80] for n in names if _short(n).startswith('conv_') and family(n)[0] not in CONV_FAMILIES})
+    if bad:
+        raise SystemExit('rocprof_families: conv kernels missing from the family table: %s' % bad)
 
 
 def _find(d, suffix):
@@ -101,16 +123,33 @@ def _find(d, suffix):
     return hits
 
 
-def kernel_trace(d):
-    fams = defaultdict(lambda: {'calls': 0, 'dispatches': 0, 'ns': 0})
+def _rows(d):
+    rows = []
     for path in _find(d, 'kernel_trace.csv'):
         with open(path) as f:
-            for row in csv.DictReader(f):
-                fam, prim = family(row['Kernel_Name'])
-                o = fams[fam]
-                o['dispatches'] += 1
-                o['calls'] += int(prim)
-                o['ns'] += int(row['End_Timestamp']) - int(row['Start_Timestamp'])
+            rows += [(r['Kernel_Name'], int(r['Start_Timestamp']), int(r['End_Timestamp'])) for r in csv.DictReader(f)]
+    return sorted(rows, key=lambda r: r[1])
+
+
+def windows(rows):
+    """Consecutive pairs of marker dispatches -> [(lo, hi), ...] in time order:
+    bench.py stamps the timed region (graph replays) and then its eager
+    timing pass; a kernel is inside a window when it starts after the opening
+    marker ends and ends before the closing marker starts."""
+    m = [(s, e) for n, s, e in rows if MARKER in n]
+    return [(m[i][1], m[i + 1][0]) for i in range(0, len(m) - 1, 2)]
+
+
+def kernel_trace(rows, window=None):
+    fams = defaultdict(lambda: {'calls': 0, 'dispatches': 0, 'ns': 0})
+    for name, t0, t1 in rows:
+        if MARKER in name or (window and not (t0 >= window[0] and t1 <= window[1])):
+            continue
+        fam, prim = family(name)
+        o = fams[fam]
+        o['dispatches'] += 1
+        o['calls'] += int(prim)
+        o['ns'] += t1 - t0
     return fams
 
 
@@ -128,6 +167,15 @@ def pmc(d, counter):
     return tot, calls
 
 
+def _bench_line(path):
+    """The JSON line bench.py printed in the traced run (its log file)."""
+    with open(path) as f:
+        for line in f:
+            if line.startswith('{') and '"metric"' in line:
+                return json.loads(line)
+    raise SystemExit('rocprof_families: no bench line in %s' % path)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--trace', required=True)
@@ -135,14 +183,26 @@ def main():
     ap.add_argument('--write')
     ap.add_argument('--mfma')
     ap.add_argument('--steps', type=int, default=0, help='steps in the traced run (warmup+timed) for per-step totals')
+    ap.add_argument('--bench-line', help='log of the traced bench.py run: its line gives the algorithmic FLOPs / bytes '
+                                         'per call of each conv family and the number of timed steps')
     ap.add_argument('--out')
     ap.add_argument('--config', default='C2', help='bench.py workload the runs were taken on')
     a = ap.parse_args()
-    fams = kernel_trace(a.trace)
+    rows = _rows(a.trace)
+    check_complete(n for n, _, _ in rows)
+    wins = windows(rows)
+    line = _bench_line(a.bench_line) if a.bench_line else None
+    fams = kernel_trace(rows, wins[0] if wins else None)
     fetch = pmc(a.fetch, 'FETCH_SIZE') if a.fetch else None
     write = pmc(a.write, 'WRITE_SIZE') if a.write else None
     busy = pmc(a.mfma, 'SQ_VALU_MFMA_BUSY_CYCLES') if a.mfma else None
     gui = pmc(a.mfma, 'GRBM_GUI_ACTIVE') if a.mfma else None
+    if wins and line:
+        a.steps = line['steps']          # the window holds exactly the K timed replays
+    elif a.steps <= 0:   # counted: one adam_tick_kernel per optimizer step, 7 per C2 train step
+        ticks = fams.get('adam_tick_kernel', {}).get('calls', 0)
+        a.steps = round(ticks / 7) if ticks else 0
+    alg = (line or {}).get('roofline', {}).get('families', {})
     out = {}
     for fam, o in sorted(fams.items(), key=lambda kv: -kv[1]['ns']):
         calls = max(o['calls'], 1)
@@ -164,18 +224,44 @@ def main():
                                    '1024 SIMDs)')
             if gui and gui[0].get(fam):
                 e['gpu_active_cycles_per_call'] = round(gui[0][fam] / 8 / n)
+        if a.steps:
+            e['ms_per_step'] = round(e['total_ms'] / a.steps, 4)
+            e['calls_per_step'] = round(o['calls'] / a.steps, 2)
+        q = alg.get(fam)
+        if q and q.get('algorithmic_flops_per_launch') and a.steps:
+            # the bench's own per-call algorithmic figures (same op families, same config)
+            e['algorithmic_flops_per_call'] = q['algorithmic_flops_per_launch']
+            e['algorithmic_bytes_per_call'] = q['algorithmic_bytes_per_launch']
+            e['bench_launches_per_step'] = q['launches_per_step']
+            sec = e['total_ms'] * 1e-3 / a.steps
+            e['frac_in_step'] = round(e['algorithmic_flops_per_call'] * e['calls_per_step'] / sec / MFMA_PEAK, 4)
+            e['algorithmic_hbm_frac_in_step'] = round(
+                e['algorithmic_bytes_per_call'] * e['calls_per_step'] / sec / HBM_PEAK, 4)
+            if e.get('hbm_bytes_per_call'):
+                e['pmc_over_algorithmic'] = round(e['hbm_bytes_per_call'] / e['algorithmic_bytes_per_call'], 3)
         out[fam] = e
     total_ns = sum(o['ns'] for o in fams.values())
-    res = {'families': out, 'gpu_busy_ms_total': round(total_ns * 1e-6, 3), 'config': a.config}
+    res = {'families': out, 'gpu_busy_ms_total': round(total_ns * 1e-6, 3), 'config': a.config,
+           'window': 'the timed graph replays between bench.py\'s markers' if wins else 'the whole trace'}
     res.update(_provenance())
-    if a.steps <= 0:   # counted: one adam_tick_kernel per optimizer step, 7 per C2 train step
-        ticks = fams.get('adam_tick_kernel', {}).get('calls', 0)
-        a.steps = round(ticks / 7) if ticks else 0
     if a.steps:
         res['steps'] = a.steps
         res['gpu_busy_ms_per_step'] = round(total_ns * 1e-6 / a.steps, 3)
-        for e in out.values():
-            e['ms_per_step'] = round(e['total_ms'] / a.steps, 3)
+        cp = [out.get(f, {}) for f in CONV_FAMILIES]
+        if all('algorithmic_bytes_per_call' in f for f in cp):
+            ab = sum(f['algorithmic_bytes_per_call'] * f['calls_per_step'] for f in cp)
+            ms = sum(f['ms_per_step'] for f in cp)
+            res['conv_path'] = {'algorithmic_bytes_per_step': round(ab), 'kernel_ms_per_step': round(ms, 4),
+                                'algorithmic_hbm_frac': round(ab / (ms * 1e-3) / HBM_PEAK, 4)}
+            if all('hbm_bytes_per_call' in f for f in cp):
+                pb = sum(f['hbm_bytes_per_call'] * f['calls_per_step'] for f in cp)
+                res['conv_path']['pmc_bytes_per_step'] = round(pb)
+                res['conv_path']['pmc_hbm_frac'] = round(pb / (ms * 1e-3) / HBM_PEAK, 4)
+    if len(wins) > 1:   # bench.py's eager, single-stream timing pass: what its HIP events time
+        tp = kernel_trace(rows, wins[1])
+        res['timing_pass'] = {f: {'calls': tp[f]['calls'], 'total_ms': round(tp[f]['ns'] * 1e-6, 3),
+                                  'avg_call_us': round(tp[f]['ns'] / max(tp[f]['calls'], 1) * 1e-3, 2)}
+                              for f in CONV_FAMILIES if f in tp}
     txt = json.dumps(res, indent=1)
     if a.out:
         with open(a.out, 'w') as f:
