@@ -163,11 +163,13 @@ def cpu_baseline(seconds_budget=30.0):
     from oracle.seeding import seeded_state, synthetic_batch
     import models
     import DAMSM
-    affinity = len(os.sched_getaffinity(0))
     # the host cores this process may use: the affinity set, capped by the
     # scheduler's share when the environment states one (OMP_NUM_THREADS: the
-    # GPU box's affinity mask spans the whole machine, its CPU share is 16)
-    share = int(os.environ.get('EEGAN_CPU_SHARE') or os.environ.get('OMP_NUM_THREADS') or 0)
+    # GPU box's affinity mask spans the whole machine, its CPU share is 16).
+    # Measured by the parent (cpu_baseline_child): here OpenMP's bound initial
+    # thread already narrowed this process's own mask to one core
+    affinity = int(os.environ.get('EEGAN_CPU_AFFINITY') or len(os.sched_getaffinity(0)))
+    share = int(os.environ.get('EEGAN_CPU_SHARE') or 0)
     torch.set_num_threads(min(affinity, share) if share > 0 else affinity)
     B, W, ncls = 4, 32, 200
     spec = lambda m: [(k, tuple(v.shape)) for k, v in m.state_dict().items()]  # noqa: E731
@@ -287,10 +289,11 @@ def cpu_baseline_child(seconds):
     only act before OpenMP starts, which in this process happened long ago),
     started after the GPU measurement; returns its JSON object."""
     import subprocess
-    env = dict(os.environ, OMP_PROC_BIND='close', OMP_PLACES='cores')
+    affinity = len(os.sched_getaffinity(0))
     share = int(os.environ.get('OMP_NUM_THREADS') or 0)
-    if share > 0:
-        env['EEGAN_CPU_SHARE'] = str(share)
+    threads = min(affinity, share) if share > 0 else affinity
+    env = dict(os.environ, OMP_PROC_BIND='close', OMP_PLACES='cores', OMP_NUM_THREADS=str(threads),
+               EEGAN_CPU_AFFINITY=str(affinity), EEGAN_CPU_SHARE=str(share))
     r = subprocess.run([sys.executable, os.path.abspath(__file__), '--cpu-baseline-only',
                         '--cpu-seconds', str(seconds)], env=env, stdout=subprocess.PIPE, text=True, timeout=900)
     lines = [l for l in r.stdout.splitlines() if l.startswith('{')]
