@@ -88,6 +88,7 @@ struct ConvArgs {
   int wide;     // conv_fast_kernel pairs: one 64-channel stage of whole 128-B lines per K-step pair
   int stage_epi;  // conv_fast_kernel: LDS-staged epilogue (unsplit bf16 output, 16-B aligned rows; host-checked)
   int* ctr;       // conv_fast_kernel split-K: per-tile arrival counters (zero on entry and exit) -> in-kernel finish
+  int tp;         // planner objective (eegan_conv_desc.plan): 1 = throughput (host only)
 };
 
 // K step kt, 8-channel chunk kc -> kernel tap and channel.  Normal mode: the
@@ -3347,7 +3348,10 @@ static int knob(const char* key, int dflt) {
 Plan plan_igemm(const ConvArgs& a, int Pc_max) {
   // tuning knobs (benchmark sweeps only): grid target, min K-steps per split,
   // and whether 64-row tiles are tried before splitting K
-  const int target = knob("target", 512);
+  // throughput objective (eegan_conv_desc.plan = 1, a stream beside the critical chain):
+  // a smaller grid target -- larger tiles, and no split-K partials / reduce launch once
+  // the grid reaches it
+  const int target = a.tp ? knob("tp_target", 128) : knob("target", 512);
   const int mink = knob("mink", 16);
   const int small_co = knob("smallco", 1);
   const int rows = a.Mrows;
@@ -3673,6 +3677,7 @@ void fill_fwd(ConvArgs& a, const eegan_conv_desc* d) {
   a.ncls = 1;
   a.nsplit = 1;
   a.res_scale = 1.f;
+  a.tp = d->plan == 1;
 }
 
 void fill_bwdd(ConvArgs& a, const eegan_conv_desc* d) {
@@ -3697,6 +3702,7 @@ void fill_bwdd(ConvArgs& a, const eegan_conv_desc* d) {
   a.ncls = d->stride > 1 ? d->stride * d->stride : 1;
   a.nsplit = 1;
   a.res_scale = 1.f;
+  a.tp = d->plan == 1;
 }
 
 int bwdd_pc_max(const eegan_conv_desc* d) {
@@ -3869,7 +3875,8 @@ static void wgrad_plan(const eegan_conv_desc* d, int& TCO, int& TK, int& nsplit,
   if (const int ht = wgrad_halo_tiles(d)) {
     // ~`wgrad_halo_blocks` blocks over the output-channel tiles, a multiple of 8 per tile (XCD-contiguous walks)
     const int co_t = d->K / 32;
-    const int want = std::max(8, knob("wgrad_halo_blocks", 512) / co_t);
+    const int want = std::max(8, (d->plan == 1 ? knob("tp_wgrad_halo_blocks", 256) : knob("wgrad_halo_blocks", 512)) /
+                                     co_t);
     pps = ee_cdiv(ht, std::min(want, ht));   // tiles per block
     nsplit = ee_round_up(ee_cdiv(ht, pps), 8);
     TCO = 32;
@@ -3890,7 +3897,8 @@ static void wgrad_plan(const eegan_conv_desc* d, int& TCO, int& TK, int& nsplit,
   // ~2 blocks per CU, >= 16 K-steps (512 pixels) per split: the fp32 slab
   // (nsplit x Cout x K) is written once and read once by the column reduce
   // knobs for sweeps: grid target (blocks) and minimum pixels per split
-  int want = std::max(1, knob("wgrad_target", 512) / std::max(tiles, 1));
+  int want = std::max(1, (d->plan == 1 ? knob("tp_wgrad_target", 256) : knob("wgrad_target", 512)) /
+                            std::max(tiles, 1));
   const int maxsplit = std::max(1, ee_cdiv(P, knob("wgrad_minp", 512)));
   nsplit = std::min(want, maxsplit);
   pps = ee_round_up(ee_cdiv(P, nsplit), BK);

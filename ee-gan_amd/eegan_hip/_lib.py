@@ -17,7 +17,8 @@ ACT_CODES = {None: 0, 'none': 0, 'relu': 1, 'lrelu': 2, 'tanh': 3, 'sigmoid': 4}
 class ConvDesc(C.Structure):
     _fields_ = [(n, C.c_int) for n in ['N', 'H', 'W', 'C', 'ldx', 'K', 'R', 'S', 'stride', 'pad_h', 'pad_w',
                                        'up2', 'Ho', 'Wo', 'ldy']] + [('splitk_ctr', C.c_void_p),
-                                                                     ('splitk_ctr_n', C.c_int)]
+                                                                     ('splitk_ctr_n', C.c_int),
+                                                                     ('plan', C.c_int)]
 
 
 class BnModDesc(C.Structure):
@@ -167,7 +168,7 @@ def _load():
 
 LIB = _load()
 ABI_VERSION = LIB.eegan_abi_version()
-EXPECTED_ABI = 14
+EXPECTED_ABI = 15
 if ABI_VERSION != EXPECTED_ABI:
     raise ImportError('%s has ABI %d, these bindings need %d: rebuild (make -C ee-gan_amd/csrc)'
                       % (LIB_PATH, ABI_VERSION, EXPECTED_ABI))

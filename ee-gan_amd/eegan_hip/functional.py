@@ -221,12 +221,21 @@ def _splitk_ctr(device):
     return t
 
 
+# Planner objective per stream (eegan_conv_desc.plan): cuda_stream handle -> 1 for
+# the step's lanes that run beside the critical chain (trainer.TP_LANES), whose
+# convs are planned for throughput (larger tiles, no split-K) instead of latency.
+# Read when a conv is issued -- inside a graph capture, when the graph is built.
+STREAM_PLAN = {}
+
+
 def _desc_io(g, x_shape, ldx, ldy, device=None):
     N, C, H, W = x_shape
     Hl, Wl = (H * 2, W * 2) if g.up2 else (H, W)
     Ho = (Hl + 2 * g.ph - g.R) // g.stride + 1
     Wo = (Wl + 2 * g.pw - g.S) // g.stride + 1
     d = ConvDesc(N, Hl, Wl, C, ldx, g.K, g.R, g.S, g.stride, g.ph, g.pw, g.up2, Ho, Wo, ldy)
+    if STREAM_PLAN:
+        d.plan = STREAM_PLAN.get(torch.cuda.current_stream().cuda_stream, 0)
     if device is not None and device.type == 'cuda':
         ctr = _splitk_ctr(device)
         if ctr is not None:

@@ -66,6 +66,13 @@ GEN_SIDE = True
 # backward kernels do not queue behind the reductions; each optimizer's step
 # waits for its lane (FlatAdam.comm_stream).  Module constant for A/B.
 COMM_LANES = True
+# Lanes whose convs are planned for throughput (eegan_conv_desc.plan = 1: larger
+# tiles, no split-K partials or reduce launches) -- lanes that run beside the
+# critical chain, where a conv's latency matters less than the CU time it takes
+# from the critical lane.  Indices of _side_streams: 0..nD-1 the discriminators'
+# lanes (0 also carries the generator's stage 2-3 branch), nD the DAMSM lane.
+# EEGAN_TP_LANES: comma-separated indices ('' = none).
+TP_LANES = tuple(int(v) for v in os.environ.get('EEGAN_TP_LANES', '').split(',') if v.strip())
 # Measured alternatives kept as module constants (A/B: tools/ab_inproc.py
 # "py:eegan_hip.trainer.NAME=value"; DESIGN.md §3, round 5, all behind the default):
 # DREAL_EARLY -- discriminators whose real-image share of d_loss (the real and
@@ -147,6 +154,11 @@ class Trainer(object):
             self._streams = [new_stream(self.device, 1 if i == hi else lo) for i in range(n)]
             for i, st in enumerate(self._streams):
                 D.bind_stream(st, i)   # one RCCL communicator per stream lane
+        for i, st in enumerate(self._streams):   # planner objective per lane (TP_LANES)
+            if i in TP_LANES:
+                Fn.STREAM_PLAN[st.cuda_stream] = 1
+            else:
+                Fn.STREAM_PLAN.pop(st.cuda_stream, None)
         if fork:
             main = torch.cuda.current_stream()
             for s in self._streams[:n]:

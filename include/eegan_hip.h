@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 14  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
+#define EEGAN_ABI_VERSION 15  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
                                 4: rectangular (local x global) DAMSM words / sentence blocks on MFMA;
                                 5: GlobalAttentionGeneral (eegan_gag_*), words backward reuses the forward's prep;
                                 6: device input pipeline (eegan_pipe_*);
@@ -38,7 +38,8 @@ extern "C" {
                                 11: BN forward with the finalize folded in (eegan_bnmod_fwd_fin);
                                 12: ScaleAdd double backward in one pass (eegan_scale_dot_res);
                                 13: split-K counters in the conv descriptor, for the in-kernel split-K finish;
-                                14: per-region peer wait bound (eegan_peer_set_wait) */
+                                14: per-region peer wait bound (eegan_peer_set_wait);
+                                15: planner objective in the conv descriptor (eegan_conv_desc.plan) */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
@@ -78,6 +79,14 @@ typedef struct eegan_conv_desc {
    * arrays (one per stream).  NULL: split-K launches reduce in a second kernel. */
   int* splitk_ctr;
   int splitk_ctr_n;
+  /* optional (ABI 15): the planner's objective for this call.  0: latency -- split K until the grid
+   * covers the chip twice (512 workgroups), smaller pixel tiles for small grids (a conv on the step's
+   * critical chain); 1: throughput -- a grid target of 128 workgroups (128 / 256 for weight
+   * gradients), so larger tiles and no split-K partials or reduce launch wherever the grid already
+   * reaches it (a conv on a stream that runs beside others and is not on the critical chain: fewer
+   * CU-cycles and HBM bytes per FLOP).  Same arithmetic either way except the split-K summation
+   * order.  The workspace queries honour it: query and launch with the same descriptor. */
+  int plan;
 } eegan_conv_desc;
 
 /* elements of the packed bf16 weight image (rows padded to 128, each tap's channel run to 32) */
