@@ -89,6 +89,12 @@ struct ConvArgs {
   int stage_epi;  // conv_fast_kernel: LDS-staged epilogue (unsplit bf16 output, 16-B aligned rows; host-checked)
   int* ctr;       // conv_fast_kernel split-K: per-tile arrival counters (zero on entry and exit) -> in-kernel finish
   int tp;         // planner objective (eegan_conv_desc.plan): 1 = throughput (host only)
+  // conv_fast_kernel XCD raster (xcd_g > 0): a 1-D grid of round_up(gx * gy * gz, 8) blocks; the
+  // blocks one XCD runs (id % 8 equal) take a contiguous range of the logical tile order, which
+  // walks groups of xcd_g co-tile rows (pixel tiles inside a group), z outermost -- so an XCD's
+  // blocks share a few weight-row tiles and a run of pixel tiles in its own L2 instead of every
+  // XCD reading every weight tile (round-robin dispatch of the x-fastest 3-D grid)
+  int xcd_g, gx, gy, gz;
 };
 
 // K step kt, 8-channel chunk kc -> kernel tap and channel.  Normal mode: the
@@ -932,8 +938,20 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wi = wave / WPIX, wj = wave % WPIX;
-  const int cls = blockIdx.z % a.ncls, split = blockIdx.z / a.ncls;
-  const int co0 = blockIdx.y * TCO;
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (a.xcd_g) {   // XCD raster (ConvArgs::xcd_g): block-uniform remap, exits before any barrier
+    const int nb = a.gx * a.gy * a.gz, nbp = (nb + 7) & ~7, id = blockIdx.x;
+    const int L = (id & 7) * (nbp >> 3) + (id >> 3);
+    if (L >= nb) return;
+    const int nbz = a.gx * a.gy;
+    bz = L / nbz;
+    const int r = L - bz * nbz, gsz = a.xcd_g * a.gx, grp = r / gsz, first = grp * a.xcd_g;
+    const int gh = min(a.gy - first, a.xcd_g), rr = r - grp * gsz;
+    by = first + rr % gh;
+    bx = rr / gh;
+  }
+  const int cls = bz % a.ncls, split = bz / a.ncls;
+  const int co0 = by * TCO;
   const bool a_wave = A_TOT >= 256 || tid < A_TOT;
 
   int qy = 0, qx = 0, CH = a.OH, CW = a.OW, stc = 1;
@@ -954,7 +972,7 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
     dqx = (qx + a.pw - s0) / a.st;
   }
   const int Pc = a.N * CH * CW;
-  const int pix0 = blockIdx.x * TPIX;
+  const int pix0 = bx * TPIX;
   if (pix0 >= Pc) return;  // block-uniform
   const int nc = a.Cgp / BK;
   const int nk_all = TR * TS * nc;
@@ -1233,7 +1251,8 @@ __global__ __launch_bounds__(256, 2) void conv_fast_kernel(ConvArgs a, long src_
     return;
   }
   if (a.ctr) {   // split-K finished here (block-uniform)
-    const int tile = (cls * (int)gridDim.y + (int)blockIdx.y) * (int)gridDim.x + (int)blockIdx.x;
+    const int tile = a.xcd_g ? (cls * a.gy + by) * a.gx + bx
+                             : (cls * (int)gridDim.y + (int)blockIdx.y) * (int)gridDim.x + (int)blockIdx.x;
     splitk_fused_finish<MODE, TCO, TPIX, FI, FJ, WT_CO, WT_PIX>(a, acc, pix0, co0, wi, wj, lane, tid, split, tile, Pc,
                                                                 CH, CW, qy, qx, stc);
     return;
@@ -3613,8 +3632,26 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   if (p.nsplit > 1 && a.red_vec4 && ctr && (long)grid.x * grid.y * a.ncls <= ctr_n &&
       (long)p.nsplit * total * 4 < 0x7fffffffL && knob("splitk_fused", 0))
     a.ctr = ctr;   // conv_fast_kernel finishes the split itself (below: only when `fast`)
+  dim3 fgrid = grid;   // conv_fast_kernel's grid: the XCD raster when it applies
+  {
+    const long nb = (long)grid.x * grid.y * grid.z;
+    const int xcd = knob("xcd", 1);
+    if (xcd && nb >= knob("xcd_minb", 64) && nb < (1L << 30)) {
+      // rows per group G ~ sqrt(S * B / A), S = blocks per XCD; per tile the weight rows carry
+      // TCO * taps * C and the pixel tile ~ TPIX * st^2 * C unique bytes (taps re-read pixels)
+      const int S_ = (int)(((nb + 7) & ~7L) / 8);
+      const double ab = (double)p.tco * a.R * a.S / ((double)p.tpix * a.st * a.st);
+      int G = xcd > 1 ? xcd : (int)(sqrt((double)S_ / ab) + 0.5);
+      G = std::max(1, std::min(G, (int)grid.y));
+      a.xcd_g = G;
+      a.gx = grid.x;
+      a.gy = grid.y;
+      a.gz = grid.z;
+      fgrid = dim3((unsigned)((nb + 7) & ~7L), 1, 1);
+    }
+  }
 #define GL(TC, TP) ee_launch(conv_glds_kernel<MODE, TC, TP>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
-#define FA(TC, TP) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 4, 2>, grid, dim3(256), 0, s, a, src_bytes, w_bytes)
+#define FA(TC, TP) ee_launch(conv_fast_kernel<MODE, TC, TP, 2, 4, 2>, fgrid, dim3(256), 0, s, a, src_bytes, w_bytes)
 #define IG(TC, TP, WC) ee_launch(conv_igemm_kernel<MODE, TC, TP, WC>, grid, dim3(256), 0, s, a)
   // glds: channel chunks fetched whole (C % 8 != 0 masked in the fragments; the
   // fast kernel needs whole valid chunks)

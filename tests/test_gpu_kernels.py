@@ -1147,3 +1147,85 @@ def test_conv_s2fwd_matches_tile_kernel(gpu, monkeypatch):
             assert torch.equal(a, c), (N, H, W, float((a - c).abs().max()))
         ref = F.conv2d(xs.to(torch.bfloat16).float(), Wt.cpu().to(torch.bfloat16).float(), None, 2, 1)
         assert rel_l2(outs['1'][1], ref) <= 1e-2
+
+
+@pytest.mark.parametrize('xcd', ['1', '3'])
+@pytest.mark.parametrize('target', ['512', '4096'])
+def test_conv_xcd_raster_bit_identical(gpu, monkeypatch, xcd, target):
+    """The tile kernel's XCD raster (EEGAN_CONV xcd=1 default: G from the
+    tile shape; xcd=3: three co-tile rows per group) against the plain 3-D
+    grid (xcd=0): the same tiles and K order, only the block -> tile map
+    differs, so torch.equal -- including grids that are not a multiple of 8
+    (blocks past the grid exit), co-tile counts not divisible by the group
+    height, split-K (target 4096) and the stride-2 parity classes."""
+    Fn, T, _ = _mods()
+    conv_knob(monkeypatch, 'target', target)
+    conv_knob(monkeypatch, 'mink', '2')
+    conv_knob(monkeypatch, 'xcd_minb', '1')
+    lrelu = Fn.ACT_CODES['lrelu']
+    for N, Cin, H, W, Cout, k, st, pad in [(2, 64, 16, 16, 128, 3, 1, 1), (3, 128, 9, 11, 320, 3, 1, 1),
+                                            (2, 96, 16, 16, 256, 4, 2, 1), (16, 768, 17, 17, 192, 1, 1, 0),
+                                            (4, 256, 8, 8, 512, 3, 1, 1), (5, 128, 7, 7, 200, 1, 1, 0)]:
+        torch.manual_seed(N * Cin + Cout + H)
+        g = Fn.Geom(Cout, k, k, st, pad, pad, 0)
+        x = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        Wt = (torch.randn(Cout, Cin, k, k) * 0.05).to(gpu)
+        b = torch.randn(Cout).to(gpu)
+        gam = torch.tensor([0.7]).to(gpu)
+        Ho, Wo = g.out_hw(H, W)
+        res = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
+        dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
+        gate = _nhwc(torch.randn(N, Cin, H, W), gpu)
+        outs = []
+        for v in ('0', xcd):
+            conv_knob(monkeypatch, 'xcd', v)
+            outs.append([Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, res=res, gamma=gam).float().cpu(),
+                         Fn.conv_fwd_raw(x, Wt, b, g, act=lrelu, out_f32=True).cpu(),
+                         Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape), gate=gate, gate_act=lrelu).float().cpu()])
+        for a, c in zip(*outs):
+            assert torch.equal(a, c), (N, Cin, H, W, Cout, k, st, xcd, target)
+
+
+def test_conv_throughput_plan(gpu, monkeypatch):
+    """eegan_conv_desc.plan = 1 (a stream registered in Fn.STREAM_PLAN, as the
+    trainer's TP_LANES are): the planner takes a 128-workgroup grid target --
+    on these small grids fewer K splits than the latency plan -- and the
+    forward, data and weight gradients still match torch fp32 (only the
+    split-K summation order differs from the latency plan)."""
+    Fn, T, _ = _mods()
+    lane = torch.cuda.Stream()
+    for N, Cin, H, W, Cout, k, st, pad in [(16, 768, 17, 17, 192, 1, 1, 0), (16, 160, 17, 17, 160, 7, 1, 3),
+                                            (4, 512, 8, 8, 512, 4, 2, 1), (16, 1280, 8, 8, 320, 1, 1, 0)]:
+        torch.manual_seed(N + Cin + Cout)
+        kh, kw = (1, k) if k == 7 else (k, k)
+        ph, pw = (0, pad) if k == 7 else (pad, pad)
+        g = Fn.Geom(Cout, kh, kw, st, ph, pw, 0)
+        xf = _bf(torch.randn(N, Cin, H, W))
+        Wf = _bf(torch.randn(Cout, Cin, kh, kw) * (2.0 / (Cin * kh * kw)) ** 0.5)
+        ref = F.conv2d(xf, Wf, stride=st, padding=(ph, pw))
+        dzf = _bf(torch.randn_like(ref))
+        xr = xf.clone().requires_grad_(True)
+        Wr = Wf.clone().requires_grad_(True)
+        F.conv2d(xr, Wr, stride=st, padding=(ph, pw)).backward(dzf)
+        x = _nhwc(xf, gpu)
+        Wt = Wf.to(gpu).contiguous(memory_format=torch.channels_last)
+        dz = _nhwc(dzf, gpu)
+        res = {}
+        for plan in (0, 1):
+            lane.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(lane):
+                if plan:
+                    Fn.STREAM_PLAN[lane.cuda_stream] = 1
+                try:
+                    y = Fn.conv_fwd_raw(x, Wt, None, g).float().cpu()
+                    dx = Fn.conv_bwd_data_raw(dz, Wt, g, tuple(x.shape)).float().cpu()
+                    dW = Fn.conv_bwd_weight_raw(x, dz, g, tuple(Wf.shape)).float().cpu()
+                finally:
+                    Fn.STREAM_PLAN.pop(lane.cuda_stream, None)
+            torch.cuda.current_stream().wait_stream(lane)
+            torch.cuda.synchronize()
+            res[plan] = (y, dx, dW)
+            for got, want, name in ((y, ref, 'y'), (dx, xr.grad, 'dx'), (dW, Wr.grad, 'dW')):
+                e = rel_l2(got, want)
+                assert e < 1e-2, (plan, name, N, Cin, Cout, k, e)
+        print('throughput plan: fwd max |plan1 - plan0| %.3g' % float((res[1][0] - res[0][0]).abs().max()))
