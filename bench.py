@@ -313,6 +313,8 @@ def main():
     ap.add_argument('--cpu-baseline-only', action='store_true', help=argparse.SUPPRESS)
     ap.add_argument('--no-timer', action='store_true', help='diagnostic: skip the roofline timing pass')
     ap.add_argument('--timing-steps', type=int, default=2, help='eager steps of the roofline timing pass')
+    ap.add_argument('--op-log', help='diagnostic: write the timing pass\'s conv / GEMM ops (issue order, shape, '
+                                     'algorithmic FLOPs / bytes) as JSON, for tools/rocprof_families.py --ops')
     ap.add_argument('--graph', default='auto', choices=['auto', 'on', 'off'],
                     help='replay the step as one captured HIP graph (auto: on; N > 1 needs the own RCCL communicators)')
     args = ap.parse_args()
@@ -417,6 +419,9 @@ def main():
         mark(3)
         T.use_streams = streams
         Fn.TIMER = None
+        if args.op_log and rank == 0:   # the timing pass's ops in issue order (per-op PMC table)
+            with open(args.op_log, 'w') as f:
+                json.dump({'config': args.config, 'timing_steps': per, 'ops': timer.ops}, f)
     kern = timer.summary() if timer is not None else {'conv_fwd': [1, 0.0, 0.0, 1.0]}
     ms = dt / args.steps * 1e3
     value = B * world * args.steps / dt

@@ -257,6 +257,7 @@ class LaunchTimer(object):
         self.rec = []
         self.detail = detail
         self._pool = []
+        self.ops = []   # issue order: (kind, shape key, flops, bytes, dispatches) -- tools/rocprof_families.py --ops
 
     def _event(self):
         ev = ctypes.c_void_p()
@@ -274,6 +275,7 @@ class LaunchTimer(object):
             ops.timing_disarm(ctypes.byref(n))
         self.rec.append((kind if not self.detail else (kind, key), flops, nbytes,
                          [(ev[2 * i], ev[2 * i + 1]) for i in range(n.value)]))
+        self.ops.append((kind, key, flops, nbytes, n.value))
 
     def summary(self):
         """{kind: [launches, flops, bytes, seconds]} (seconds = summed kernel time)."""

@@ -167,6 +167,79 @@ def pmc(d, counter):
     return tot, calls
 
 
+def _pmc_rows(d, counter):
+    rows = []
+    for path in _find(d, 'counter_collection.csv'):
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                if r['Counter_Name'] == counter:
+                    rows.append((int(r['Dispatch_Id']), r['Kernel_Name'], float(r['Counter_Value']),
+                                 int(r['Start_Timestamp']), int(r['End_Timestamp'])))
+    return sorted(rows)
+
+
+def per_op(d, counter, ops):
+    """The counter summed per conv op of bench.py's timing pass (its ops in
+    issue order from --op-log): the pass lies between the 3rd and 4th marker;
+    on one stream its dispatches come in issue order, each op's primary
+    kernel opening it and its secondaries (split-K reduce) following."""
+    rows = _pmc_rows(d, counter)
+    m = [(s, e) for _, n, _, s, e in rows if MARKER in n]
+    if len(m) < 4:
+        raise SystemExit('rocprof_families: %s has no timing-pass markers (run bench.py with the timer)' % d)
+    lo, hi = m[2][1], m[3][0]
+    conv = iter([i for i, o in enumerate(ops) if o[0] in CONV_FAMILIES])
+    vals, cur = [0.0] * len(ops), None
+    for _, name, v, s, e in rows:
+        if s < lo or e > hi or MARKER in name:
+            continue
+        fam, prim = family(name)
+        if fam not in CONV_FAMILIES:
+            continue
+        if prim:
+            cur = next(conv)
+            if ops[cur][0] != fam:
+                raise SystemExit('rocprof_families: op %d is %s, its dispatch %s' % (cur, ops[cur][0], name[:60]))
+        vals[cur] += v
+    if next(conv, None) is not None:
+        raise SystemExit('rocprof_families: fewer conv dispatches than ops in the timing pass')
+    return vals
+
+
+def op_table(fetch_dir, write_dir, op_log):
+    """Per conv shape and direction: PMC HBM bytes per call (FETCH_SIZE x 2 +
+    WRITE_SIZE) against its algorithmic bytes, and the excess per step."""
+    with open(op_log) as f:
+        meta = json.load(f)
+    ops = meta['ops']
+    rd, wr = per_op(fetch_dir, 'FETCH_SIZE', ops), per_op(write_dir, 'WRITE_SIZE', ops)
+    groups = defaultdict(lambda: [0, 0.0, 0.0, 0.0])
+    for i, (kind, key, fl, nb, nd) in enumerate(ops):
+        if kind not in CONV_FAMILIES:
+            continue
+        g = groups[(kind, key)]
+        g[0] += 1
+        g[1] += nb
+        g[2] += 2.0 * rd[i] * 1024 + wr[i] * 1024
+        g[3] += fl
+    per = meta.get('timing_steps', 1)
+    out = []
+    for (kind, key), (n, nb, pb, fl) in groups.items():
+        out.append({'kind': kind, 'shape': key, 'calls_per_step': n / per,
+                    'algorithmic_bytes_per_call': round(nb / n), 'pmc_bytes_per_call': round(pb / n),
+                    'pmc_over_algorithmic': round(pb / nb, 3) if nb else None,
+                    'excess_MB_per_step': round((pb - nb) / per / 1e6, 2),
+                    'gflop_per_call': round(fl / n / 1e9, 3)})
+    out.sort(key=lambda r: -r['excess_MB_per_step'])
+    tot = {k: [0.0, 0.0] for k in CONV_FAMILIES}
+    for r in out:
+        tot[r['kind']][0] += r['algorithmic_bytes_per_call'] * r['calls_per_step']
+        tot[r['kind']][1] += r['pmc_bytes_per_call'] * r['calls_per_step']
+    fam = {k: {'algorithmic_MB_per_step': round(a / 1e6, 1), 'pmc_MB_per_step': round(p / 1e6, 1),
+               'pmc_over_algorithmic': round(p / a, 3) if a else None} for k, (a, p) in tot.items()}
+    return out, fam
+
+
 def _bench_line(path):
     """The JSON line bench.py printed in the traced run (its log file)."""
     with open(path) as f:
@@ -185,6 +258,7 @@ def main():
     ap.add_argument('--steps', type=int, default=0, help='steps in the traced run (warmup+timed) for per-step totals')
     ap.add_argument('--bench-line', help='log of the traced bench.py run: its line gives the algorithmic FLOPs / bytes '
                                          'per call of each conv family and the number of timed steps')
+    ap.add_argument('--ops', help='op log of the PMC runs (bench.py --op-log): adds the per-shape PMC table')
     ap.add_argument('--out')
     ap.add_argument('--config', default='C2', help='bench.py workload the runs were taken on')
     a = ap.parse_args()
@@ -206,7 +280,7 @@ def main():
     out = {}
     for fam, o in sorted(fams.items(), key=lambda kv: -kv[1]['ns']):
         calls = max(o['calls'], 1)
-        e = {'calls': o['calls'], 'dispatches': o['dispatches'], 'total_ms': round(o['ns'] * 1e-6, 3),
+        e = {'calls': o['calls'], 'dispatches': o['dispatches'], 'total_ms': round(o['ns'] * 1e-6, 6),
              'avg_call_us': round(o['ns'] / calls * 1e-3, 2)}
         if fetch and write and fam in fetch[0] and fam in write[0]:
             # KB -> bytes; FETCH_SIZE x2 (gfx950 wide-read correction)
@@ -225,7 +299,7 @@ def main():
             if gui and gui[0].get(fam):
                 e['gpu_active_cycles_per_call'] = round(gui[0][fam] / 8 / n)
         if a.steps:
-            e['ms_per_step'] = round(e['total_ms'] / a.steps, 4)
+            e['ms_per_step'] = round(e['total_ms'] / a.steps, 6)
             e['calls_per_step'] = round(o['calls'] / a.steps, 2)
         q = alg.get(fam)
         if q and q.get('algorithmic_flops_per_launch') and a.steps:
@@ -259,9 +333,11 @@ def main():
                 res['conv_path']['pmc_hbm_frac'] = round(pb / (ms * 1e-3) / HBM_PEAK, 4)
     if len(wins) > 1:   # bench.py's eager, single-stream timing pass: what its HIP events time
         tp = kernel_trace(rows, wins[1])
-        res['timing_pass'] = {f: {'calls': tp[f]['calls'], 'total_ms': round(tp[f]['ns'] * 1e-6, 3),
+        res['timing_pass'] = {f: {'calls': tp[f]['calls'], 'total_ms': round(tp[f]['ns'] * 1e-6, 6),
                                   'avg_call_us': round(tp[f]['ns'] / max(tp[f]['calls'], 1) * 1e-3, 2)}
                               for f in CONV_FAMILIES if f in tp}
+    if a.ops and a.fetch and a.write:
+        res['per_shape'], res['per_shape_families'] = op_table(a.fetch, a.write, a.ops)
     txt = json.dumps(res, indent=1)
     if a.out:
         with open(a.out, 'w') as f:
