@@ -102,6 +102,20 @@ class SyncBatchNorm2d(nn.Module):
         self.register_buffer('running_mean', torch.zeros(num_features))
         self.register_buffer('running_var', torch.ones(num_features))
         self.register_buffer('num_batches_tracked', torch.tensor(0, dtype=torch.long))
+        # replication state (batchnorm.py:42-46), set by sync_batchnorm.replicate's callbacks
+        self._is_parallel = False
+        self._parallel_id = None
+        self._sync_group = None
+
+    def __data_parallel_replicate__(self, ctx, copy_id):
+        """batchnorm.py:80-88: copy 0 is the master.  One process per GPU: the
+        copies are the ranks, and ctx.sync_master is the rank group whose
+        transport (eegan_hip.dist: RCCL or the peer-write kernel) carries the
+        statistics; the kernels synchronise whenever it spans more than one
+        rank, which is when the reference leaves F.batch_norm (batchnorm.py:50)."""
+        self._parallel_id = copy_id
+        self._sync_group = getattr(ctx, 'sync_master', None)
+        self._is_parallel = self._sync_group is not None and self._sync_group.world > 1
 
     def forward(self, x, act=None, slope=0.2, up2=False):
         if not self.training:

@@ -1,2 +1,3 @@
 from .batchnorm import SynchronizedBatchNorm1d, SynchronizedBatchNorm2d, SynchronizedBatchNorm3d
-from .replicate import DataParallelWithCallback, patch_replication_callback
+from .replicate import (CallbackContext, DataParallelWithCallback, RankGroup, execute_replication_callbacks,
+                        patch_replication_callback)

@@ -177,3 +177,31 @@ def test_gradient_penalty_mask_sources_detached_only_inside_the_scope():
     assert not Fn.DETACH_MASK_SRC
     with Fn.detached_mask_sources(False):
         assert Fn._mask_src(t, ACT_CODES['relu']) is t
+
+
+def test_replication_callbacks_one_process():
+    """sync_batchnorm.replicate's callback API (replicate.py:23-88) in one
+    process: wrapping runs __data_parallel_replicate__ on every SyncBN with
+    copy_id = the rank (0), one shared context per submodule position whose
+    sync_master is the rank group; a single copy is not parallel (the
+    reference keeps F.batch_norm then, batchnorm.py:50)."""
+    import models
+    from sync_batchnorm import (CallbackContext, DataParallelWithCallback, execute_replication_callbacks,
+                                patch_replication_callback)
+    g = DataParallelWithCallback(models.Gen(8, 100))
+    bns = [m for m in g.module.modules() if hasattr(m, '__data_parallel_replicate__')]
+    assert bns and all(m._parallel_id == 0 and not m._is_parallel for m in bns)
+    assert all(m._sync_group.world == 1 and m._sync_group.rank == 0 for m in bns)
+    assert g.replicate(g.module, [0]) == [g.module]
+    # two copies in one process (the reference's own replicate): master first, shared contexts
+    seen = []
+
+    class M(torch.nn.Module):
+        def __data_parallel_replicate__(self, ctx, copy_id):
+            seen.append((id(ctx), copy_id))
+    a, b = torch.nn.Sequential(M()), torch.nn.Sequential(M())
+    ctxs = execute_replication_callbacks([b, a], copy_ids=[1, 0])
+    assert [c for _, c in seen] == [0, 1] and seen[0][0] == seen[1][0]
+    assert isinstance(ctxs[1], CallbackContext) and ctxs[1].sync_master.world == 1
+    dp = torch.nn.DataParallel(models.ATTR_Enhance())
+    assert patch_replication_callback(dp) is dp
