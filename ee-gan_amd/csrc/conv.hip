@@ -3635,7 +3635,7 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   dim3 fgrid = grid;   // conv_fast_kernel's grid: the XCD raster when it applies
   {
     const long nb = (long)grid.x * grid.y * grid.z;
-    const int xcd = knob("xcd", 1);
+    const int xcd = knob("xcd", 0);
     if (xcd && nb >= knob("xcd_minb", 64) && nb < (1L << 30)) {
       // rows per group G ~ sqrt(S * B / A), S = blocks per XCD; per tile the weight rows carry
       // TCO * taps * C and the pixel tile ~ TPIX * st^2 * C unique bytes (taps re-read pixels)
