@@ -3879,8 +3879,12 @@ static long wgrad_x_bytes(const eegan_conv_desc* d) {
 }
 static long wgrad_dy_bytes(const eegan_conv_desc* d) { return (long)d->N * d->Ho * d->Wo * d->ldy * 2; }
 // the pipelined kernel addresses its operands with 32-bit buffer offsets
+// <= 16 output channels (get_image / get_mask heads, models.py:25-41) also take the
+// pipelined kernels, as a 32-row tile whose rows >= Cout load zeros and are never
+// stored (knob wgrad_small=0: the register-staged conv_wgrad_kernel<16, ...>)
 static bool wgrad_glds_ok(const eegan_conv_desc* d) {
-  return d->K > 16 && wgrad_x_bytes(d) < 0x7fffffffL && wgrad_dy_bytes(d) < 0x7fffffffL;
+  return (d->K > 16 || (d->C % 8 == 0 && knob("wgrad_small", 1))) && wgrad_x_bytes(d) < 0x7fffffffL &&
+         wgrad_dy_bytes(d) < 0x7fffffffL;
 }
 
 // blocks of conv_wgrad_thin_kernel for this shape, or 0 when it does not apply
@@ -3927,7 +3931,7 @@ static void wgrad_plan(const eegan_conv_desc* d, int& TCO, int& TK, int& nsplit,
     pps = 0;
     return;
   }
-  TCO = d->K > 64 ? 128 : d->K > 32 ? 64 : (d->K > 16 && wgrad_glds_ok(d)) ? 32 : d->K > 16 ? 64 : 16;
+  TCO = d->K > 64 ? 128 : d->K > 32 ? 64 : wgrad_glds_ok(d) ? 32 : d->K > 16 ? 64 : 16;
   TK = K > 64 ? 128 : 64;
   const int P = d->N * d->Ho * d->Wo;
   const int tiles = ee_cdiv(d->K, TCO) * ee_cdiv(K, TK);
