@@ -173,6 +173,47 @@ __global__ __launch_bounds__(NT) void scale_dot_partial_kernel(const bf16_t* g, 
   if (threadIdx.x == 0) ws[blockIdx.x] = acc;
 }
 
+// ScaleAdd's backward with the residual branch's activation gated, under create_graph
+// (the gradient penalty through resD): out = (r ? r : 0) + s * act'(q) * a and, when ws
+// is given, the per-block partials of <act'(q) * a, b>.  q = the activation output h
+// whose derivative gates (piecewise constant: no gradient flows into it)
+__global__ __launch_bounds__(NT) void scale_gate_kernel(const bf16_t* a_, int lda, const bf16_t* q_, int ldq,
+                                                        const bf16_t* b_, int ldb, const float* gamma, float alpha,
+                                                        long P, int C, const bf16_t* r, int ldr, bf16_t* out, int ldo,
+                                                        float* ws, int act, float slope) {
+  __shared__ float red[16];
+  const int C8 = (C + 7) / 8;
+  const bool vec = (lda % 8 == 0) && (ldq % 8 == 0) && (ldo % 8 == 0) && (!r || ldr % 8 == 0) &&
+                   (!ws || ldb % 8 == 0);
+  const float s = alpha * (gamma ? *gamma : 1.f);
+  float acc = 0.f;
+  GRID_LOOP(e, P * C8) {
+    const long p = e / C8;
+    const int c0 = (int)(e % C8) * 8;
+    const int nv = min(8, C - c0);
+    V8 a = load8(a_ + p * lda + c0, nv, vec);
+    const V8 q = load8(q_ + p * ldq + c0, nv, vec);
+    V8 b;
+    if (ws) b = load8(b_ + p * ldb + c0, nv, vec);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float m = act_dgrad_from_y(q.v[j], act, slope);
+      if (ws) acc += (a.v[j] * m) * b.v[j];
+      a.v[j] *= s * m;
+    }
+    if (r) {
+      V8 c = load8(r + p * ldr + c0, nv, vec);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a.v[j] += c.v[j];
+    }
+    store8(out + p * ldo + c0, a, nv, vec);
+  }
+  if (ws) {   // block-uniform
+    acc = block_sum(acc, red);
+    if (threadIdx.x == 0) ws[blockIdx.x] = acc;
+  }
+}
+
 __global__ void dot_final_kernel(const float* ws, int n, float scale, float* out, int accumulate) {
   __shared__ float red[16];
   float acc = 0.f;
@@ -643,6 +684,22 @@ int eegan_scale_dot_res(const uint16_t* g, int ldg, const uint16_t* h, int ldh, 
   scale_dot_partial_kernel<<<blocks, NT, 0, s>>>(g, ldg, h, ldh, gamma, alpha, P, C, r, ldr, out, ldo, ws, 0, 0.f);
   int rc = ee_check_launch("scale_dot_partial");
   if (rc) return rc;
+  dot_final_kernel<<<1, 1024, 0, s>>>(ws, blocks, 1.f, dot_out, accumulate);
+  return ee_check_launch("dot_final");
+}
+
+int eegan_scale_gate(const uint16_t* a, int lda, const uint16_t* q, int ldq, int act, float slope, const float* gamma,
+                     float alpha, long P, int C, const uint16_t* r, int ldr, const uint16_t* b, int ldb, uint16_t* out,
+                     int ldo, float* ws, float* dot_out, int accumulate, hipStream_t s) {
+  if (dot_out && (!ws || !b)) {
+    ee_set_error("scale_gate: the dot needs b and a workspace");
+    return -22;
+  }
+  const int blocks = std::min(1024, grid_for(P * ((C + 7) / 8)));
+  scale_gate_kernel<<<blocks, NT, 0, s>>>(a, lda, q, ldq, b, ldb, gamma, alpha, P, C, r, ldr, out, ldo,
+                                          dot_out ? ws : nullptr, act, slope);
+  int rc = ee_check_launch("scale_gate");
+  if (rc || !dot_out) return rc;
   dot_final_kernel<<<1, 1024, 0, s>>>(ws, blocks, 1.f, dot_out, accumulate);
   return ee_check_launch("dot_final");
 }

@@ -85,6 +85,7 @@ _SIGS = {
     'eegan_cat_channels': ([P, P, P, I, L, P, I, P], I),
     'eegan_scale_dot': ([P, I, P, I, P, F, L, I, P, I, P, P, I, I, F, P], I),
     'eegan_scale_dot_res': ([P, I, P, I, P, F, L, I, P, I, P, I, P, P, I, P], I),
+    'eegan_scale_gate': ([P, I, P, I, I, F, P, F, L, I, P, I, P, I, P, I, P, P, I, P], I),
     'eegan_dot_workspace': ([], L),
     'eegan_dot': ([P, I, P, I, L, I, F, P, P, I, P], I),
     'eegan_chansum_workspace': ([L, I], L),
@@ -168,7 +169,7 @@ def _load():
 
 LIB = _load()
 ABI_VERSION = LIB.eegan_abi_version()
-EXPECTED_ABI = 15
+EXPECTED_ABI = 16
 if ABI_VERSION != EXPECTED_ABI:
     raise ImportError('%s has ABI %d, these bindings need %d: rebuild (make -C ee-gan_amd/csrc)'
                       % (LIB_PATH, ABI_VERSION, EXPECTED_ABI))

@@ -446,9 +446,10 @@ def _act_deferred(ctx, fused, cg):
     """Whether this layer's activation backward runs in its consumers instead.
     defer_act=True: every consumer is a conv with in_act (gates in the first-
     order backward and, through GatedConvBwdDataFn, under create_graph);
-    defer_act='first_order': the consumer gates only in the first-order
-    backward (resD's ScaleAddFn h_act)."""
-    return bool(ctx.defer_act) and (fused or (cg and ctx.defer_act is True))
+    defer_act='first_order': the consumer gates in the first-order backward
+    and, with FUSE_GP_GATE, under create_graph too (resD's ScaleAddFn h_act:
+    ScaleAddGateBwdFn)."""
+    return bool(ctx.defer_act) and (fused or (cg and (ctx.defer_act is True or FUSE_GP_GATE)))
 
 
 class Conv2dFn(torch.autograd.Function):
@@ -910,12 +911,72 @@ class ScaleAddFn(torch.autograd.Function):
             if not _needed(ctx, 2):
                 d_g = None
             return d_res, d_h, d_g, None, None
-        if FUSE_GP_ADDS and d_res is not None and ctx.needs_input_grad[1]:
+        if FUSE_GP_GATE and h_act and d_res is not None and ctx.needs_input_grad[1]:
+            # create_graph with the residual branch's activation deferred here (its
+            # producer, resD's conv_r[2], skips its ActBwdFn: _act_deferred)
+            d_res, d_h = ScaleAddGateBwdFn.apply(g, _mask_src(h, h_act), gamma, h_act, ctx.h_slope)
+        elif FUSE_GP_ADDS and d_res is not None and ctx.needs_input_grad[1]:
             d_res, d_h = ScaleAddBwdFn.apply(g, gamma)
         else:
             d_h = ScaleFn.apply(g, gamma) if ctx.needs_input_grad[1] else None
         d_g = DotFn.apply(g, h) if _needed(ctx, 2) else None
         return d_res, d_h, d_g, None, None
+
+
+# False: under create_graph ScaleAddFn does not gate, and resD's conv_r[2] runs its
+# activation backward as its own ActBwdFn pass in the gradient penalty's first
+# backward (and that pass's backward in the second); module constant for A/B
+FUSE_GP_GATE = True
+
+
+class ScaleAddGateBwdFn(torch.autograd.Function):
+    """(g, gamma * g * act'(h)): ScaleAddFn's gradients of (res, z) under
+    create_graph, z the pre-activation of the residual branch h = act(z)
+    (resD, models.py:270-278: the last LeakyReLU's backward folded in, as the
+    first-order path does) -- ONE pass instead of ScaleAddBwdFn's scale and
+    conv_r[2]'s ActBwdFn.  act' is piecewise constant, so h gets no gradient.
+    The double backward is one pass too: gg_res + gamma * act'(h) * gg_z and
+    gamma's <act'(h) * gg_z, g> (eegan_scale_gate), where the composition it
+    replaces ran ScaleAddBwdFn's pass and ActBwdFn's backward."""
+
+    @staticmethod
+    def forward(ctx, g, h, gamma, act, slope):
+        ctx.act, ctx.slope = act, slope
+        ctx.save_for_backward(g, h, gamma)
+        N, C, H, W = g.shape
+        out = empty_nhwc(N, C, H, W, g.device)
+        ops.scale_gate(g.data_ptr(), ld_of(g), h.data_ptr(), ld_of(h), act, slope, gamma.data_ptr(), 1.0, N * H * W, C,
+                       None, 0, None, 0, out.data_ptr(), ld_of(out), None, None, 0, stream())
+        return g, out
+
+    @staticmethod
+    def backward(ctx, gg_res, gg_z):
+        g, h, gamma = ctx.saved_tensors
+        if gg_z is None:
+            return gg_res, None, None, None, None
+        gg_z = _as_bf16_grad(gg_z)
+        if gg_res is not None:
+            gg_res = _as_bf16_grad(gg_res)
+        need_gamma = _needed(ctx, 2)
+        if torch.is_grad_enabled():   # a third-order pass: composed of differentiable Functions
+            m = ActBwdFn.apply(gg_z, h.detach(), ctx.act, ctx.slope)
+            out = ScaleFn.apply(m, gamma)
+            if gg_res is not None:
+                out = out + gg_res
+            return out, None, (DotFn.apply(m, g) if need_gamma else None), None, None
+        N, C, H, W = gg_z.shape
+        out = empty_nhwc(N, C, H, W, gg_z.device)
+        d_g = sink = ws = None
+        if need_gamma:
+            sink = _grad_sink(ctx, 2)
+            d_g = torch.empty(1, dtype=F32, device=g.device) if sink is None else None
+            ws = workspace(ops.dot_workspace(), g.device)
+        ops.scale_gate(gg_z.data_ptr(), ld_of(gg_z), h.data_ptr(), ld_of(h), ctx.act, ctx.slope, gamma.data_ptr(), 1.0,
+                       N * H * W, C, ptr(gg_res), ld_of(gg_res) if gg_res is not None else 0,
+                       g.data_ptr() if need_gamma else None, ld_of(g) if need_gamma else 0, out.data_ptr(),
+                       ld_of(out), ptr(ws), (sink if d_g is None else d_g).data_ptr() if need_gamma else None,
+                       int(need_gamma and d_g is None), stream())
+        return out, None, d_g, None, None
 
 
 class ScaleAddBwdFn(torch.autograd.Function):

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 15  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
+#define EEGAN_ABI_VERSION 16  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
                                 4: rectangular (local x global) DAMSM words / sentence blocks on MFMA;
                                 5: GlobalAttentionGeneral (eegan_gag_*), words backward reuses the forward's prep;
                                 6: device input pipeline (eegan_pipe_*);
@@ -39,7 +39,8 @@ extern "C" {
                                 12: ScaleAdd double backward in one pass (eegan_scale_dot_res);
                                 13: split-K counters in the conv descriptor, for the in-kernel split-K finish;
                                 14: per-region peer wait bound (eegan_peer_set_wait);
-                                15: planner objective in the conv descriptor (eegan_conv_desc.plan) */
+                                15: planner objective in the conv descriptor (eegan_conv_desc.plan);
+                                16: gated ScaleAdd backward under create_graph (eegan_scale_gate) */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
@@ -205,6 +206,14 @@ int eegan_scale_dot(const uint16_t* g, int ldg, const uint16_t* h, int ldh, cons
 int eegan_scale_dot_res(const uint16_t* g, int ldg, const uint16_t* h, int ldh, const float* gamma, float alpha, long P,
                         int C, const uint16_t* r, int ldr, uint16_t* out, int ldo, float* ws, float* dot_out,
                         int accumulate, hipStream_t stream);
+/* ScaleAdd backward with the residual branch's activation folded in, under create_graph (the gradient
+ * penalty through resD, models.py:270-278; ABI 16): out = r + alpha*gamma*act'(q)*a with q the activation
+ * output that gates (r optional) and, with dot_out, dot_out (+)= <act'(q)*a, b>; first backward:
+ * a = g, q = h (gamma*g*act'(h), no dot); second backward: a = gg_h, q = h, r = gg_res, b = g (gamma's
+ * gradient).  ws = eegan_dot_workspace() bytes (unused without dot_out) */
+int eegan_scale_gate(const uint16_t* a, int lda, const uint16_t* q, int ldq, int act, float slope, const float* gamma,
+                     float alpha, long P, int C, const uint16_t* r, int ldr, const uint16_t* b, int ldb, uint16_t* out,
+                     int ldo, float* ws, float* dot_out, int accumulate, hipStream_t s);
 long eegan_dot_workspace(void);
 int eegan_dot(const uint16_t* x, int ldx, const uint16_t* y, int ldy, long P, int C, float scale, float* ws,
               float* out, int accumulate, hipStream_t s);
