@@ -487,7 +487,7 @@ def test_fused_activation_backward_matches_separate(gpu, monkeypatch):
         assert rel_l2(gp1[n], gp0[n]) < 2e-2, n
 
 
-@pytest.mark.parametrize('knob', ['FUSE_GP_ADDS', 'FUSE_GP_ACT'])
+@pytest.mark.parametrize('knob', ['FUSE_GP_ADDS', 'FUSE_GP_ACT', 'FUSE_GP_GATE'])
 def test_gradient_penalty_fused_adds_match_separate(gpu, monkeypatch, knob):
     """The gradient penalty's create_graph backward with resD's two input
     gradients summed in the conv epilogue (PoolConvBwdDataFn) and ScaleAdd's
@@ -495,8 +495,11 @@ def test_gradient_penalty_fused_adds_match_separate(gpu, monkeypatch, knob):
     plus autograd adds (Fn.FUSE_GP_ADDS = False); and with the LeakyReLU
     backward folded into the consuming conv's data gradient
     (GatedConvBwdDataFn) against separate ActBwdFn passes
-    (Fn.FUSE_GP_ACT = False): the same values, rounded to bf16 once instead of
-    twice, so gradients agree to bf16 rounding."""
+    (Fn.FUSE_GP_ACT = False); and with resD's last LeakyReLU folded into
+    ScaleAdd's create_graph backward (ScaleAddGateBwdFn: gamma * g * act'(h)
+    in one pass, its double backward in one more) against ScaleAddBwdFn plus
+    conv_r[2]'s ActBwdFn (Fn.FUSE_GP_GATE = False): the same values, rounded
+    to bf16 once instead of twice, so gradients agree to bf16 rounding."""
     import models
     from eegan_hip import functional as Fn
     from eegan_hip.trainer import Trainer
