@@ -911,9 +911,10 @@ class ScaleAddFn(torch.autograd.Function):
             if not _needed(ctx, 2):
                 d_g = None
             return d_res, d_h, d_g, None, None
-        if FUSE_GP_GATE and h_act and d_res is not None and ctx.needs_input_grad[1]:
+        if FUSE_GP_GATE and FUSE_GP_ACT and h_act and d_res is not None and ctx.needs_input_grad[1]:
             # create_graph with the residual branch's activation deferred here (its
-            # producer, resD's conv_r[2], skips its ActBwdFn: _act_deferred)
+            # producer, resD's conv_r[2], skips its ActBwdFn: _act_deferred -- the same
+            # switches, FUSE_ACT_BWD, FUSE_GP_ACT and FUSE_GP_GATE, decide both sides)
             d_res, d_h = ScaleAddGateBwdFn.apply(g, _mask_src(h, h_act), gamma, h_act, ctx.h_slope)
         elif FUSE_GP_ADDS and d_res is not None and ctx.needs_input_grad[1]:
             d_res, d_h = ScaleAddBwdFn.apply(g, gamma)
