@@ -1840,7 +1840,7 @@ struct WgradArgs {
   int accumulate;
   int quad;            // split slab in co-quad order [Cout/4][K][4] (Cout % 4 == 0): one 16-B store per lane
   int stage;           // unsplit dW through LDS: 16-B read-add-write runs along Cin (Cin % 4 == 0, host-checked)
-  int xcd_remap;       // conv_wgrad_fast_kernel: blocks of one (co tile, split) on one XCD (grid size % 8 == 0)
+  int xcd_remap;       // conv_wgrad_fast / glds kernels: blocks of one (co tile, split) on one XCD (grid size % 8 == 0)
 };
 
 // split-slab column (co, (tap, c)) -> channels-last weight layout [Cout][R][S][Cin]
@@ -2173,8 +2173,22 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_glds_kernel(WgradArgs w, lo
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wi = wave / WKK, wj = wave % WKK;
-  const int co0 = blockIdx.y * TCO, kb0 = blockIdx.x * TK;
-  const int p_begin = blockIdx.z * w.p_per_split;
+  // XCD remap as conv_wgrad_fast_kernel's (WgradArgs::xcd_remap): a (co tile, split)'s k
+  // tiles share one XCD's L2 -- they all read the same dy and x rows (with an up2 source,
+  // each x pixel serves 4 output pixels x 9 taps)
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (w.xcd_remap) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int total = gx * gy * gridDim.z;
+    const int lin = bx + gx * (by + gy * bz);
+    const int logical = (lin & 7) * (total >> 3) + (lin >> 3);
+    bx = logical % gx;
+    const int t = logical / gx;
+    by = t % gy;
+    bz = t / gy;
+  }
+  const int co0 = by * TCO, kb0 = bx * TK;
+  const int p_begin = bz * w.p_per_split;
   const int p_end = min(w.P, p_begin + w.p_per_split);
   const int nk = p_begin < p_end ? (p_end - p_begin + BK - 1) / BK : 0;
   const int PH = w.IH >> w.up2, PW = w.IW >> w.up2;
@@ -2292,7 +2306,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_glds_kernel(WgradArgs w, lo
       for (int j = 0; j < FJ; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
   }
-  wgrad_epilogue<FI, FJ, WT_CO, WT_K>(w, acc, co0, kb0, wi, wj, lane);
+  wgrad_epilogue<FI, FJ, WT_CO, WT_K>(w, acc, co0, kb0, wi, wj, lane, bz);
 }
 
 // Weight gradient with the per-K-step index math hoisted (cf. conv_fast_kernel):
@@ -3635,7 +3649,7 @@ int launch_igemm(ConvArgs a, int Pc_max, float* part_ws, hipStream_t s, long src
   dim3 fgrid = grid;   // conv_fast_kernel's grid: the XCD raster when it applies
   {
     const long nb = (long)grid.x * grid.y * grid.z;
-    const int xcd = knob("xcd", 0);
+    const int xcd = knob("xcd", 1);
     if (xcd && nb >= knob("xcd_minb", 64) && nb < (1L << 30)) {
       // rows per group G ~ sqrt(S * B / A), S = blocks per XCD; per tile the weight rows carry
       // TCO * taps * C and the pixel tile ~ TPIX * st^2 * C unique bytes (taps re-read pixels)

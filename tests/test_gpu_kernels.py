@@ -781,12 +781,16 @@ def test_wgrad_staged_epilogue_bit_identical(gpu, monkeypatch):
 def test_wgrad_xcd_remap_bit_identical(gpu, monkeypatch):
     """Weight-gradient tiles remapped so one (co tile, split)'s k tiles share an
     XCD (EEGAN_CONV wgrad_xcd=1, default) compute the same tiles: torch.equal with
-    the plain block order, split and unsplit, fresh and accumulated."""
+    the plain block order, split and unsplit, fresh and accumulated -- on the
+    pipelined kernel for power-of-two grids and on the LDS-DMA kernel for the
+    others (17^2, and up2 sources: the generator's upsampling convs)."""
     Fn, T, _ = _mods()
-    for N, Cin, H, W, Cout, k, st, pad in [(16, 128, 32, 32, 128, 3, 1, 1), (8, 64, 64, 64, 64, 3, 1, 1),
-                                            (8, 64, 32, 32, 128, 4, 2, 1), (8, 768, 4, 4, 1024, 3, 1, 1)]:
+    for N, Cin, H, W, Cout, k, st, pad, up2 in [(16, 128, 32, 32, 128, 3, 1, 1, 0), (8, 64, 64, 64, 64, 3, 1, 1, 0),
+                                                 (8, 64, 32, 32, 128, 4, 2, 1, 0), (8, 768, 4, 4, 1024, 3, 1, 1, 0),
+                                                 (16, 192, 17, 17, 192, 3, 1, 1, 0), (8, 128, 16, 16, 128, 3, 1, 1, 1),
+                                                 (4, 64, 32, 32, 32, 3, 1, 1, 1)]:
         torch.manual_seed(Cin + H + Cout)
-        g = Fn.Geom(Cout, k, k, st, pad, pad, 0)
+        g = Fn.Geom(Cout, k, k, st, pad, pad, up2)
         x = _nhwc(torch.randn(N, Cin, H, W), gpu)
         Ho, Wo = g.out_hw(H, W)
         dz = _nhwc(torch.randn(N, Cout, Ho, Wo), gpu)
