@@ -99,9 +99,128 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   }
 }
 
+// ---- Adam step fused with the bf16 weight re-pack (FlatAdam over conv weights) ----
+// The separate form reads every updated conv weight back from HBM in the pack
+// kernel (and launches it).  Here a workgroup owns a 64 (output channel) x 64
+// (input channel) tile of one tap of one conv weight -- channels-last fp32,
+// element (co, tap, ci) at p_off + (co * RS + tap) * Cin + ci -- steps it (the
+// same adam_elem arithmetic as adam_kernel), keeps the new values in LDS and
+// writes both packed images from there: the forward image row co, columns
+// tap * Cgp(Cin) + ci (16-B runs along ci) and the data-gradient image row ci,
+// columns tap * Cgp(Cout) + co (the transpose, 4-B pairs along co).  Packing
+// padding (rows past Cout / Cin, the K tail) is never written: it keeps the
+// zeros of the full pack that created the images.  Parameters that are not
+// packed conv weights (biases, linear layers, gains, the flat buffer's
+// alignment gaps) are stepped by range jobs of 4096 elements per workgroup.
+// Job table (int64, 8 per job): conv {0, p_off, fwd image or 0, bwd image or 0,
+// Cout, Cin, R*S, 0}, range {1, start, len, 0...}; then njobs + 1 prefix block
+// offsets.
+constexpr int AP_T = 64, AP_RANGE = 4096;
+
+EE_DEV int ap_cgp(int C) { return C <= 8 ? 8 : (C + 31) / 32 * 32; }
+
+template <bool B1ZERO>
+__global__ __launch_bounds__(256) void adam_pack_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        const long* __restrict__ table, int njobs, float b1,
+                                                        float b2, float lr, float eps, float wd,
+                                                        const double* __restrict__ step) {
+  __shared__ float buf[AP_T * (AP_T + 1)];
+  const double t = *step;
+  const float step_size = (float)((double)lr / (1.0 - pow((double)b1, t)));
+  const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, t));
+  const long* pre = table + 8L * njobs;
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pre[mid] <= blockIdx.x) lo = mid;
+    else hi = mid - 1;
+  }
+  const long* j = table + 8L * lo;
+  const long lb = (long)blockIdx.x - pre[lo];
+  const int tid = threadIdx.x;
+  if (j[0] == 1) {   // range job
+    const long s0 = j[1] + lb * AP_RANGE, s1 = min(j[1] + j[2], s0 + AP_RANGE);
+    for (long i = s0 + tid; i < s1; i += 256) {
+      float P = p[i], M = B1ZERO ? 0.f : m[i], V = v[i];
+      adam_elem<B1ZERO>(P, g[i], M, V, b1, b2, wd, step_size, bc2_sqrt, eps);
+      p[i] = P;
+      m[i] = M;
+      v[i] = V;
+    }
+    return;
+  }
+  const long off = j[1];
+  bf16_t* fwd = reinterpret_cast<bf16_t*>(j[2]);
+  bf16_t* bwd = reinterpret_cast<bf16_t*>(j[3]);
+  const int Cout = (int)j[4], Cin = (int)j[5], RS = (int)j[6];
+  const int nci = (Cin + AP_T - 1) / AP_T;
+  const int it = (int)(lb % nci), tap = (int)((lb / nci) % RS), ct = (int)(lb / ((long)nci * RS));
+  const int ci0 = it * AP_T, co0 = ct * AP_T;
+#pragma unroll 4
+  for (int k = 0; k < AP_T * AP_T / 256; ++k) {
+    const int e = k * 256 + tid, r = e / AP_T, c = e % AP_T;   // lanes along ci: 256-B rows
+    float P = 0.f;
+    if (co0 + r < Cout && ci0 + c < Cin) {
+      const long i = off + ((long)(co0 + r) * RS + tap) * Cin + ci0 + c;
+      P = p[i];
+      float M = B1ZERO ? 0.f : m[i], V = v[i];
+      adam_elem<B1ZERO>(P, g[i], M, V, b1, b2, wd, step_size, bc2_sqrt, eps);
+      p[i] = P;
+      m[i] = M;
+      v[i] = V;
+    }
+    buf[r * (AP_T + 1) + c] = P;
+  }
+  __syncthreads();
+  if (fwd) {   // rows co < Cout, this tap's channel run [0, Cgp(Cin)): pairs along ci
+    const int cg = ap_cgp(Cin), Kw = (RS * cg + 31) / 32 * 32, ncol = min(AP_T, cg - ci0);
+    for (int e = tid; e < AP_T * AP_T / 2; e += 256) {
+      const int r = e / (AP_T / 2), cp = 2 * (e % (AP_T / 2));
+      if (co0 + r < Cout && cp < ncol)
+        *reinterpret_cast<uint32_t*>(fwd + (long)(co0 + r) * Kw + tap * cg + ci0 + cp) =
+            pack2(buf[r * (AP_T + 1) + cp], buf[r * (AP_T + 1) + cp + 1]);
+    }
+  }
+  if (bwd) {   // rows ci < Cin, this tap's run [0, Cgp(Cout)): pairs along co
+    const int cg = ap_cgp(Cout), Kw = (RS * cg + 31) / 32 * 32, ncol = min(AP_T, cg - co0);
+    for (int e = tid; e < AP_T * AP_T / 2; e += 256) {
+      const int c = e / (AP_T / 2), rp = 2 * (e % (AP_T / 2));
+      if (ci0 + c < Cin && rp < ncol)
+        *reinterpret_cast<uint32_t*>(bwd + (long)(ci0 + c) * Kw + tap * cg + co0 + rp) =
+            pack2(buf[rp * (AP_T + 1) + c], buf[(rp + 1) * (AP_T + 1) + c]);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+long eegan_adam_pack_blocks(int Cout, int Cin, int R, int S) {
+  return (long)((Cout + AP_T - 1) / AP_T) * R * S * ((Cin + AP_T - 1) / AP_T);
+}
+
+long eegan_adam_range_blocks(long len) { return (len + AP_RANGE - 1) / AP_RANGE; }
+
+int eegan_adam_pack(float* p, const float* g, float* m, float* v, float beta1, float beta2, float lr, float eps,
+                    float weight_decay, double* step, const long* table, int njobs, long total_blocks,
+                    hipStream_t s) {
+  if (njobs <= 0 || total_blocks <= 0) {
+    ee_set_error("adam_pack: empty job table");
+    return -22;
+  }
+  adam_tick_kernel<<<1, 1, 0, s>>>(step);
+  int rc = ee_check_launch("adam_tick");
+  if (rc) return rc;
+  if (beta1 == 0.f)
+    adam_pack_kernel<true><<<(unsigned)total_blocks, 256, 0, s>>>(p, g, m, v, table, njobs, beta1, beta2, lr, eps,
+                                                                  weight_decay, step);
+  else
+    adam_pack_kernel<false><<<(unsigned)total_blocks, 256, 0, s>>>(p, g, m, v, table, njobs, beta1, beta2, lr, eps,
+                                                                   weight_decay, step);
+  return ee_check_launch("adam_pack");
+}
 
 int eegan_adam(float* p, const float* g, float* m, float* v, long n, float beta1, float beta2, float lr, float eps,
                float weight_decay, double* step, hipStream_t s) {

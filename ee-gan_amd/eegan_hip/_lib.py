@@ -135,6 +135,9 @@ _SIGS = {
     'eegan_attr_attn': ([P, P, P, I, I, I, F, P, P, P, P], I),
     'eegan_attr_attn_bwd': ([P, P, P, P, P, I, I, I, F, P, P, P, P], I),
     'eegan_adam': ([P, P, P, P, L, F, F, F, F, F, P, P], I),
+    'eegan_adam_pack_blocks': ([I, I, I, I], L),
+    'eegan_adam_range_blocks': ([L], L),
+    'eegan_adam_pack': ([P, P, P, P, F, F, F, F, F, P, P, I, L, P], I),
     'eegan_embedding': ([P, L, P, I, P, P], I),
     'eegan_lstm_bidir': ([P, P, P, I, I, I, I, P, P, P], I),
     'eegan_fid_preprocess': ([P, I, I, I, I, I, P, P, P, I, P], I),
@@ -169,7 +172,7 @@ def _load():
 
 LIB = _load()
 ABI_VERSION = LIB.eegan_abi_version()
-EXPECTED_ABI = 16
+EXPECTED_ABI = 17
 if ABI_VERSION != EXPECTED_ABI:
     raise ImportError('%s has ABI %d, these bindings need %d: rebuild (make -C ee-gan_amd/csrc)'
                       % (LIB_PATH, ABI_VERSION, EXPECTED_ABI))

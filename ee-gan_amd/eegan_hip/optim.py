@@ -49,7 +49,7 @@ import os
 import torch
 
 from ._lib import ops
-from .tensor import stream
+from .tensor import ptr, stream
 
 
 def _align(n, a=4):
@@ -57,6 +57,10 @@ def _align(n, a=4):
 
 
 OVERLAP = os.environ.get('EEGAN_GRAD_OVERLAP', '1') != '0'
+# EEGAN_ADAM_PACK=0: Adam over the flat buffer, then the conv weight re-pack as a
+# second launch (instead of eegan_adam_pack: one launch, the updated weights packed
+# from LDS without reading them back); module constant for A/B
+ADAM_PACK = os.environ.get('EEGAN_ADAM_PACK', '1') != '0'
 
 
 class FlatAdam(torch.optim.Optimizer):
@@ -98,6 +102,11 @@ class FlatAdam(torch.optim.Optimizer):
         self._pack_sig = None
         self._pack_table = None
         self._pack_total = 0
+        self._fused_sig = None
+        self._fused_table = None
+        self._fused_jobs = 0
+        self._fused_total = 0
+        self._fused_packs = []
         self.step_count = 0   # host mirror (state_dict); the kernels use step_dev
         self.step_dev = torch.zeros(1, dtype=torch.float64, device=dev)
         self._index = {id(p): i for i, p in enumerate(uniq)}
@@ -298,11 +307,72 @@ class FlatAdam(torch.optim.Optimizer):
         g = self.param_groups[0]
         b1, b2 = g['betas']
         self.step_count += 1
+        if ADAM_PACK and self._fused_plan():
+            ops.adam_pack(self.flat.data_ptr(), self.gflat.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), b1, b2,
+                          g['lr'], g['eps'], g['weight_decay'], self.step_dev.data_ptr(), self._fused_table.data_ptr(),
+                          self._fused_jobs, self._fused_total, stream())
+            self._gen[0] += 1
+            self._mark_packs(self._fused_packs)
+            return loss
         ops.adam(self.flat.data_ptr(), self.gflat.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.numel, b1, b2,
                  g['lr'], g['eps'], g['weight_decay'], self.step_dev.data_ptr(), stream())
         self._gen[0] += 1
         self._repack()
         return loss
+
+    def _packed_weights(self):
+        """(param, flat offset, cache) of this optimizer's conv weights with bf16 packs."""
+        out = []
+        for p, o, k, g in self._views:
+            c = getattr(p, '_eegan_packcache', None)
+            if c is None or p.dim() != 4 or c.scale is not None or (c.fwd is None and c.bwd is None):
+                continue
+            if not p.is_contiguous(memory_format=torch.channels_last):
+                raise RuntimeError('FlatAdam: conv weight %s is not stored channels-last' % (tuple(p.shape),))
+            out.append((p, o, c))
+        return out
+
+    def _fused_plan(self):
+        """The job table of eegan_adam_pack (conv weights as tap tiles, everything
+        else -- other parameters and the alignment gaps -- as element ranges),
+        rebuilt when the set of packs changes (never inside a capture).  False
+        when there is nothing to pack: the plain Adam launch then."""
+        ws = self._packed_weights()
+        if not ws:
+            return False
+        sig = tuple((id(c), o, ptr(c.fwd), ptr(c.bwd)) for p, o, c in ws)
+        if sig != self._fused_sig:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError('FlatAdam: the set of weight packs changed during graph capture; '
+                                   'run an eager warm-up step first')
+            rows, pre, pos = [], [0], 0
+            for p, o, c in sorted(ws, key=lambda t: t[1]):
+                if o > pos:
+                    rows += [1, pos, o - pos, 0, 0, 0, 0, 0]
+                    pre.append(pre[-1] + ops.adam_range_blocks(o - pos))
+                Cout, Cin, R, S = p.shape
+                rows += [0, o, ptr(c.fwd), ptr(c.bwd), Cout, Cin, R * S, 0]
+                pre.append(pre[-1] + ops.adam_pack_blocks(Cout, Cin, R, S))
+                pos = o + p.numel()
+            if pos < self.numel:
+                rows += [1, pos, self.numel - pos, 0, 0, 0, 0, 0]
+                pre.append(pre[-1] + ops.adam_range_blocks(self.numel - pos))
+            self._fused_jobs = len(pre) - 1
+            self._fused_table = torch.tensor(rows + pre, dtype=torch.int64).to(self.flat.device)
+            self._fused_total = pre[-1]
+            self._fused_packs = [(p, c) for p, o, c in ws]
+            self._fused_sig = sig
+        return True
+
+    @staticmethod
+    def _mark_packs(packs):
+        from .functional import PackCache
+        for p, c in packs:
+            key = PackCache._key(p)
+            if c.fwd is not None:
+                c.fwd_key = key
+            if c.bwd is not None:
+                c.bwd_key = key
 
     def _repack(self):
         """Refresh the registered bf16 packs of this optimizer's conv weights in

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define EEGAN_ABI_VERSION 16  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
+#define EEGAN_ABI_VERSION 17  /* 2: fp32 conv weights channels-last; 3: eegan_scale_dot act gate;
                                 4: rectangular (local x global) DAMSM words / sentence blocks on MFMA;
                                 5: GlobalAttentionGeneral (eegan_gag_*), words backward reuses the forward's prep;
                                 6: device input pipeline (eegan_pipe_*);
@@ -40,7 +40,8 @@ extern "C" {
                                 13: split-K counters in the conv descriptor, for the in-kernel split-K finish;
                                 14: per-region peer wait bound (eegan_peer_set_wait);
                                 15: planner objective in the conv descriptor (eegan_conv_desc.plan);
-                                16: gated ScaleAdd backward under create_graph (eegan_scale_gate) */
+                                16: gated ScaleAdd backward under create_graph (eegan_scale_gate);
+                                17: Adam fused with the conv weight re-pack (eegan_adam_pack) */
 
 const char* eegan_last_error(void);
 int eegan_abi_version(void);
@@ -428,6 +429,18 @@ int eegan_peer_status(void* own, int reset, int* timed_out);
  * corrections (graph-replay safe). */
 int eegan_adam(float* p, const float* g, float* m, float* v, long n, float beta1, float beta2, float lr, float eps,
                float weight_decay, double* step, hipStream_t s);
+/* The same Adam step fused with the re-pack of the optimizer's conv weights (ABI 17; replaces
+ * eegan_adam + eegan_conv_pack_weights_multi after each step): `table` is device memory, int64, 8 per
+ * job -- conv weight {0, element offset in p, forward image or 0, data-gradient image or 0, Cout, Cin,
+ * R*S, 0} (the weight channels-last [Cout][R][S][Cin], unscaled; the images as
+ * eegan_conv_pack_weights writes them, created by it: padding is never rewritten) or element range
+ * {1, start, len, 0, 0, 0, 0, 0} -- every element of p in exactly one job -- then njobs + 1 prefix
+ * offsets of the blocks each job takes (eegan_adam_pack_blocks / eegan_adam_range_blocks).  Bit-identical
+ * to eegan_adam followed by the pack. */
+long eegan_adam_pack_blocks(int Cout, int Cin, int R, int S);
+long eegan_adam_range_blocks(long len);
+int eegan_adam_pack(float* p, const float* g, float* m, float* v, float beta1, float beta2, float lr, float eps,
+                    float weight_decay, double* step, const long* table, int njobs, long total_blocks, hipStream_t s);
 
 #ifdef __cplusplus
 }

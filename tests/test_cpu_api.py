@@ -20,7 +20,7 @@ def test_library_exports_header_symbols():
         assert hasattr(_lib.LIB, name), name          # exported by libeegan_hip.so
         assert name in _lib._SIGS, name               # bound with a ctypes signature
     assert set(_lib._SIGS) == set(declared)
-    assert eegan_hip.ABI_VERSION == 16
+    assert eegan_hip.ABI_VERSION == 17
     # rows padded to 128; every tap's channel run padded to 32 (to 8 for <= 8
     # channels: 4 taps per K step), rows padded to whole 32-deep steps
     assert _lib.ops.conv_packed_elems(100, 3, 3, 3, 0) == 128 * 96

@@ -995,6 +995,44 @@ def test_flat_adam_repacks_conv_weights(gpu):
             assert torch.equal(buf, Fn.pack_weight(m.weight, tr))
 
 
+def test_flat_adam_fused_pack_bit_identical(gpu, monkeypatch):
+    """eegan_adam_pack (the Adam step fused with the conv weight re-pack, one
+    launch; optim.ADAM_PACK, default) against eegan_adam + the batched pack:
+    parameters, both Adam moments and every pack torch.equal after two steps
+    -- conv weights with 3 / 1 / 192 / 1024 channels (ragged 64-wide tiles,
+    Cgp 8 runs), 4x4 / 3x3 / 1x1 taps, biases and alignment gaps as range jobs."""
+    from eegan_hip import optim
+    Fn, T, Conv2d = _mods()
+    runs = []
+    for fused in (False, True):
+        torch.manual_seed(33)
+        mods = (Conv2d(3, 40, 3, 1, 1).to(gpu), Conv2d(40, 136, 4, 2, 1).to(gpu), Conv2d(136, 1, 1, 1, 0).to(gpu),
+                Conv2d(3, 192, 1, 1, 0).to(gpu), Conv2d(136, 1024, 3, 1, 1, bias=False).to(gpu))
+        extra = torch.nn.Parameter(torch.randn(7, device=gpu))    # a non-conv parameter (range job, gap after it)
+        opt = optim.FlatAdam([p for m in mods for p in m.parameters()] + [extra], lr=1e-2, betas=(0.0, 0.9))
+        monkeypatch.setattr(optim, 'ADAM_PACK', fused)
+        torch.manual_seed(34)
+        for _ in range(2):
+            opt.zero_grad()
+            x = _nhwc(_bf(torch.randn(2, 3, 8, 8)), gpu).requires_grad_()
+            h = mods[1](mods[0](x, act='lrelu'))
+            y = mods[2](h)
+            u = mods[3](x)
+            w = mods[4](h)
+            (y.float().sum() + u.float().sum() + w.float().square().mean() + (extra * extra).sum()).backward()
+            opt.step()
+        torch.cuda.synchronize()
+        runs.append((opt.flat.clone(), opt.m.clone(), opt.v.clone(),
+                     [(m._cache.fwd.clone(), m._cache.bwd.clone()) for m in mods]))
+        for m in mods:
+            for tr, buf in ((False, m._cache.fwd), (True, m._cache.bwd)):
+                assert torch.equal(buf, Fn.pack_weight(m.weight, tr)), (fused, tr, tuple(m.weight.shape))
+    (p0, m0, v0, k0), (p1, m1, v1, k1) = runs
+    assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
+    for (f0, b0), (f1, b1) in zip(k0, k1):
+        assert torch.equal(f0, f1) and torch.equal(b0, b1)
+
+
 @pytest.mark.parametrize('th', ['16', '8', '0'])
 def test_conv_halo3_matches_tile_kernel(gpu, monkeypatch, th):
     """3x3 / stride-1 convs on the LDS halo-tile kernel (conv_halo3_kernel,
