@@ -16,20 +16,24 @@ namespace {
 
 __global__ void adam_tick_kernel(double* step) { *step += 1.0; }
 
+// Every fused multiply-add is spelled out and contraction is off: left to
+// -ffp-contract the compiler fused different products in different kernels
+// (adam_kernel / adam_pack_kernel), which then disagreed in the last bit.
 template <bool B1ZERO>
 __device__ __forceinline__ void adam_elem(float& P, float G, float& M, float& V, float b1, float b2, float wd,
                                           float step_size, float bc2_sqrt, float eps) {
-  const float gr = G + wd * P;
+#pragma clang fp contract(off)
+  const float gr = __builtin_fmaf(wd, P, G);
   // torch: exp_avg.lerp_(g, 1 - b1); at b1 = 0 (train.py:252-263's betas) the
   // lerp with weight 1 is g - (g - m) * 0 = g exactly for any finite m, so
   // the old moment is not read
   if (B1ZERO)
     M = gr;
   else
-    M = (1.f - b1) >= 0.5f ? gr - (gr - M) * b1 : M + (1.f - b1) * (gr - M);
-  V = V * b2 + (1.f - b2) * gr * gr;
+    M = (1.f - b1) >= 0.5f ? __builtin_fmaf(-(gr - M), b1, gr) : __builtin_fmaf(1.f - b1, gr - M, M);
+  V = __builtin_fmaf(V, b2, ((1.f - b2) * gr) * gr);
   const float denom = sqrtf(V) / bc2_sqrt + eps;
-  P = P + (-step_size) * (M / denom);
+  P = __builtin_fmaf(-step_size, M / denom, P);
 }
 
 template <bool B1ZERO>
