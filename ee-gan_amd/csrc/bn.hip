@@ -8,6 +8,9 @@
 //
 // Layout: x NHWC bf16 [N][H][W][ld]; statistics fp32; per-(sample,channel)
 // modulation gamma/beta fp32 [N][C]; spatial mask fp32 [N][Ho*Wo].
+#include <stdlib.h>
+#include <string.h>
+
 #include "common.h"
 #include "../../include/eegan_hip.h"
 
@@ -657,6 +660,20 @@ ModArgs make_args(const eegan_bnmod_desc* d) {
   return a;
 }
 
+// Grid knobs for sweeps (tools/bn_bench.py): EEGAN_BN="fwd_target=1536,dx_target=2048,
+// bwd_target=1024,bwd_minpix=64,stats_blocks=1024" (unset keys keep these defaults).
+static int bn_knob(const char* key, int dflt) {
+  const char* v = getenv("EEGAN_BN");
+  if (!v) return dflt;
+  const size_t n = strlen(key);
+  for (const char* p = v; p && *p;) {
+    if (!strncmp(p, key, n) && p[n] == '=') return atoi(p + n + 1);
+    p = strchr(p, ',');
+    if (p) ++p;
+  }
+  return dflt;
+}
+
 // chunks of a per-sample pixel range: ~`target` blocks overall (whole rounds of
 // resident blocks: the forward holds 6 blocks per CU -> 1536, the dx pass 4 ->
 // 2048 = two rounds), >= 8 pixel rows per block
@@ -689,7 +706,8 @@ bool vec_ok(const eegan_bnmod_desc* d, int ld, const void* p, const char* what) 
 int bwd_chunks(const eegan_bnmod_desc* d, int& ppc) {
   const long HWo = (long)(d->H << d->up2) * (d->W << d->up2);
   // aim at ~1024 blocks overall, >= 64 pixels each
-  int chunks = std::max(1, std::min<int>(ee_cdiv(HWo, 64), ee_cdiv(1024, d->N)));
+  int chunks = std::max(1, std::min<int>(ee_cdiv(HWo, bn_knob("bwd_minpix", 64)),
+                                         ee_cdiv(bn_knob("bwd_target", 1024), d->N)));
   ppc = ee_cdiv(HWo, chunks);
   chunks = ee_cdiv(HWo, ppc);
   return chunks;
@@ -702,7 +720,8 @@ extern "C" {
 long eegan_bn_stats_workspace(long P, int C) {
   const int C8 = (C + 7) / 8;
   const int rows = NT / C8;
-  long rpb = std::max<long>(rows * 16, (P + 1023) / 1024);
+  const long sb = bn_knob("stats_blocks", 1024);
+  long rpb = std::max<long>(rows * 16, (P + sb - 1) / sb);
   const long nblk = (P + rpb - 1) / rpb;
   return nblk * 2 * C * (long)sizeof(float);
 }
@@ -714,7 +733,8 @@ int eegan_bn_stats(const uint16_t* x, long P, int C, int ld, float* ws, double* 
     return -22;
   }
   const int rows = NT / C8;
-  long rpb = std::max<long>(rows * 16, (P + 1023) / 1024);
+  const long sb = bn_knob("stats_blocks", 1024);
+  long rpb = std::max<long>(rows * 16, (P + sb - 1) / sb);
   const int nblk = (int)std::max<long>(1, (P + rpb - 1) / rpb);
   const size_t shm = 2 * rows * C8 * 8 * sizeof(float);
   bn_partial_kernel<<<nblk, NT, shm, stream>>>(x, P, C, ld, rpb, ws);
@@ -735,7 +755,8 @@ int eegan_bnmod_fwd(const eegan_bnmod_desc* d, uint16_t* y, int ldy, hipStream_t
   ModArgs a = make_args(d);
   if (!vec_ok(d, ldy, y, "bnmod_fwd")) return -22;
   int ppc;
-  const int chunks = pix_chunks(d->N, (long)(d->H << d->up2) * (d->W << d->up2), d->C, ppc, 1536);
+  const int chunks = pix_chunks(d->N, (long)(d->H << d->up2) * (d->W << d->up2), d->C, ppc,
+                                bn_knob("fwd_target", 1536));
   bnmod_fwd_kernel<false><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, FinArgs{});
   return ee_check_launch("bnmod_fwd");
 }
@@ -750,7 +771,8 @@ int eegan_bnmod_fwd_fin(const eegan_bnmod_desc* d, const double* sums, double co
     return -22;
   }
   int ppc;
-  const int chunks = pix_chunks(d->N, (long)(d->H << d->up2) * (d->W << d->up2), d->C, ppc, 1536);
+  const int chunks = pix_chunks(d->N, (long)(d->H << d->up2) * (d->W << d->up2), d->C, ppc,
+                                bn_knob("fwd_target", 1536));
   const FinArgs f{sums, count, sum_scale, eps, momentum, clamp_mode, running_mean, running_var,
                   const_cast<float*>(d->stats)};
   bnmod_fwd_kernel<true><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, f);
@@ -795,7 +817,7 @@ int eegan_bnmod_bwd_dx(const eegan_bnmod_desc* d, const uint16_t* dt, int lddt, 
   ModArgs a = make_args(d);
   if (!vec_ok(d, lddt, dt, "bnmod_bwd_dx") || !vec_ok(d, lddx, dx, "bnmod_bwd_dx")) return -22;
   int ppc;
-  const int chunks = pix_chunks(d->N, (long)d->H * d->W, d->C, ppc);
+  const int chunks = pix_chunks(d->N, (long)d->H * d->W, d->C, ppc, bn_knob("dx_target", 2048));
   bnmod_bwd_dx_kernel<<<dim3(chunks, d->N), NT, 0, stream>>>(a, dt, lddt, chan, count, dx, lddx, ppc);
   return ee_check_launch("bnmod_bwd_dx");
 }

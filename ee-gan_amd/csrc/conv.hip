@@ -868,9 +868,13 @@ EE_DEV void splitk_fused_finish(const ConvArgs& a, const f32x4_t (&acc)[FI][FJ],
   __syncthreads();
   if (tid == 0) {
     int* c = a.ctr + tile;
-    // release: this block's partial tile is visible device-wide before its ticket;
-    // acquire: the last arriver sees every other split's partial (across XCD L2s)
-    const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    // The partials were stored with sc1 (written through to memory, not parked in this
+    // XCD's L2) and every wave waited for them (vmcnt(0) + barrier) before this ticket,
+    // and the last arriver reads them back with sc1 loads: the hand-off of
+    // cdna_hip_programming.md §6 Guideline 16 (sc1 form), which needs no release /
+    // acquire fence -- an agent-scope acq_rel here writes back and invalidates the
+    // whole XCD L2 per block (3-8x slower).
+    const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = old == a.nsplit - 1;
     if (old == a.nsplit - 1) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
