@@ -660,8 +660,9 @@ ModArgs make_args(const eegan_bnmod_desc* d) {
   return a;
 }
 
-// Grid knobs for sweeps (tools/bn_bench.py): EEGAN_BN="fwd_target=1536,dx_target=2048,
-// bwd_target=1024,bwd_minpix=64,stats_blocks=1024" (unset keys keep these defaults).
+// Grid knobs for sweeps (tools/bn_bench.py): EEGAN_BN="fwd_target=1536,fwd_prow=8,
+// dx_target=2048,dx_prow=8,bwd_target=1024,bwd_minpix=64,stats_blocks=1024" (unset keys
+// keep these defaults; *_prow: the fewest pixel rows a block walks).
 static int bn_knob(const char* key, int dflt) {
   const char* v = getenv("EEGAN_BN");
   if (!v) return dflt;
@@ -677,9 +678,9 @@ static int bn_knob(const char* key, int dflt) {
 // chunks of a per-sample pixel range: ~`target` blocks overall (whole rounds of
 // resident blocks: the forward holds 6 blocks per CU -> 1536, the dx pass 4 ->
 // 2048 = two rounds), >= 8 pixel rows per block
-int pix_chunks(int N, long HW, int C, int& ppc, int target = 2048) {
+int pix_chunks(int N, long HW, int C, int& ppc, int target = 2048, int prow = 8) {
   const int rows = NT / ((C + 7) / 8);
-  ppc = (int)std::max<long>((long)rows * 8, (HW * N + target - 1) / target);
+  ppc = (int)std::max<long>((long)rows * prow, (HW * N + target - 1) / target);
   return std::max(1, ee_cdiv(HW, ppc));
 }
 
@@ -756,7 +757,7 @@ int eegan_bnmod_fwd(const eegan_bnmod_desc* d, uint16_t* y, int ldy, hipStream_t
   if (!vec_ok(d, ldy, y, "bnmod_fwd")) return -22;
   int ppc;
   const int chunks = pix_chunks(d->N, (long)(d->H << d->up2) * (d->W << d->up2), d->C, ppc,
-                                bn_knob("fwd_target", 1536));
+                                bn_knob("fwd_target", 1536), bn_knob("fwd_prow", 8));
   bnmod_fwd_kernel<false><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, FinArgs{});
   return ee_check_launch("bnmod_fwd");
 }
@@ -772,7 +773,7 @@ int eegan_bnmod_fwd_fin(const eegan_bnmod_desc* d, const double* sums, double co
   }
   int ppc;
   const int chunks = pix_chunks(d->N, (long)(d->H << d->up2) * (d->W << d->up2), d->C, ppc,
-                                bn_knob("fwd_target", 1536));
+                                bn_knob("fwd_target", 1536), bn_knob("fwd_prow", 8));
   const FinArgs f{sums, count, sum_scale, eps, momentum, clamp_mode, running_mean, running_var,
                   const_cast<float*>(d->stats)};
   bnmod_fwd_kernel<true><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, f);
@@ -817,7 +818,8 @@ int eegan_bnmod_bwd_dx(const eegan_bnmod_desc* d, const uint16_t* dt, int lddt, 
   ModArgs a = make_args(d);
   if (!vec_ok(d, lddt, dt, "bnmod_bwd_dx") || !vec_ok(d, lddx, dx, "bnmod_bwd_dx")) return -22;
   int ppc;
-  const int chunks = pix_chunks(d->N, (long)d->H * d->W, d->C, ppc, bn_knob("dx_target", 2048));
+  const int chunks = pix_chunks(d->N, (long)d->H * d->W, d->C, ppc, bn_knob("dx_target", 2048),
+                                bn_knob("dx_prow", 8));
   bnmod_bwd_dx_kernel<<<dim3(chunks, d->N), NT, 0, stream>>>(a, dt, lddt, chan, count, dx, lddx, ppc);
   return ee_check_launch("bnmod_bwd_dx");
 }
