@@ -20,6 +20,7 @@ constexpr int NT = 256;
 
 // ------------------------------------------------------------- statistics --
 // per-block partial (sum, sumsq) per channel -> ws[block][2][C]
+template <int SU = 4>   // pixels' loads in flight per thread (summed in pixel order for any count)
 __global__ __launch_bounds__(NT) void bn_partial_kernel(const bf16_t* __restrict__ x, long P, int C, int ld,
                                                         long rows_per_block, float* __restrict__ ws) {
   extern __shared__ float sh[];  // [rows][C8*8] x2
@@ -38,7 +39,6 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(const bf16_t* __restrict
     long p = p0 + row;
     if (vec) {
       // SU pixels' loads in flight per thread, summed in pixel order (as one at a time)
-      constexpr int SU = 4;
       for (; p < p1; p += SU * rows) {
         uint4 v[SU];
 #pragma unroll
@@ -257,12 +257,12 @@ EE_DEV int in_pix(const ModArgs& a, int q, int Wo) {
 // grid (chunks, N): output pixels [chunk*ppc, ...) of sample n.  FUNR pixels
 // per thread per iteration: their loads are all issued before any arithmetic
 // (a single 16-byte load per iteration left these kernels latency-bound).
-constexpr int FUNR = 2;
+constexpr int FUNR_DEFAULT = 2;
 
 // FIN: the statistics come from the sums (the finalize kernel folded in: every block
 // recomputes its channels' mean / inv_std, block (0, 0) also writes stats[] and the
 // running statistics -- one launch less per BN call on the generator's serial chain)
-template <bool FIN>
+template <bool FIN, int FUNR = FUNR_DEFAULT>
 __global__ __launch_bounds__(NT, 6) void bnmod_fwd_kernel(ModArgs a, bf16_t* __restrict__ y, int ldy, int ppc,
                                                        FinArgs fin) {
   if (FIN && blockIdx.x == 0 && blockIdx.y == 0) {
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(NT, 6) void bnmod_fwd_kernel(ModArgs a, bf16_t* __r
 }
 
 // ------------------------------------------------------ backward, pass 1 --
-constexpr int RU = 2;
+constexpr int RU_DEFAULT = 2;
 
 // sum of v over the C8 consecutive lanes that hold one pixel's channel groups
 // (C8 a power of two <= 64; every lane of the group gets the same bits, summed
@@ -345,6 +345,7 @@ EE_DEV float group_sum(float v, int c8) {
 // (affine: S0 = D, S1 = G, S2 = pm*G, S3 = pm*D) -- dxhat = g*(pm*m + 1).
 // RU pixels' loads per thread are issued before their arithmetic; at <= 128
 // VGPRs four blocks fit a CU, so the ~1024-block grid runs in one round.
+template <int RU = RU_DEFAULT>
 __global__ __launch_bounds__(NT, 4) void bnmod_bwd_reduce_kernel(ModArgs a, const bf16_t* __restrict__ dt, int lddt,
                                                               int pix_per_chunk, float* __restrict__ ws,
                                                               float* __restrict__ dmask) {
@@ -614,6 +615,7 @@ EE_DEV void bwd_dx_body(const ModArgs& a, const bf16_t* __restrict__ dt, int ldd
   }
 }
 
+template <int DXU1 = 4>
 __global__ __launch_bounds__(NT) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_t* __restrict__ dt, int lddt,
                                                           const double* __restrict__ chan, double count,
                                                           bf16_t* __restrict__ dx, int lddx, int ppc) {
@@ -632,8 +634,8 @@ __global__ __launch_bounds__(NT) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_
     m1[j] = (float)(chan[c] / count);
     m2[j] = (float)(chan[a.C + c] / count);
   }
-  if (a.up2) bwd_dx_body<2, 4>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
-  else bwd_dx_body<4, 1>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
+  if (a.up2) bwd_dx_body<DXU1 / 2, 4>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
+  else bwd_dx_body<DXU1, 1>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
 }
 
 ModArgs make_args(const eegan_bnmod_desc* d) {
@@ -662,7 +664,8 @@ ModArgs make_args(const eegan_bnmod_desc* d) {
 
 // Grid knobs for sweeps (tools/bn_bench.py): EEGAN_BN="fwd_target=1536,fwd_prow=8,
 // dx_target=2048,dx_prow=8,bwd_target=1024,bwd_minpix=64,stats_blocks=1024" (unset keys
-// keep these defaults; *_prow: the fewest pixel rows a block walks).
+// keep these defaults; *_prow: the fewest pixel rows a block walks) and the pixels a
+// thread keeps in flight: fwd_u (2 | 4), red_u (2 | 4), dx_u (4 | 8), stats_u (4 | 8).
 static int bn_knob(const char* key, int dflt) {
   const char* v = getenv("EEGAN_BN");
   if (!v) return dflt;
@@ -738,7 +741,10 @@ int eegan_bn_stats(const uint16_t* x, long P, int C, int ld, float* ws, double* 
   long rpb = std::max<long>(rows * 16, (P + sb - 1) / sb);
   const int nblk = (int)std::max<long>(1, (P + rpb - 1) / rpb);
   const size_t shm = 2 * rows * C8 * 8 * sizeof(float);
-  bn_partial_kernel<<<nblk, NT, shm, stream>>>(x, P, C, ld, rpb, ws);
+  if (bn_knob("stats_u", 4) >= 8)
+    bn_partial_kernel<8><<<nblk, NT, shm, stream>>>(x, P, C, ld, rpb, ws);
+  else
+    bn_partial_kernel<><<<nblk, NT, shm, stream>>>(x, P, C, ld, rpb, ws);
   int rc = ee_check_launch("bn_partial");
   if (rc) return rc;
   launch_colsum<double, double>(ws, nblk, 2 * C, 2 * C, 0, sums, 0, 1, 0, stream);
@@ -758,7 +764,11 @@ int eegan_bnmod_fwd(const eegan_bnmod_desc* d, uint16_t* y, int ldy, hipStream_t
   int ppc;
   const int chunks = pix_chunks(d->N, (long)(d->H << d->up2) * (d->W << d->up2), d->C, ppc,
                                 bn_knob("fwd_target", 1536), bn_knob("fwd_prow", 8));
-  bnmod_fwd_kernel<false><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, FinArgs{});
+  // pixels whose loads a thread issues before their arithmetic (same results for any count)
+  if (bn_knob("fwd_u", FUNR_DEFAULT) >= 4)
+    bnmod_fwd_kernel<false, 4><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, FinArgs{});
+  else
+    bnmod_fwd_kernel<false><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, FinArgs{});
   return ee_check_launch("bnmod_fwd");
 }
 
@@ -776,7 +786,10 @@ int eegan_bnmod_fwd_fin(const eegan_bnmod_desc* d, const double* sums, double co
                                 bn_knob("fwd_target", 1536), bn_knob("fwd_prow", 8));
   const FinArgs f{sums, count, sum_scale, eps, momentum, clamp_mode, running_mean, running_var,
                   const_cast<float*>(d->stats)};
-  bnmod_fwd_kernel<true><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, f);
+  if (bn_knob("fwd_u", FUNR_DEFAULT) >= 4)
+    bnmod_fwd_kernel<true, 4><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, f);
+  else
+    bnmod_fwd_kernel<true><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, f);
   return ee_check_launch("bnmod_fwd_fin");
 }
 
@@ -801,7 +814,12 @@ int eegan_bnmod_bwd(const eegan_bnmod_desc* d, const uint16_t* dt, int lddt, flo
   const int rows = NT / C8;
   const size_t shm = (rows * C8 + rows * (4 * C8 * 8 + 1)) * sizeof(float);
   dim3 grid(chunks, d->N);
-  bnmod_bwd_reduce_kernel<<<grid, NT, shm, stream>>>(a, dt, lddt, ppc, ws, dmask);
+  // pixels per thread with their loads in flight together; the per-thread pixel order, hence
+  // every partial sum, is the same for any count
+  if (bn_knob("red_u", RU_DEFAULT) >= 4)
+    bnmod_bwd_reduce_kernel<4><<<grid, NT, shm, stream>>>(a, dt, lddt, ppc, ws, dmask);
+  else
+    bnmod_bwd_reduce_kernel<><<<grid, NT, shm, stream>>>(a, dt, lddt, ppc, ws, dmask);
   int rc = ee_check_launch("bnmod_bwd_reduce");
   if (rc) return rc;
   double* tmp = reinterpret_cast<double*>(ws + (long)d->N * chunks * 4 * d->C);
@@ -820,7 +838,10 @@ int eegan_bnmod_bwd_dx(const eegan_bnmod_desc* d, const uint16_t* dt, int lddt, 
   int ppc;
   const int chunks = pix_chunks(d->N, (long)d->H * d->W, d->C, ppc, bn_knob("dx_target", 2048),
                                 bn_knob("dx_prow", 8));
-  bnmod_bwd_dx_kernel<<<dim3(chunks, d->N), NT, 0, stream>>>(a, dt, lddt, chan, count, dx, lddx, ppc);
+  if (bn_knob("dx_u", 4) >= 8)
+    bnmod_bwd_dx_kernel<8><<<dim3(chunks, d->N), NT, 0, stream>>>(a, dt, lddt, chan, count, dx, lddx, ppc);
+  else
+    bnmod_bwd_dx_kernel<><<<dim3(chunks, d->N), NT, 0, stream>>>(a, dt, lddt, chan, count, dx, lddx, ppc);
   return ee_check_launch("bnmod_bwd_dx");
 }
 
