@@ -348,7 +348,9 @@ EE_DEV float group_sum(float v, int c8) {
 template <int RU = RU_DEFAULT>
 __global__ __launch_bounds__(NT, 4) void bnmod_bwd_reduce_kernel(ModArgs a, const bf16_t* __restrict__ dt, int lddt,
                                                               int pix_per_chunk, float* __restrict__ ws,
-                                                              float* __restrict__ dmask) {
+                                                              float* __restrict__ dmask, int knock) {
+  // knock (diagnostic knock-outs, EEGAN_BN knock=bits; results wrong): 1 no pixel loads,
+  // 2 no cross-row tail (zeros written), 4 no channel-parameter loads
   extern __shared__ float sh[];
   const int C = a.C;
   const int C8 = (C + 7) / 8;
@@ -370,7 +372,11 @@ __global__ __launch_bounds__(NT, 4) void bnmod_bwd_reduce_kernel(ModArgs a, cons
   float* red = sh;                 // [rows][C8] for dmask
   ChanParams P;
   const bool live = row < rows;
-  if (live) load_params(a, n, c0, P);
+  if (live && !(knock & 4)) load_params(a, n, c0, P);
+  if (knock & 4) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) P.mean[k] = P.pm[k] = P.pa[k] = splat2(0.f), P.istd[k] = splat2(1.f);
+  }
   // a pixel's C8 channel groups are C8 consecutive lanes of one wave when C8 is a
   // power of two <= 64: its dmask is then a DPP / shuffle reduction (no barriers)
   const bool wave_red = (C8 & (C8 - 1)) == 0 && C8 <= 64;
@@ -386,9 +392,14 @@ __global__ __launch_bounds__(NT, 4) void bnmod_bwd_reduce_kernel(ModArgs a, cons
     for (int u = 0; u < RU; ++u) {
       const int q = qb + u * rows + row;
       if (live && q < q1) {
-        xc[u] = *reinterpret_cast<const uint4*>(xs + (unsigned)in_pix(a, q, Wo) * (unsigned)a.ldx);
-        gc[u] = *reinterpret_cast<const uint4*>(gs + (unsigned)q * (unsigned)lddt);
-        mc[u] = ssa ? ms[q] : 0.f;
+        if (knock & 1) {
+          xc[u] = gc[u] = make_uint4(0x3f803f80u, 0, 0, 0);
+          mc[u] = 0.5f;
+        } else {
+          xc[u] = *reinterpret_cast<const uint4*>(xs + (unsigned)in_pix(a, q, Wo) * (unsigned)a.ldx);
+          gc[u] = *reinterpret_cast<const uint4*>(gs + (unsigned)q * (unsigned)lddt);
+          mc[u] = ssa ? ms[q] : 0.f;
+        }
       }
     }
 #pragma unroll
@@ -446,6 +457,12 @@ __global__ __launch_bounds__(NT, 4) void bnmod_bwd_reduce_kernel(ModArgs a, cons
   // output sums the rows in order and forms S0..S3.
   float* sacc = sh + rows * C8;  // [rows][4 * W8 + 1]
   const int W8 = C8 * 8, RS = 4 * W8 + 1;
+  if (knock & 2) {
+    float* out = ws + ((long)n * gridDim.x + blockIdx.x) * 4 * C;
+    const float z = acc[0][0].x + acc[3][3].y;   // keep the loop live
+    for (int c = t; c < 4 * C; c += NT) out[c] = z;
+    return;
+  }
   if (live) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -817,9 +834,9 @@ int eegan_bnmod_bwd(const eegan_bnmod_desc* d, const uint16_t* dt, int lddt, flo
   // pixels per thread with their loads in flight together; the per-thread pixel order, hence
   // every partial sum, is the same for any count
   if (bn_knob("red_u", RU_DEFAULT) >= 4)
-    bnmod_bwd_reduce_kernel<4><<<grid, NT, shm, stream>>>(a, dt, lddt, ppc, ws, dmask);
+    bnmod_bwd_reduce_kernel<4><<<grid, NT, shm, stream>>>(a, dt, lddt, ppc, ws, dmask, bn_knob("knock", 0));
   else
-    bnmod_bwd_reduce_kernel<><<<grid, NT, shm, stream>>>(a, dt, lddt, ppc, ws, dmask);
+    bnmod_bwd_reduce_kernel<><<<grid, NT, shm, stream>>>(a, dt, lddt, ppc, ws, dmask, bn_knob("knock", 0));
   int rc = ee_check_launch("bnmod_bwd_reduce");
   if (rc) return rc;
   double* tmp = reinterpret_cast<double*>(ws + (long)d->N * chunks * 4 * d->C);
