@@ -180,29 +180,50 @@ struct ChanParams {
 
 EE_DEV f2_t splat2(float v) { return f2_t{v, v}; }
 
-EE_DEV void load_params(const ModArgs& a, int n, int c0, ChanParams& q, const FinArgs* fin = nullptr) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = min(c0 + j, a.C - 1);
-    float mean, istd, pm, pa;
-    if (fin) {   // statistics straight from the sums (the forward's fused finalize)
-      bn_finalize_channel(*fin, a.C, c, mean, istd, false);
+// The block's channel parameters are staged once through LDS: prm[4][W8] = mean,
+// istd, pm, pa (mode 0: w, b; mode 1: gam[n], bet[n]) for channels 0..W8 (those
+// >= C repeat channel C-1).  Loading them per thread (8 channels x 4 values,
+// every thread of every block on the same few hundred bytes) cost as much as
+// the pixel loads on the small-image layers.  FIN: mean / istd straight from
+// the sums (the forward's fused finalize); `commit` also writes stats[] and
+// the running statistics (block (0, 0) only).
+EE_DEV void stage_params(const ModArgs& a, int n, float* prm, int W8, const FinArgs* fin = nullptr,
+                         bool commit = false) {
+  for (int c = threadIdx.x; c < W8; c += NT) {
+    const int cc = min(c, a.C - 1);
+    float mean, istd;
+    if (fin) {
+      bn_finalize_channel(*fin, a.C, cc, mean, istd, commit && c < a.C);
     } else {
-      mean = a.stats[c];
-      istd = a.stats[a.C + c];
+      mean = a.stats[cc];
+      istd = a.stats[a.C + cc];
     }
+    prm[c] = mean;
+    prm[W8 + c] = istd;
     if (a.mode == 0) {
-      pm = a.w ? a.w[c] : 1.f;
-      pa = a.b ? a.b[c] : 0.f;
+      prm[2 * W8 + c] = a.w ? a.w[cc] : 1.f;
+      prm[3 * W8 + c] = a.b ? a.b[cc] : 0.f;
     } else {
-      pm = a.gam[(long)n * a.C + c];
-      pa = a.bet[(long)n * a.C + c];
+      prm[2 * W8 + c] = a.gam[(long)n * a.C + cc];
+      prm[3 * W8 + c] = a.bet[(long)n * a.C + cc];
     }
-    q.mean[j >> 1][j & 1] = mean;
-    q.istd[j >> 1][j & 1] = istd;
-    q.pm[j >> 1][j & 1] = pm;
-    q.pa[j >> 1][j & 1] = pa;
   }
+}
+
+EE_DEV void lds8(const float* p, f2_t (&d)[4]) {
+  const float4 lo = *reinterpret_cast<const float4*>(p), hi = *reinterpret_cast<const float4*>(p + 4);
+  d[0] = f2_t{lo.x, lo.y};
+  d[1] = f2_t{lo.z, lo.w};
+  d[2] = f2_t{hi.x, hi.y};
+  d[3] = f2_t{hi.z, hi.w};
+}
+
+// a thread's 8 channels c0.. from the staged table
+EE_DEV void load_params(const float* prm, int W8, int c0, ChanParams& q) {
+  lds8(prm + c0, q.mean);
+  lds8(prm + W8 + c0, q.istd);
+  lds8(prm + 2 * W8 + c0, q.pm);
+  lds8(prm + 3 * W8 + c0, q.pa);
 }
 
 EE_DEV void unpack8(uint4 v, f2_t (&f)[4]) {
@@ -260,18 +281,16 @@ EE_DEV int in_pix(const ModArgs& a, int q, int Wo) {
 constexpr int FUNR_DEFAULT = 2;
 
 // FIN: the statistics come from the sums (the finalize kernel folded in: every block
-// recomputes its channels' mean / inv_std, block (0, 0) also writes stats[] and the
-// running statistics -- one launch less per BN call on the generator's serial chain)
+// recomputes its channels' mean / inv_std while staging them, block (0, 0) also writes
+// stats[] and the running statistics -- one launch less per BN call on the generator's
+// serial chain).  Dynamic LDS: 4 * W8 floats (stage_params).
 template <bool FIN, int FUNR = FUNR_DEFAULT>
 __global__ __launch_bounds__(NT, 6) void bnmod_fwd_kernel(ModArgs a, bf16_t* __restrict__ y, int ldy, int ppc,
                                                        FinArgs fin) {
-  if (FIN && blockIdx.x == 0 && blockIdx.y == 0) {
-    for (int c = threadIdx.x; c < a.C; c += NT) {
-      float m, i;
-      bn_finalize_channel(fin, a.C, c, m, i, true);
-    }
-  }
-  const int C8 = (a.C + 7) / 8, rows = NT / C8;
+  extern __shared__ float prm[];  // [4][W8]
+  const int C8 = (a.C + 7) / 8, rows = NT / C8, W8 = C8 * 8;
+  stage_params(a, blockIdx.y, prm, W8, FIN ? &fin : nullptr, FIN && blockIdx.x == 0 && blockIdx.y == 0);
+  __syncthreads();
   const int row = threadIdx.x / C8, cg = threadIdx.x - row * C8;
   if (row >= rows) return;
   const int n = blockIdx.y, c0 = cg * 8, nv = a.C - c0;
@@ -279,7 +298,7 @@ __global__ __launch_bounds__(NT, 6) void bnmod_fwd_kernel(ModArgs a, bf16_t* __r
   const int HWo = Ho * Wo;  // per-sample pixel counts fit 32 bits
   const int q1 = min(HWo, ((int)blockIdx.x + 1) * ppc);
   ChanParams P;
-  load_params(a, n, c0, P, FIN ? &fin : nullptr);
+  load_params(prm, W8, c0, P);
   const bf16_t* xs = a.x + (unsigned)(n * a.H * a.W) * (unsigned)a.ldx + c0;
   bf16_t* ys = y + (unsigned)(n * HWo) * (unsigned)ldy + c0;
   const float* ms = a.mask + (long)n * HWo;
@@ -350,7 +369,7 @@ __global__ __launch_bounds__(NT, 4) void bnmod_bwd_reduce_kernel(ModArgs a, cons
                                                               int pix_per_chunk, float* __restrict__ ws,
                                                               float* __restrict__ dmask, int knock) {
   // knock (diagnostic knock-outs, EEGAN_BN knock=bits; results wrong): 1 no pixel loads,
-  // 2 no cross-row tail (zeros written), 4 no channel-parameter loads
+  // 2 no cross-row tail (zeros written), 4 no channel parameters (constants)
   extern __shared__ float sh[];
   const int C = a.C;
   const int C8 = (C + 7) / 8;
@@ -369,10 +388,15 @@ __global__ __launch_bounds__(NT, 4) void bnmod_bwd_reduce_kernel(ModArgs a, cons
 #pragma unroll
     for (int k = 0; k < 4; ++k) acc[i][k] = splat2(0.f);
   const int c0 = cg * 8, nv = C - c0;
-  float* red = sh;                 // [rows][C8] for dmask
+  const int W8 = C8 * 8, RS = 4 * W8 + 1;
+  float* prm = sh;                 // [4][W8] channel parameters (stage_params)
+  float* red = sh + 4 * W8;        // [rows][C8] for dmask
+  float* sacc = red + rows * C8;   // [rows][RS] row partials
   ChanParams P;
   const bool live = row < rows;
-  if (live && !(knock & 4)) load_params(a, n, c0, P);
+  if (!(knock & 4)) stage_params(a, n, prm, W8);
+  __syncthreads();
+  if (live && !(knock & 4)) load_params(prm, W8, c0, P);
   if (knock & 4) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) P.mean[k] = P.pm[k] = P.pa[k] = splat2(0.f), P.istd[k] = splat2(1.f);
@@ -455,8 +479,6 @@ __global__ __launch_bounds__(NT, 4) void bnmod_bwd_reduce_kernel(ModArgs a, cons
   // reduce acc over rows -> ws: every row's partials through LDS (a row stride of
   // 4 * W8 + 1 floats spreads a wave's rows over the banks), then one thread per
   // output sums the rows in order and forms S0..S3.
-  float* sacc = sh + rows * C8;  // [rows][4 * W8 + 1]
-  const int W8 = C8 * 8, RS = 4 * W8 + 1;
   if (knock & 2) {
     float* out = ws + ((long)n * gridDim.x + blockIdx.x) * 4 * C;
     const float z = acc[0][0].x + acc[3][3].y;   // keep the loop live
@@ -476,7 +498,7 @@ __global__ __launch_bounds__(NT, 4) void bnmod_bwd_reduce_kernel(ModArgs a, cons
     for (int r = 0; r < rows; ++r)
 #pragma unroll
       for (int i = 0; i < 4; ++i) s[i] += sacc[r * RS + i * W8 + c];
-    const float pm = ssa ? a.gam[(long)n * C + c] : (a.w ? a.w[c] : 1.f);
+    const float pm = knock & 4 ? 0.f : prm[2 * W8 + c];
     if (ssa) {
       out[c] = s[0];
       out[C + c] = s[1];
@@ -500,12 +522,19 @@ __global__ void bnmod_bwd_sums_kernel(const double* __restrict__ tmp, int N, int
   if (j >= 4 * C) return;
   const int i = j / C, c = j - i * C;
   double s = 0;
-  for (int n = 0; n < N; ++n) {
-    const double v = tmp[(long)n * 4 * C + j];
-    s += v;
-    if (mode == 1 && i < 2) {
-      float* d = i == 0 ? d0 : d1;
-      if (d) d[(long)n * C + c] = (float)v;
+  // 16 samples' loads in flight before their sums (the sums stay in sample order)
+  for (int n0 = 0; n0 < N; n0 += 16) {
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = tmp[(long)min(n0 + u, N - 1) * 4 * C + j];   // unconditional loads
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (n0 + u >= N) break;
+      s += v[u];
+      if (mode == 1 && i < 2) {
+        float* d = i == 0 ? d0 : d1;
+        if (d) d[(long)(n0 + u) * C + c] = (float)v[u];
+      }
     }
   }
   if (i >= 2) chan[(i - 2) * C + c] = s;
@@ -526,20 +555,9 @@ struct ChanParamsS {
   float mean[8], istd[8], pm[8], pa[8];  // mode 0: w, b ; mode 1: gam[n], bet[n]
 };
 
-EE_DEV void load_params_s(const ModArgs& a, int n, int c0, ChanParamsS& q) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = min(c0 + j, a.C - 1);
-    q.mean[j] = a.stats[c];
-    q.istd[j] = a.stats[a.C + c];
-    if (a.mode == 0) {
-      q.pm[j] = a.w ? a.w[c] : 1.f;
-      q.pa[j] = a.b ? a.b[c] : 0.f;
-    } else {
-      q.pm[j] = a.gam[(long)n * a.C + c];
-      q.pa[j] = a.bet[(long)n * a.C + c];
-    }
-  }
+EE_DEV void lds8_s(const float* p, float (&d)[8]) {
+  const float4 lo = *reinterpret_cast<const float4*>(p), hi = *reinterpret_cast<const float4*>(p + 4);
+  d[0] = lo.x, d[1] = lo.y, d[2] = lo.z, d[3] = lo.w, d[4] = hi.x, d[5] = hi.y, d[6] = hi.z, d[7] = hi.w;
 }
 
 EE_DEV void coeffs_s(const ModArgs& a, const ChanParamsS& q, int j, float m, float& mul, float& add) {
@@ -636,21 +654,30 @@ template <int DXU1 = 4>
 __global__ __launch_bounds__(NT) void bnmod_bwd_dx_kernel(ModArgs a, const bf16_t* __restrict__ dt, int lddt,
                                                           const double* __restrict__ chan, double count,
                                                           bf16_t* __restrict__ dx, int lddx, int ppc) {
-  const int C8 = (a.C + 7) / 8, rows = NT / C8;
+  // dynamic LDS [7][W8]: stage_params' four rows, then vg, mean(dxhat), mean(dxhat*xhat)
+  extern __shared__ float prm[];
+  const int C8 = (a.C + 7) / 8, rows = NT / C8, W8 = C8 * 8;
+  stage_params(a, blockIdx.y, prm, W8);
+  for (int c = threadIdx.x; c < W8; c += NT) {
+    const int cc = min(c, a.C - 1);
+    prm[4 * W8 + c] = a.stats[2 * a.C + cc];
+    prm[5 * W8 + c] = (float)(chan[cc] / count);
+    prm[6 * W8 + c] = (float)(chan[a.C + cc] / count);
+  }
+  __syncthreads();
   const int row = threadIdx.x / C8, cg = threadIdx.x - row * C8;
   if (row >= rows) return;
   const int n = blockIdx.y, c0 = cg * 8, nv = a.C - c0;
   const int q1 = min(a.H * a.W, ((int)blockIdx.x + 1) * ppc);
   ChanParamsS P;
-  load_params_s(a, n, c0, P);
   float vg[8], m1[8], m2[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = min(c0 + j, a.C - 1);
-    vg[j] = a.stats[2 * a.C + c];
-    m1[j] = (float)(chan[c] / count);
-    m2[j] = (float)(chan[a.C + c] / count);
-  }
+  lds8_s(prm + c0, P.mean);
+  lds8_s(prm + W8 + c0, P.istd);
+  lds8_s(prm + 2 * W8 + c0, P.pm);
+  lds8_s(prm + 3 * W8 + c0, P.pa);
+  lds8_s(prm + 4 * W8 + c0, vg);
+  lds8_s(prm + 5 * W8 + c0, m1);
+  lds8_s(prm + 6 * W8 + c0, m2);
   if (a.up2) bwd_dx_body<DXU1 / 2, 4>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
   else bwd_dx_body<DXU1, 1>(a, dt, lddt, dx, lddx, ppc, P, vg, m1, m2, n, c0, nv, row, rows, q1);
 }
@@ -724,6 +751,9 @@ bool vec_ok(const eegan_bnmod_desc* d, int ld, const void* p, const char* what) 
   return true;
 }
 
+// the forward's staged channel parameters (stage_params)
+size_t fwd_shm(const eegan_bnmod_desc* d) { return 4 * ((d->C + 7) / 8) * 8 * sizeof(float); }
+
 int bwd_chunks(const eegan_bnmod_desc* d, int& ppc) {
   const long HWo = (long)(d->H << d->up2) * (d->W << d->up2);
   // aim at ~1024 blocks overall, >= 64 pixels each
@@ -783,9 +813,9 @@ int eegan_bnmod_fwd(const eegan_bnmod_desc* d, uint16_t* y, int ldy, hipStream_t
                                 bn_knob("fwd_target", 1536), bn_knob("fwd_prow", 8));
   // pixels whose loads a thread issues before their arithmetic (same results for any count)
   if (bn_knob("fwd_u", FUNR_DEFAULT) >= 4)
-    bnmod_fwd_kernel<false, 4><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, FinArgs{});
+    bnmod_fwd_kernel<false, 4><<<dim3(chunks, d->N), NT, fwd_shm(d), stream>>>(a, y, ldy, ppc, FinArgs{});
   else
-    bnmod_fwd_kernel<false><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, FinArgs{});
+    bnmod_fwd_kernel<false><<<dim3(chunks, d->N), NT, fwd_shm(d), stream>>>(a, y, ldy, ppc, FinArgs{});
   return ee_check_launch("bnmod_fwd");
 }
 
@@ -804,9 +834,9 @@ int eegan_bnmod_fwd_fin(const eegan_bnmod_desc* d, const double* sums, double co
   const FinArgs f{sums, count, sum_scale, eps, momentum, clamp_mode, running_mean, running_var,
                   const_cast<float*>(d->stats)};
   if (bn_knob("fwd_u", FUNR_DEFAULT) >= 4)
-    bnmod_fwd_kernel<true, 4><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, f);
+    bnmod_fwd_kernel<true, 4><<<dim3(chunks, d->N), NT, fwd_shm(d), stream>>>(a, y, ldy, ppc, f);
   else
-    bnmod_fwd_kernel<true><<<dim3(chunks, d->N), NT, 0, stream>>>(a, y, ldy, ppc, f);
+    bnmod_fwd_kernel<true><<<dim3(chunks, d->N), NT, fwd_shm(d), stream>>>(a, y, ldy, ppc, f);
   return ee_check_launch("bnmod_fwd_fin");
 }
 
@@ -829,7 +859,7 @@ int eegan_bnmod_bwd(const eegan_bnmod_desc* d, const uint16_t* dt, int lddt, flo
     return -22;
   }
   const int rows = NT / C8;
-  const size_t shm = (rows * C8 + rows * (4 * C8 * 8 + 1)) * sizeof(float);
+  const size_t shm = (4 * C8 * 8 + rows * C8 + rows * (4 * C8 * 8 + 1)) * sizeof(float);
   dim3 grid(chunks, d->N);
   // pixels per thread with their loads in flight together; the per-thread pixel order, hence
   // every partial sum, is the same for any count
@@ -855,10 +885,11 @@ int eegan_bnmod_bwd_dx(const eegan_bnmod_desc* d, const uint16_t* dt, int lddt, 
   int ppc;
   const int chunks = pix_chunks(d->N, (long)d->H * d->W, d->C, ppc, bn_knob("dx_target", 2048),
                                 bn_knob("dx_prow", 8));
+  const size_t dx_shm = 7 * ((d->C + 7) / 8) * 8 * sizeof(float);
   if (bn_knob("dx_u", 4) >= 8)
-    bnmod_bwd_dx_kernel<8><<<dim3(chunks, d->N), NT, 0, stream>>>(a, dt, lddt, chan, count, dx, lddx, ppc);
+    bnmod_bwd_dx_kernel<8><<<dim3(chunks, d->N), NT, dx_shm, stream>>>(a, dt, lddt, chan, count, dx, lddx, ppc);
   else
-    bnmod_bwd_dx_kernel<><<<dim3(chunks, d->N), NT, 0, stream>>>(a, dt, lddt, chan, count, dx, lddx, ppc);
+    bnmod_bwd_dx_kernel<><<<dim3(chunks, d->N), NT, dx_shm, stream>>>(a, dt, lddt, chan, count, dx, lddx, ppc);
   return ee_check_launch("bnmod_bwd_dx");
 }
 
