@@ -216,8 +216,11 @@ def cpu_baseline(seconds_budget=30.0):
                                                                        len(times), times[-1]), file=sys.stderr,
                   flush=True)
         spread = (max(times) - min(times)) / min(times)
-        warmups[stages] = (warm, spread)
         times.sort()
+        # interquartile spread: one step slowed by another job on the shared host moves
+        # max/min, not the quartiles (nor the median that is reported)
+        q1, q3 = times[len(times) // 4], times[(3 * len(times)) // 4]
+        warmups[stages] = (warm, spread, (q3 - q1) / q1)
         return B / times[len(times) // 2], len(times)
 
     warmups = {}
@@ -240,6 +243,7 @@ def cpu_baseline(seconds_budget=30.0):
                 os.environ.get('OMP_PROC_BIND', 'unset'), os.environ.get('OMP_PLACES', 'unset'),
                 torch.get_num_threads(), torch.get_num_interop_threads()),
             'timed_spread': round(warmups[3][1], 4),
+            'timed_iqr_spread': round(warmups[3][2], 4),
             'c1_stage1': {'value': c1, 'unit': 'images/sec', 'sample': 'C1 stage-1 slice (img_64, Dis64, DAMSM on '
                                                                        'img_64), B=4, median of %d steps after %d '
                                                                        'warm-ups' % (n_c1, warmups[1][0])}}
@@ -510,6 +514,10 @@ def main():
            'replay_depth': StepGraph.DEPTH if use_graph else None,
            'execution': 'hip-graph replay of the captured step' if use_graph else 'eager',
            'roofline': roof}
+    if timer is None:   # --no-timer: no dispatch was timed, so there is no roofline figure to report
+        out['roofline'] = {'kernel': None, 'bound': 'mfma', 'achieved': None, 'peak': MFMA_PEAK_TFLOPS,
+                           'unit': 'TFLOP/s', 'frac': None, 'traffic': None,
+                           'note': 'not measured: --no-timer diagnostic run'}
     if args.config in CEILINGS:
         cm, ch = CEILINGS[args.config]
         out['step_roofline'] = {'img_s_per_gpu': round(value / world, 2), 'mfma_ceiling': cm, 'hbm_ceiling': ch,
