@@ -37,6 +37,15 @@ __device__ __forceinline__ void adam_elem(float& P, float G, float& M, float& V,
 }
 
 template <bool B1ZERO>
+__device__ __forceinline__ void adam4(float4& P, float4 G, float4& M, float4& V, float b1, float b2, float wd,
+                                      float step_size, float bc2_sqrt, float eps) {
+  adam_elem<B1ZERO>(P.x, G.x, M.x, V.x, b1, b2, wd, step_size, bc2_sqrt, eps);
+  adam_elem<B1ZERO>(P.y, G.y, M.y, V.y, b1, b2, wd, step_size, bc2_sqrt, eps);
+  adam_elem<B1ZERO>(P.z, G.z, M.z, V.z, b1, b2, wd, step_size, bc2_sqrt, eps);
+  adam_elem<B1ZERO>(P.w, G.w, M.w, V.w, b1, b2, wd, step_size, bc2_sqrt, eps);
+}
+
+template <bool B1ZERO>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long n, float b1,
                                                    float b2, float lr, float eps, float wd,
@@ -145,7 +154,33 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(float* __restrict__ p, c
   const int tid = threadIdx.x;
   if (j[0] == 1) {   // range job
     const long s0 = j[1] + lb * AP_RANGE, s1 = min(j[1] + j[2], s0 + AP_RANGE);
-    for (long i = s0 + tid; i < s1; i += 256) {
+    long i0 = s0;
+    if ((s0 & 3) == 0) {   // float4 body: a thread's AP_RANGE / 1024 groups, all loads before the arithmetic
+      const long nq = (s1 - s0) >> 2;
+      float4 pp[AP_RANGE / 1024], gg[AP_RANGE / 1024], mm[AP_RANGE / 1024], vv[AP_RANGE / 1024];
+#pragma unroll
+      for (int u = 0; u < AP_RANGE / 1024; ++u) {
+        const long q = tid + u * 256;
+        if (q < nq) {
+          pp[u] = reinterpret_cast<const float4*>(p + s0)[q];
+          gg[u] = reinterpret_cast<const float4*>(g + s0)[q];
+          if (!B1ZERO) mm[u] = reinterpret_cast<const float4*>(m + s0)[q];
+          vv[u] = reinterpret_cast<const float4*>(v + s0)[q];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < AP_RANGE / 1024; ++u) {
+        const long q = tid + u * 256;
+        if (q < nq) {
+          adam4<B1ZERO>(pp[u], gg[u], mm[u], vv[u], b1, b2, wd, step_size, bc2_sqrt, eps);
+          reinterpret_cast<float4*>(p + s0)[q] = pp[u];
+          reinterpret_cast<float4*>(m + s0)[q] = mm[u];
+          reinterpret_cast<float4*>(v + s0)[q] = vv[u];
+        }
+      }
+      i0 = s0 + nq * 4;
+    }
+    for (long i = i0 + tid; i < s1; i += 256) {   // unaligned gaps (< 4 elements) and the tail
       float P = p[i], M = B1ZERO ? 0.f : m[i], V = v[i];
       adam_elem<B1ZERO>(P, g[i], M, V, b1, b2, wd, step_size, bc2_sqrt, eps);
       p[i] = P;
@@ -161,20 +196,56 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(float* __restrict__ p, c
   const int nci = (Cin + AP_T - 1) / AP_T;
   const int it = (int)(lb % nci), tap = (int)((lb / nci) % RS), ct = (int)(lb / ((long)nci * RS));
   const int ci0 = it * AP_T, co0 = ct * AP_T;
-#pragma unroll 4
-  for (int k = 0; k < AP_T * AP_T / 256; ++k) {
-    const int e = k * 256 + tid, r = e / AP_T, c = e % AP_T;   // lanes along ci: 256-B rows
-    float P = 0.f;
-    if (co0 + r < Cout && ci0 + c < Cin) {
-      const long i = off + ((long)(co0 + r) * RS + tap) * Cin + ci0 + c;
-      P = p[i];
-      float M = B1ZERO ? 0.f : m[i], V = v[i];
-      adam_elem<B1ZERO>(P, g[i], M, V, b1, b2, wd, step_size, bc2_sqrt, eps);
-      p[i] = P;
-      m[i] = M;
-      v[i] = V;
+  if ((Cin & 3) == 0) {
+    // float4 along ci (offsets of the flat buffer's views are multiples of 4): 16 lanes per
+    // 256-B row, a thread's four groups' loads issued before their arithmetic
+    constexpr int NQ = AP_T * AP_T / 4 / 256;
+    float4 pp[NQ], gg[NQ], mm[NQ], vv[NQ];
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) {
+      const int e = u * 256 + tid, r = e / (AP_T / 4), c = 4 * (e % (AP_T / 4));
+      if (co0 + r < Cout && ci0 + c < Cin) {
+        const long i = off + ((long)(co0 + r) * RS + tap) * Cin + ci0 + c;
+        pp[u] = *reinterpret_cast<const float4*>(p + i);
+        gg[u] = *reinterpret_cast<const float4*>(g + i);
+        if (!B1ZERO) mm[u] = *reinterpret_cast<const float4*>(m + i);
+        vv[u] = *reinterpret_cast<const float4*>(v + i);
+      }
     }
-    buf[r * (AP_T + 1) + c] = P;
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) {
+      const int e = u * 256 + tid, r = e / (AP_T / 4), c = 4 * (e % (AP_T / 4));
+      float4 P4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (co0 + r < Cout && ci0 + c < Cin) {
+        const long i = off + ((long)(co0 + r) * RS + tap) * Cin + ci0 + c;
+        adam4<B1ZERO>(pp[u], gg[u], mm[u], vv[u], b1, b2, wd, step_size, bc2_sqrt, eps);
+        *reinterpret_cast<float4*>(p + i) = pp[u];
+        *reinterpret_cast<float4*>(m + i) = mm[u];
+        *reinterpret_cast<float4*>(v + i) = vv[u];
+        P4 = pp[u];
+      }
+      float* b = buf + r * (AP_T + 1) + c;
+      b[0] = P4.x;
+      b[1] = P4.y;
+      b[2] = P4.z;
+      b[3] = P4.w;
+    }
+  } else {
+#pragma unroll 4
+    for (int k = 0; k < AP_T * AP_T / 256; ++k) {
+      const int e = k * 256 + tid, r = e / AP_T, c = e % AP_T;   // lanes along ci: 256-B rows
+      float P = 0.f;
+      if (co0 + r < Cout && ci0 + c < Cin) {
+        const long i = off + ((long)(co0 + r) * RS + tap) * Cin + ci0 + c;
+        P = p[i];
+        float M = B1ZERO ? 0.f : m[i], V = v[i];
+        adam_elem<B1ZERO>(P, g[i], M, V, b1, b2, wd, step_size, bc2_sqrt, eps);
+        p[i] = P;
+        m[i] = M;
+        v[i] = V;
+      }
+      buf[r * (AP_T + 1) + c] = P;
+    }
   }
   __syncthreads();
   if (fwd) {   // rows co < Cout, this tap's channel run [0, Cgp(Cin)): pairs along ci
