@@ -3388,7 +3388,10 @@ Plan plan_igemm(const ConvArgs& a, int Pc_max) {
   // throughput objective (eegan_conv_desc.plan = 1, a stream beside the critical chain):
   // a smaller grid target -- larger tiles, and no split-K partials / reduce launch once
   // the grid reaches it
-  const int target = a.tp ? knob("tp_target", 128) : knob("target", 512);
+  // 1024 (four workgroups per CU) over 512: +0.6 / +0.7 % in-process on the replayed step
+  // (profiles/r06n_target_ab.txt; 1536 / 2048 -0.1 %) -- the small-grid 3x3 launches
+  // (512-channel 16^2, 256-channel 8^2 ...) are latency-bound per K step, two splits halve that
+  const int target = a.tp ? knob("tp_target", 128) : knob("target", 1024);
   const int mink = knob("mink", 16);
   const int small_co = knob("smallco", 1);
   const int rows = a.Mrows;
